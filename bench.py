@@ -1,0 +1,243 @@
+"""Headline benchmark: 1 query x 31 rotations x N templates, masked Hamming
+(Template path) with fused min/argmin, on N GPUs (one process per GPU).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--n-per-gpu T]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+
+A step = one search of the query against every resident template on every
+rank (the kernel + the partials reduce) plus, for N > 1, the RCCL all-gather
+of the per-shard minima and their merge.  The database is synthetic (the
+DESIGN.md §5 generator, uniform random pattern and mask bits as the
+reference's rng.gen::<Template>()), generated on each GPU so that shard k
+holds global templates [k*T, (k+1)*T) — inputs are resident in HBM before
+the timed region.  A rotated, lightly perturbed copy of the query is planted
+at a known global index; every step's result is checked against it.
+"""
+import argparse
+import ctypes
+import json
+import os
+import pathlib
+import subprocess
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = pathlib.Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "mpc-iris-code_amd"))
+
+import iris_hip as ih  # noqa: E402
+
+METRIC = "template comparisons/sec (query×rotations×DB) + % HBM roofline, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
+HBM_MEASURED_GBS = 6290.0    # MI355X_MICROARCH.md: float4 copy
+VALU_PEAK_OPS = 256 * 4 * 32 * 2.4e9   # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz lane-ops/s
+BYTES_PER_TEMPLATE = 3200    # pattern + mask planes, read once per query
+VALU_OPS_PER_TEMPLATE = 400 * 31 * 4   # words x rotations x (and, bitop3, 2x bcnt)
+ROT = 31
+SEED = 20251015
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--n-per-gpu", type=int, default=10_000_000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    return ap.parse_args()
+
+
+def planted_record(query, rotation):
+    p = ih.Bits(query[:200]).rotated(rotation).limbs.copy()
+    m = ih.Bits(query[200:]).rotated(rotation).limbs
+    p[7] ^= np.uint64(0x00FF00FF00FF00FF)  # 32 flipped bits
+    return np.concatenate([p, m])
+
+
+def cpu_baseline(seconds):
+    """The oracle's engine-style CPU path (test infrastructure), compiled for
+    this host, timed on a bounded sample of the same workload."""
+    from oracle import oracle_c as oc
+
+    threads = min(16, os.cpu_count() or 1)
+    path = pathlib.Path(tempfile.gettempdir()) / f"liboracle_native_{os.getpid()}.so"
+    try:
+        oc.build(path, march="native")
+        lib = str(path)
+    except Exception:
+        lib = None  # fall back to the prebuilt x86-64-v3 oracle
+    oc_lib = oc.load(lib) if lib else oc.load()
+    query = oc.gen_templates(SEED + 1, 0, 1)[0]
+
+    def run(n):
+        db = oc.gen_templates(SEED, 0, n)
+        out = np.empty(n, np.float64)
+        t0 = time.perf_counter()
+        oc_lib.orc_template_distances_batch(oc._p(query), oc._p(db), n, oc._p(out), threads)
+        d = np.zeros(1, np.float64)
+        i = np.zeros(1, np.uint64)
+        oc_lib.orc_argmin(oc._p(out), n, oc._p(d), oc._p(i))  # resolver aggregation, src/main.rs:616-621
+        return time.perf_counter() - t0
+
+    probe = 40_000
+    t = run(probe)
+    n = int(min(2_000_000, max(probe, probe * seconds / max(t, 1e-6))))
+    t = run(n)
+    try:
+        model = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
+    except Exception:
+        model = "unknown"
+    return {
+        "value": ROT * n / t, "unit": "template comparisons/s", "cores": threads, "kind": "port",
+        "sample": f"{n} templates x 31 rotations, 1 query, distances + argmin, {t:.2f} s, "
+                  f"{threads} threads on {model}, gcc -O3 -march=native oracle/iris_oracle.c",
+    }
+
+
+def load_traffic(n_per_launch):
+    """HBM bytes per launch of the search kernel from the committed PMC run
+    (profiles/*pmc*.json), scaled to this launch size; None if absent."""
+    for p in sorted((ROOT / "profiles").glob("*pmc*.json"), reverse=True):
+        try:
+            j = json.loads(p.read_text())
+            return j["hbm_bytes_per_template"] * n_per_launch, p.name
+        except Exception:
+            continue
+    return None, None
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", rank=rank, world_size=world)
+        import iris_dist
+
+    n = args.n_per_gpu
+    lo = rank * n
+    total = n * world
+    dev = ih.Device(local)
+    db = ih.Database(dev, ih.KIND_TEMPLATES, n)
+    t0 = time.time()
+    db.generate(n, SEED, global_index0=lo)
+    gen_s = time.time() - t0
+
+    from oracle import oracle_c as oc  # query/plant construction only (host data)
+
+    query = oc.gen_templates(SEED + 1, 0, 1)[0]
+    plant_global = total * 3 // 4 + 12345
+    plant_rot = 9
+    if lo <= plant_global < lo + n:
+        db.write(plant_global - lo, planted_record(query, plant_rot)[None, :])
+    eng = ih.TemplateEngine(dev, query)
+
+    def sync_all():
+        if dist is not None:
+            import torch
+
+            torch.cuda.synchronize()
+            dist.barrier()
+            torch.cuda.synchronize()
+        else:
+            dev.synchronize()
+
+    def step():
+        m = eng.search(db, index_base=lo)
+        if dist is not None:
+            m = iris_dist.allgather_merge(m, device=f"cuda:{local}")
+        return m
+
+    for _ in range(args.warmup):
+        m = step()
+    dev.reset_stats()
+    dev.set_profiling(True)
+    sync_all()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        m = step()
+    sync_all()
+    elapsed = time.perf_counter() - t0
+    dev.set_profiling(False)
+    if dist is not None:
+        import torch
+
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    ok = m.index == plant_global and m.rotation == plant_rot
+    launches, kms, items = dev.kernel_stats("template_search")
+    _, rms, _ = dev.kernel_stats("reduce")
+    avg_ms = kms / max(1, launches)
+    achieved = BYTES_PER_TEMPLATE * n / (avg_ms * 1e-3) / 1e9
+    traffic, traffic_src = load_traffic(n)
+    ms_per_step = elapsed / args.steps * 1e3
+    value = ROT * total / (elapsed / args.steps)
+
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                cpu = cpu_baseline(args.cpu_seconds)
+            except Exception as ex:  # reported, never fatal
+                cpu = {"value": None, "error": str(ex)}
+        line = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "template comparisons/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic (on-device counter-based generator, uniform random pattern+mask bits; planted known answer)",
+            "config": {
+                "workload": "1 query x 31 rotations x N templates, Template masked Hamming + fused min/argmin (BASELINE configs[1] at N=1)",
+                "templates_per_gpu": n, "total_templates": total, "queries": 1, "rotations": ROT,
+                "bytes_per_template": BYTES_PER_TEMPLATE, "parallelism": f"db-shard x{world}",
+            },
+            "roofline": {
+                "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+            },
+            "kernel": {
+                "name": "template_kernel<MODE_SEARCH>", "avg_ms": avg_ms, "launches": launches,
+                "reduce_avg_ms": rms / max(1, launches),
+                "frac_of_measured_hbm": achieved / HBM_MEASURED_GBS,
+                "valu_frac": VALU_OPS_PER_TEMPLATE * n / (avg_ms * 1e-3) / VALU_PEAK_OPS,
+                "traffic_source": traffic_src,
+            },
+            "cpu_baseline": cpu,
+            "check": {"planted_index": plant_global, "found_index": int(m.index), "rotation": int(m.rotation),
+                      "distance": m.distance, "ok": bool(ok)},
+            "setup": {"generate_s": gen_s},
+        }
+        print(json.dumps(line))
+    eng.close()
+    db.close()
+    dev.close()
+    if dist is not None:
+        dist.destroy_process_group()
+    if not ok:
+        sys.exit(3)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,191 @@
+/*
+ * iris_hip.h — C ABI of the MI355X-native masked-Hamming iris-matching engine.
+ *
+ * This is the drop-in boundary for the hot path of recmo/mpc-iris-code
+ * (reference v0.8.0).  Every entry point names the reference interface it
+ * replaces (path:line inside the reference repository).  The Rust-side
+ * binding a maintainer would add (`src/arch/hip.rs`) is in INTEGRATION.md.
+ *
+ * Conventions
+ *  - Plain pointers and sizes only.  Host buffers are owned by the caller;
+ *    device buffers are owned by the library behind opaque handles.
+ *  - Every function returns an int status: 0 = ok, < 0 = error.  The message
+ *    of the last error on the calling thread is returned by iris_last_error().
+ *    (The reference panics on `assert_eq!(out.len(), db.len())`,
+ *    src/lib.rs:43,70; the Rust shim maps IRIS_E_ARG back to that panic.)
+ *  - All calls are blocking: when they return, host outputs are filled, as the
+ *    reference's synchronous `batch_process` (src/lib.rs:42,69).
+ *  - Handles are thread-safe: calls on one device are serialised internally
+ *    (the reference engines are `Sync` and shared by rayon workers).
+ *  - Record layouts are the reference's in-memory / on-disk layouts
+ *    (bytemuck views, little-endian):
+ *      Bits        = uint64_t[200]            (src/bits.rs:13-15)      1600 B
+ *      EncodedBits = uint16_t[12800]          (src/encoded_bits.rs:13-15) 25600 B
+ *      Template    = { Bits pattern; Bits mask; } (src/template.rs:11-29) 3200 B
+ *    On the device the library keeps its own lane-interleaved layout
+ *    (DESIGN.md §3); conversion happens on upload / read-back.
+ */
+#ifndef IRIS_HIP_H
+#define IRIS_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Geometry: src/lib.rs:10-12, src/bits.rs:10-11 */
+#define IRIS_COLS 200
+#define IRIS_ROWS 64
+#define IRIS_BITS 12800
+#define IRIS_LIMBS 200
+#define IRIS_ROTATIONS 31   /* r = k - 15, k = 0..30 (src/lib.rs:34,61) */
+#define IRIS_MAX_ROTATION 15
+
+/* Status codes */
+#define IRIS_OK 0
+#define IRIS_E_ARG (-1)       /* bad argument / length mismatch            */
+#define IRIS_E_HIP (-2)       /* HIP runtime error                          */
+#define IRIS_E_NOMEM (-3)     /* device or host allocation failed          */
+#define IRIS_E_NODEV (-4)     /* no usable gfx950 device                    */
+#define IRIS_E_RANGE (-5)     /* index range outside the database          */
+
+/* Database record kinds */
+#define IRIS_KIND_MASKS 1     /* records are Bits (the resolver's masks file, src/main.rs:455-469) */
+#define IRIS_KIND_SHARES 2    /* records are EncodedBits (a participant's share file, src/main.rs:386-400) */
+#define IRIS_KIND_TEMPLATES 3 /* records are Template (plaintext masked Hamming, src/template.rs) */
+
+typedef struct iris_template {
+    uint64_t pattern[IRIS_LIMBS];
+    uint64_t mask[IRIS_LIMBS];
+} iris_template_t;
+
+/* Result of a search: the reference resolver's (min_distance, min_index)
+ * pair (src/main.rs:581-582, 616-621) plus the exact fraction behind it.   */
+typedef struct iris_match {
+    double distance;   /* f64 value, +inf when no template has a valid rotation */
+    uint64_t index;    /* global template index; UINT64_MAX when distance is +inf */
+    uint32_t num;      /* uneq count of the winning rotation                   */
+    uint32_t den;      /* jointly-valid bit count of the winning rotation      */
+    int32_t rotation;  /* winning r in -15..15 (lowest r on ties); 0 if none   */
+    uint32_t reserved;
+} iris_match_t;
+
+typedef struct iris_device iris_device_t;
+typedef struct iris_db iris_db_t;
+typedef struct iris_engine iris_engine_t;
+
+/* ---------------------------------------------------------------- errors */
+const char *iris_last_error(void);
+const char *iris_version(void);
+
+/* --------------------------------------------------------------- devices */
+int iris_device_count(int *count);
+/* Opens a HIP device (must be gfx950).  Owns one non-blocking HIP stream. */
+int iris_device_open(int ordinal, iris_device_t **out);
+int iris_device_close(iris_device_t *dev);
+int iris_device_synchronize(iris_device_t *dev);
+/* The device's stream as a hipStream_t, for callers that order their own work. */
+int iris_device_stream(iris_device_t *dev, void **stream);
+/* Kernel timing with HIP events recorded on the device stream around every
+ * launch of the named kernel family ("template_search", "template_counts",
+ * "masks", "shares", ...).  Disabled by default. */
+int iris_device_set_profiling(iris_device_t *dev, int enabled);
+int iris_device_kernel_stats(iris_device_t *dev, const char *kernel, uint64_t *launches,
+                             double *total_ms, uint64_t *items);
+int iris_device_reset_stats(iris_device_t *dev);
+/* Raw device memory for outputs that stay on the GPU (e.g. per-template distances). */
+int iris_device_alloc(iris_device_t *dev, size_t bytes, void **ptr);
+int iris_device_free(iris_device_t *dev, void *ptr);
+int iris_memcpy_d2h(iris_device_t *dev, void *host, const void *device, size_t bytes);
+
+/* -------------------------------------------------------------- databases
+ * Device-resident database of `kind` records.  Replaces the mmap'd share /
+ * masks files the reference keeps in host memory (src/main.rs:389,458).     */
+int iris_db_create(iris_device_t *dev, int kind, uint64_t capacity, iris_db_t **out);
+int iris_db_destroy(iris_db_t *db);
+int iris_db_len(const iris_db_t *db, uint64_t *len);
+int iris_db_capacity(const iris_db_t *db, uint64_t *cap);
+int iris_db_kind(const iris_db_t *db, int *kind);
+/* Appends n host records (reference layout) at the end. */
+int iris_db_append(iris_db_t *db, const void *records, uint64_t n);
+/* Overwrites records [index, index+n) (must lie inside [0, len]) — grows len if needed. */
+int iris_db_write(iris_db_t *db, uint64_t index, const void *records, uint64_t n);
+/* Reads records [first, first+n) back to the reference layout. */
+int iris_db_read(const iris_db_t *db, uint64_t first, uint64_t n, void *records);
+/* Appends n synthetic records generated on the device by the counter-based
+ * generator of DESIGN.md §5 (template index t = global_index0 + i): uniform
+ * random bits / u16 as the reference's `rng.gen()` (src/bits.rs:95-101,
+ * src/encoded_bits.rs:81-87, src/template.rs:67-74). */
+int iris_db_generate(iris_db_t *db, uint64_t n, uint64_t seed, uint64_t global_index0);
+int iris_db_clear(iris_db_t *db);
+
+/* ---------------------------------------------------------------- engines
+ * MasksEngine::new(&Bits)            src/lib.rs:60-67
+ * DistanceEngine::new(&EncodedBits)  src/lib.rs:33-40
+ * Template engine (query Template vs Template DB; src/template.rs:43-64)
+ * Each builds the 31 rotated query copies once, as the reference does.     */
+int iris_masks_engine_new(iris_device_t *dev, const uint64_t query_mask[IRIS_LIMBS], iris_engine_t **out);
+int iris_distance_engine_new(iris_device_t *dev, const uint16_t query[IRIS_BITS], iris_engine_t **out);
+int iris_template_engine_new(iris_device_t *dev, const iris_template_t *query, iris_engine_t **out);
+int iris_engine_destroy(iris_engine_t *engine);
+
+/* batch_process(&self, out: &mut [[u16; 31]], db: &[T])   src/lib.rs:42-52, 69-79
+ * Masks engine: out[i][k] = dot_bool(rot(query_mask, k-15), db[i])
+ * Distance engine: out[i][k] = dot_u16(rot(query, k-15), db[i])  (mod 2^16)
+ * Device-resident form: processes db records [first, first+n); out is a host
+ * array of n*31 uint16_t.  The engine kind must match the DB kind. */
+int iris_engine_batch_process(iris_engine_t *engine, const iris_db_t *db, uint64_t first, uint64_t n,
+                              uint16_t *out);
+/* Host-slice form with exactly the reference signature: `db` is a host array
+ * of n reference-layout records, `out` a host array of n*31 uint16_t. */
+int iris_engine_batch_process_host(iris_engine_t *engine, const void *db, uint64_t n, uint16_t *out);
+
+/* Template engine, per template and rotation k: num = popcount((qp^ep)&qm&em),
+ * den = popcount(qm&em) with q rotated by k-15 (src/template.rs:49-64).
+ * num_out / den_out: host arrays of n*31 uint16_t (either may be NULL). */
+int iris_template_counts(iris_engine_t *engine, const iris_db_t *db, uint64_t first, uint64_t n,
+                         uint16_t *num_out, uint16_t *den_out);
+/* Template::distance(query, db[i]) for each i (src/template.rs:43-47):
+ * out is a host array of n doubles (bit-exact to the reference). */
+int iris_template_distances(iris_engine_t *engine, const iris_db_t *db, uint64_t first, uint64_t n,
+                            double *out);
+/* Fused search: per-template distance + global min / argmin with the
+ * resolver's strict-< lowest-index rule (src/main.rs:581-621).  Indices in
+ * *out are global: db index + index_base.  dist_out_device (optional, may be
+ * NULL) receives the n per-template distances in DEVICE memory. */
+int iris_template_search(iris_engine_t *engine, const iris_db_t *db, uint64_t first, uint64_t n,
+                         uint64_t index_base, double *dist_out_device, iris_match_t *out);
+
+/* ------------------------------------------------------------ arch plugin
+ * The reference's backend plugin point (src/arch/mod.rs:5):
+ *   dot_bool(&[u64;200], &[u64;200]) -> u16   src/arch/generic.rs:4-9
+ *   dot_u16(&[u16;12800], &[u16;12800]) -> u16 src/arch/generic.rs:11-16
+ * Batched all-pairs form (the criterion shapes of src/arch/mod.rs:29,53):
+ * out[j*na + i] = dot(a[i], b[j]) for i < na, j < nb. */
+int iris_dot_bool_batch(iris_device_t *dev, const uint64_t *a, uint64_t na, const uint64_t *b, uint64_t nb,
+                        uint16_t *out);
+int iris_dot_u16_batch(iris_device_t *dev, const uint16_t *a, uint64_t na, const uint16_t *b, uint64_t nb,
+                       uint16_t *out);
+
+/* ------------------------------------------------- host-side value helpers
+ * CPU implementations of the value-type operations the engines are built
+ * from; they need no GPU. */
+/* Bits::rotated (src/bits.rs:18-29,178-205): out[row,col] = in[row,(col-amount) mod 200] */
+int iris_bits_rotated(const uint64_t in[IRIS_LIMBS], int32_t amount, uint64_t out[IRIS_LIMBS]);
+/* EncodedBits::rotated (src/encoded_bits.rs:40-58) */
+int iris_encoded_rotated(const uint16_t in[IRIS_BITS], int32_t amount, uint16_t out[IRIS_BITS]);
+/* encode(&Template) (src/lib.rs:16-26): mask - 2*(pattern&mask) per bit as u16 */
+int iris_encode(const iris_template_t *t, uint16_t out[IRIS_BITS]);
+/* decode_distance(&[u16;31], &[u16;31]) -> f64 (src/lib.rs:97-107) */
+int iris_decode_distance(const uint16_t distances[IRIS_ROTATIONS], const uint16_t denominators[IRIS_ROTATIONS],
+                         double *out);
+/* Merges per-shard search results into the global one (min fraction, then
+ * lowest index) — the cross-shard step of the resolver's argmin (src/main.rs:616-621). */
+int iris_match_merge(const iris_match_t *records, uint64_t count, iris_match_t *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* IRIS_HIP_H */

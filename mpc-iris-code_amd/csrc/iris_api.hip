@@ -1,0 +1,797 @@
+// iris_api.hip — the C ABI (include/iris_hip.h): devices, device-resident
+// databases, engines, arch plugin entry points and host helpers.
+//
+// Every call is blocking and serialised per device (one HIP stream per
+// device).  Errors never throw across the ABI: they return a negative status
+// and set a thread-local message (iris_last_error).
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+#include <map>
+#include <mutex>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "iris_internal.hpp"
+
+using namespace iris;
+
+// ------------------------------------------------------------------ errors
+
+static thread_local std::string g_err;
+
+static int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHK(x)                                                                                   \
+    do {                                                                                            \
+        hipError_t e_ = (x);                                                                        \
+        if (e_ != hipSuccess) return fail(IRIS_E_HIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+#define CHK(x)                   \
+    do {                         \
+        int rc_ = (x);           \
+        if (rc_ != 0) return rc_; \
+    } while (0)
+
+#define ARG(cond, msg)                                    \
+    do {                                                  \
+        if (!(cond)) return fail(IRIS_E_ARG, (msg));      \
+    } while (0)
+
+// ------------------------------------------------------------------ handles
+
+struct KStat {
+    uint64_t launches = 0, items = 0;
+    double ms = 0;
+};
+
+struct Pending {
+    std::string name;
+    hipEvent_t a, b;
+    uint64_t items;
+};
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+};
+
+struct iris_device {
+    int ordinal = 0;
+    hipStream_t stream = nullptr;
+    std::recursive_mutex mu;
+    bool profiling = false;
+    std::map<std::string, KStat> stats;
+    std::vector<Pending> pending;
+    std::vector<hipEvent_t> event_pool;
+    DevBuf partials, result, staging, out_a, out_b;
+};
+
+struct iris_db {
+    iris_device *dev = nullptr;
+    KindInfo k{};
+    uint64_t len = 0, cap = 0;
+    void *data = nullptr;
+};
+
+struct iris_engine {
+    iris_device *dev = nullptr;
+    int kind = 0;  // IRIS_KIND_* of the DB it runs against
+    void *qtab = nullptr;
+};
+
+namespace {
+
+int set_device(iris_device *d) {
+    HIPCHK(hipSetDevice(d->ordinal));
+    return 0;
+}
+
+int ensure(DevBuf &b, size_t bytes) {
+    if (bytes <= b.cap) return 0;
+    if (b.p) HIPCHK(hipFree(b.p));
+    b.p = nullptr;
+    b.cap = 0;
+    size_t want = std::max(bytes, (size_t)4096);
+    hipError_t e = hipMalloc(&b.p, want);
+    if (e != hipSuccess) return fail(IRIS_E_NOMEM, std::string("hipMalloc workspace: ") + hipGetErrorString(e));
+    b.cap = want;
+    return 0;
+}
+
+hipEvent_t take_event(iris_device *d) {
+    if (!d->event_pool.empty()) {
+        hipEvent_t e = d->event_pool.back();
+        d->event_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+// Runs `launch` on the device stream, bracketed by HIP events when profiling.
+template <class F>
+int timed(iris_device *d, const char *name, uint64_t items, F &&launch) {
+    hipEvent_t a = nullptr, b = nullptr;
+    if (d->profiling) {
+        a = take_event(d);
+        b = take_event(d);
+        if (a && b) HIPCHK(hipEventRecord(a, d->stream));
+    }
+    int rc = launch();
+    if (rc != 0) return fail(IRIS_E_HIP, std::string("kernel launch failed: ") + name + ": " +
+                                             hipGetErrorString(hipGetLastError()));
+    if (d->profiling && a && b) {
+        HIPCHK(hipEventRecord(b, d->stream));
+        d->pending.push_back(Pending{name, a, b, items});
+    }
+    return 0;
+}
+
+// Waits for the stream, then folds recorded kernel times into the stats.
+int sync(iris_device *d) {
+    HIPCHK(hipStreamSynchronize(d->stream));
+    for (auto &p : d->pending) {
+        float ms = 0;
+        HIPCHK(hipEventElapsedTime(&ms, p.a, p.b));
+        KStat &s = d->stats[p.name];
+        s.launches += 1;
+        s.ms += ms;
+        s.items += p.items;
+        d->event_pool.push_back(p.a);
+        d->event_pool.push_back(p.b);
+    }
+    d->pending.clear();
+    return 0;
+}
+
+constexpr size_t kStagingBytes = 256ull << 20;  // H2D/D2H staging per chunk
+
+uint64_t chunk_records(const KindInfo &k) { return std::max<uint64_t>(64, kStagingBytes / k.rec_bytes / 64 * 64); }
+
+int check_kind(int kind) {
+    if (kind != IRIS_KIND_MASKS && kind != IRIS_KIND_SHARES && kind != IRIS_KIND_TEMPLATES)
+        return fail(IRIS_E_ARG, "unknown record kind");
+    return 0;
+}
+
+int db_write_locked(iris_db *db, uint64_t index, const void *records, uint64_t n) {
+    iris_device *d = db->dev;
+    if (index > db->len) return fail(IRIS_E_RANGE, "iris_db_write: index beyond the end of the database");
+    if (n > db->cap - index) return fail(IRIS_E_RANGE, "iris_db_write: database capacity exceeded");
+    if (n == 0) return 0;
+    ARG(records != nullptr, "iris_db_write: records is NULL");
+    const KindInfo &k = db->k;
+    const uint64_t ch = chunk_records(k);
+    CHK(ensure(d->staging, std::min<uint64_t>(n, ch) * k.rec_bytes));
+    for (uint64_t done = 0; done < n; done += ch) {
+        const uint64_t m = std::min<uint64_t>(ch, n - done);
+        HIPCHK(hipMemcpyAsync(d->staging.p, (const char *)records + done * k.rec_bytes, m * k.rec_bytes,
+                              hipMemcpyHostToDevice, d->stream));
+        CHK(timed(d, "pack", m, [&] { return launch_pack(d->stream, k, d->staging.p, db->data, index + done, m); }));
+        CHK(sync(d));  // staging is reused by the next chunk
+    }
+    db->len = std::max(db->len, index + n);
+    return 0;
+}
+
+// A transient device DB holding host records (the host-slice engine forms).
+struct TempDb {
+    iris_db db;
+    ~TempDb() {
+        if (db.data) (void)hipFree(db.data);
+    }
+};
+
+int temp_db(iris_device *d, int kind, uint64_t cap, TempDb &t) {
+    t.db.dev = d;
+    t.db.k = kind_info(kind);
+    t.db.cap = (cap + kLanes - 1) / kLanes * kLanes;
+    t.db.len = 0;
+    const size_t bytes = std::max<uint64_t>(1, t.db.cap / kLanes) * block_bytes(t.db.k);
+    hipError_t e = hipMalloc(&t.db.data, bytes);
+    if (e != hipSuccess) return fail(IRIS_E_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+    HIPCHK(hipMemsetAsync(t.db.data, 0, bytes, d->stream));
+    return 0;
+}
+
+int range_ok(const iris_db *db, uint64_t first, uint64_t n) {
+    if (first > db->len || n > db->len - first) return fail(IRIS_E_RANGE, "record range outside the database");
+    return 0;
+}
+
+// Engine kernel over [first, first+n) of db, u16 [n][31] outputs to host.
+int run_u16_engine(iris_engine *e, const iris_db *db, uint64_t first, uint64_t n, uint16_t *out) {
+    iris_device *d = e->dev;
+    const uint64_t ch = 4ull << 20;
+    CHK(ensure(d->out_a, std::min<uint64_t>(n, ch) * kRot * 2));
+    for (uint64_t done = 0; done < n; done += ch) {
+        const uint64_t m = std::min<uint64_t>(ch, n - done);
+        LaunchRange r{first + done, m};
+        if (e->kind == IRIS_KIND_MASKS)
+            CHK(timed(d, "masks", m, [&] { return launch_masks(d->stream, db->data, e->qtab, r, (uint16_t *)d->out_a.p); }));
+        else
+            CHK(timed(d, "shares", m, [&] { return launch_shares(d->stream, db->data, e->qtab, r, (uint16_t *)d->out_a.p); }));
+        HIPCHK(hipMemcpyAsync(out + done * kRot, d->out_a.p, m * kRot * 2, hipMemcpyDeviceToHost, d->stream));
+        CHK(sync(d));
+    }
+    return 0;
+}
+
+int engine_new(iris_device *dev, int kind, const void *table, size_t bytes, iris_engine **out) {
+    iris_engine *e = new (std::nothrow) iris_engine();
+    if (!e) return fail(IRIS_E_NOMEM, "out of host memory");
+    e->dev = dev;
+    e->kind = kind;
+    hipError_t err = hipMalloc(&e->qtab, bytes);
+    if (err != hipSuccess) {
+        delete e;
+        return fail(IRIS_E_NOMEM, std::string("hipMalloc query table: ") + hipGetErrorString(err));
+    }
+    err = hipMemcpyAsync(e->qtab, table, bytes, hipMemcpyHostToDevice, dev->stream);
+    if (err == hipSuccess) err = hipStreamSynchronize(dev->stream);
+    if (err != hipSuccess) {
+        (void)hipFree(e->qtab);
+        delete e;
+        return fail(IRIS_E_HIP, std::string("upload query table: ") + hipGetErrorString(err));
+    }
+    *out = e;
+    return 0;
+}
+
+double rust_f64_min(double a, double b) {
+    if (isnan(a)) return b;
+    if (isnan(b)) return a;
+    return a < b ? a : b;
+}
+
+}  // namespace
+
+// ================================================================== C ABI
+
+extern "C" {
+
+const char *iris_last_error(void) { return g_err.c_str(); }
+const char *iris_version(void) { return "iris-hip 0.1.0 (gfx950)"; }
+
+int iris_device_count(int *count) {
+    ARG(count, "count is NULL");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) n = 0;
+    *count = n;
+    return 0;
+}
+
+int iris_device_open(int ordinal, iris_device_t **out) {
+    ARG(out, "out is NULL");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(IRIS_E_NODEV, "no HIP device visible");
+    if (ordinal < 0 || ordinal >= n) return fail(IRIS_E_NODEV, "device ordinal out of range");
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, ordinal));
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(IRIS_E_NODEV, std::string("device is ") + prop.gcnArchName + ", this build targets gfx950");
+    iris_device *d = new (std::nothrow) iris_device();
+    if (!d) return fail(IRIS_E_NOMEM, "out of host memory");
+    d->ordinal = ordinal;
+    hipError_t e = hipSetDevice(ordinal);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete d;
+        return fail(IRIS_E_HIP, std::string("stream create: ") + hipGetErrorString(e));
+    }
+    *out = d;
+    return 0;
+}
+
+int iris_device_close(iris_device_t *d) {
+    if (!d) return 0;
+    {
+        std::lock_guard<std::recursive_mutex> g(d->mu);
+        (void)hipSetDevice(d->ordinal);
+        (void)hipStreamSynchronize(d->stream);
+        for (DevBuf *b : {&d->partials, &d->result, &d->staging, &d->out_a, &d->out_b})
+            if (b->p) (void)hipFree(b->p);
+        for (auto &p : d->pending) {
+            (void)hipEventDestroy(p.a);
+            (void)hipEventDestroy(p.b);
+        }
+        for (auto e : d->event_pool) (void)hipEventDestroy(e);
+        (void)hipStreamDestroy(d->stream);
+    }
+    delete d;
+    return 0;
+}
+
+int iris_device_synchronize(iris_device_t *d) {
+    ARG(d, "device is NULL");
+    std::lock_guard<std::recursive_mutex> g(d->mu);
+    CHK(set_device(d));
+    return sync(d);
+}
+
+int iris_device_stream(iris_device_t *d, void **stream) {
+    ARG(d && stream, "NULL argument");
+    *stream = (void *)d->stream;
+    return 0;
+}
+
+int iris_device_set_profiling(iris_device_t *d, int enabled) {
+    ARG(d, "device is NULL");
+    std::lock_guard<std::recursive_mutex> g(d->mu);
+    d->profiling = enabled != 0;
+    return 0;
+}
+
+int iris_device_kernel_stats(iris_device_t *d, const char *kernel, uint64_t *launches, double *total_ms,
+                             uint64_t *items) {
+    ARG(d && kernel, "NULL argument");
+    std::lock_guard<std::recursive_mutex> g(d->mu);
+    auto it = d->stats.find(kernel);
+    KStat s = it == d->stats.end() ? KStat{} : it->second;
+    if (launches) *launches = s.launches;
+    if (total_ms) *total_ms = s.ms;
+    if (items) *items = s.items;
+    return 0;
+}
+
+int iris_device_reset_stats(iris_device_t *d) {
+    ARG(d, "device is NULL");
+    std::lock_guard<std::recursive_mutex> g(d->mu);
+    d->stats.clear();
+    return 0;
+}
+
+int iris_device_alloc(iris_device_t *d, size_t bytes, void **ptr) {
+    ARG(d && ptr, "NULL argument");
+    std::lock_guard<std::recursive_mutex> g(d->mu);
+    CHK(set_device(d));
+    hipError_t e = hipMalloc(ptr, std::max<size_t>(bytes, 1));
+    if (e != hipSuccess) return fail(IRIS_E_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+    return 0;
+}
+
+int iris_device_free(iris_device_t *d, void *ptr) {
+    ARG(d, "device is NULL");
+    std::lock_guard<std::recursive_mutex> g(d->mu);
+    CHK(set_device(d));
+    if (ptr) HIPCHK(hipFree(ptr));
+    return 0;
+}
+
+int iris_memcpy_d2h(iris_device_t *d, void *host, const void *device, size_t bytes) {
+    ARG(d && (bytes == 0 || (host && device)), "NULL argument");
+    std::lock_guard<std::recursive_mutex> g(d->mu);
+    CHK(set_device(d));
+    HIPCHK(hipMemcpyAsync(host, device, bytes, hipMemcpyDeviceToHost, d->stream));
+    return sync(d);
+}
+
+// ------------------------------------------------------------------ databases
+
+int iris_db_create(iris_device_t *d, int kind, uint64_t capacity, iris_db_t **out) {
+    ARG(d && out, "NULL argument");
+    CHK(check_kind(kind));
+    std::lock_guard<std::recursive_mutex> g(d->mu);
+    CHK(set_device(d));
+    iris_db *db = new (std::nothrow) iris_db();
+    if (!db) return fail(IRIS_E_NOMEM, "out of host memory");
+    db->dev = d;
+    db->k = kind_info(kind);
+    db->cap = (capacity + kLanes - 1) / kLanes * kLanes;
+    const size_t bytes = std::max<uint64_t>(1, db->cap / kLanes) * block_bytes(db->k);
+    hipError_t e = hipMalloc(&db->data, bytes);
+    if (e != hipSuccess) {
+        delete db;
+        return fail(IRIS_E_NOMEM, std::string("hipMalloc database (") + std::to_string(bytes) +
+                                      " B): " + hipGetErrorString(e));
+    }
+    // zeroed padding lanes: a zero mask gives den = 0, i.e. "no candidate"
+    e = hipMemsetAsync(db->data, 0, bytes, d->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(d->stream);
+    if (e != hipSuccess) {
+        (void)hipFree(db->data);
+        delete db;
+        return fail(IRIS_E_HIP, std::string("memset database: ") + hipGetErrorString(e));
+    }
+    *out = db;
+    return 0;
+}
+
+int iris_db_destroy(iris_db_t *db) {
+    if (!db) return 0;
+    {
+        std::lock_guard<std::recursive_mutex> g(db->dev->mu);
+        (void)hipSetDevice(db->dev->ordinal);
+        (void)hipStreamSynchronize(db->dev->stream);
+        if (db->data) (void)hipFree(db->data);
+    }
+    delete db;
+    return 0;
+}
+
+int iris_db_len(const iris_db_t *db, uint64_t *len) {
+    ARG(db && len, "NULL argument");
+    *len = db->len;
+    return 0;
+}
+
+int iris_db_capacity(const iris_db_t *db, uint64_t *cap) {
+    ARG(db && cap, "NULL argument");
+    *cap = db->cap;
+    return 0;
+}
+
+int iris_db_kind(const iris_db_t *db, int *kind) {
+    ARG(db && kind, "NULL argument");
+    *kind = db->k.kind;
+    return 0;
+}
+
+int iris_db_append(iris_db_t *db, const void *records, uint64_t n) {
+    ARG(db, "database is NULL");
+    std::lock_guard<std::recursive_mutex> g(db->dev->mu);
+    CHK(set_device(db->dev));
+    return db_write_locked(db, db->len, records, n);
+}
+
+int iris_db_write(iris_db_t *db, uint64_t index, const void *records, uint64_t n) {
+    ARG(db, "database is NULL");
+    std::lock_guard<std::recursive_mutex> g(db->dev->mu);
+    CHK(set_device(db->dev));
+    return db_write_locked(db, index, records, n);
+}
+
+int iris_db_read(const iris_db_t *db, uint64_t first, uint64_t n, void *records) {
+    ARG(db, "database is NULL");
+    iris_device *d = db->dev;
+    std::lock_guard<std::recursive_mutex> g(d->mu);
+    CHK(set_device(d));
+    CHK(range_ok(db, first, n));
+    if (n == 0) return 0;
+    ARG(records, "records is NULL");
+    const KindInfo &k = db->k;
+    const uint64_t ch = chunk_records(k);
+    CHK(ensure(d->staging, std::min<uint64_t>(n, ch) * k.rec_bytes));
+    for (uint64_t done = 0; done < n; done += ch) {
+        const uint64_t m = std::min<uint64_t>(ch, n - done);
+        CHK(timed(d, "unpack", m, [&] { return launch_unpack(d->stream, k, db->data, d->staging.p, first + done, m); }));
+        HIPCHK(hipMemcpyAsync((char *)records + done * k.rec_bytes, d->staging.p, m * k.rec_bytes,
+                              hipMemcpyDeviceToHost, d->stream));
+        CHK(sync(d));
+    }
+    return 0;
+}
+
+int iris_db_generate(iris_db_t *db, uint64_t n, uint64_t seed, uint64_t global_index0) {
+    ARG(db, "database is NULL");
+    iris_device *d = db->dev;
+    std::lock_guard<std::recursive_mutex> g(d->mu);
+    CHK(set_device(d));
+    if (n > db->cap - db->len) return fail(IRIS_E_RANGE, "iris_db_generate: database capacity exceeded");
+    if (n == 0) return 0;
+    CHK(timed(d, "generate", n, [&] { return launch_generate(d->stream, db->k, db->data, db->len, n, seed, global_index0); }));
+    CHK(sync(d));
+    db->len += n;
+    return 0;
+}
+
+int iris_db_clear(iris_db_t *db) {
+    ARG(db, "database is NULL");
+    std::lock_guard<std::recursive_mutex> g(db->dev->mu);
+    CHK(set_device(db->dev));
+    const size_t bytes = std::max<uint64_t>(1, db->cap / kLanes) * block_bytes(db->k);
+    HIPCHK(hipMemsetAsync(db->data, 0, bytes, db->dev->stream));
+    CHK(sync(db->dev));
+    db->len = 0;
+    return 0;
+}
+
+// ------------------------------------------------------------------ engines
+
+int iris_masks_engine_new(iris_device_t *d, const uint64_t query_mask[IRIS_LIMBS], iris_engine_t **out) {
+    ARG(d && query_mask && out, "NULL argument");
+    std::lock_guard<std::recursive_mutex> g(d->mu);
+    CHK(set_device(d));
+    std::vector<uint32_t> tab((size_t)kPlaneDwords * kSlotTabStride);
+    build_masks_rotations(query_mask, tab.data());
+    return engine_new(d, IRIS_KIND_MASKS, tab.data(), tab.size() * 4, out);
+}
+
+int iris_distance_engine_new(iris_device_t *d, const uint16_t query[IRIS_BITS], iris_engine_t **out) {
+    ARG(d && query && out, "NULL argument");
+    std::lock_guard<std::recursive_mutex> g(d->mu);
+    CHK(set_device(d));
+    std::vector<uint32_t> tab((size_t)kShareDwords * kSlotTabStride);
+    build_shares_rotations(query, tab.data());
+    return engine_new(d, IRIS_KIND_SHARES, tab.data(), tab.size() * 4, out);
+}
+
+int iris_template_engine_new(iris_device_t *d, const iris_template_t *query, iris_engine_t **out) {
+    ARG(d && query && out, "NULL argument");
+    std::lock_guard<std::recursive_mutex> g(d->mu);
+    CHK(set_device(d));
+    std::vector<uint32_t> tab((size_t)kPlaneDwords * kTemplateTabStride);
+    build_template_table(query, tab.data());
+    return engine_new(d, IRIS_KIND_TEMPLATES, tab.data(), tab.size() * 4, out);
+}
+
+int iris_engine_destroy(iris_engine_t *e) {
+    if (!e) return 0;
+    {
+        std::lock_guard<std::recursive_mutex> g(e->dev->mu);
+        (void)hipSetDevice(e->dev->ordinal);
+        (void)hipStreamSynchronize(e->dev->stream);
+        if (e->qtab) (void)hipFree(e->qtab);
+    }
+    delete e;
+    return 0;
+}
+
+int iris_engine_batch_process(iris_engine_t *e, const iris_db_t *db, uint64_t first, uint64_t n, uint16_t *out) {
+    ARG(e && db, "NULL argument");
+    ARG(e->kind == IRIS_KIND_MASKS || e->kind == IRIS_KIND_SHARES, "batch_process needs a masks or distance engine");
+    ARG(db->k.kind == e->kind, "engine kind does not match the database kind");
+    ARG(e->dev == db->dev, "engine and database live on different devices");
+    std::lock_guard<std::recursive_mutex> g(e->dev->mu);
+    CHK(set_device(e->dev));
+    CHK(range_ok(db, first, n));
+    if (n == 0) return 0;
+    ARG(out, "out is NULL");
+    return run_u16_engine(e, db, first, n, out);
+}
+
+int iris_engine_batch_process_host(iris_engine_t *e, const void *records, uint64_t n, uint16_t *out) {
+    ARG(e, "engine is NULL");
+    ARG(e->kind == IRIS_KIND_MASKS || e->kind == IRIS_KIND_SHARES, "batch_process needs a masks or distance engine");
+    iris_device *d = e->dev;
+    std::lock_guard<std::recursive_mutex> g(d->mu);
+    CHK(set_device(d));
+    if (n == 0) return 0;
+    ARG(records && out, "NULL argument");
+    const KindInfo k = kind_info(e->kind);
+    const uint64_t ch = std::min<uint64_t>(n, 1ull << 20 >> (e->kind == IRIS_KIND_SHARES ? 4 : 0));
+    TempDb t;
+    CHK(temp_db(d, e->kind, ch, t));
+    for (uint64_t done = 0; done < n; done += ch) {
+        const uint64_t m = std::min<uint64_t>(ch, n - done);
+        t.db.len = 0;
+        CHK(db_write_locked(&t.db, 0, (const char *)records + done * k.rec_bytes, m));
+        CHK(run_u16_engine(e, &t.db, 0, m, out + done * kRot));
+    }
+    return 0;
+}
+
+static int template_args(iris_engine_t *e, const iris_db_t *db) {
+    ARG(e && db, "NULL argument");
+    ARG(e->kind == IRIS_KIND_TEMPLATES, "not a template engine");
+    ARG(db->k.kind == IRIS_KIND_TEMPLATES, "database does not hold templates");
+    ARG(e->dev == db->dev, "engine and database live on different devices");
+    return 0;
+}
+
+int iris_template_counts(iris_engine_t *e, const iris_db_t *db, uint64_t first, uint64_t n, uint16_t *num_out,
+                         uint16_t *den_out) {
+    CHK(template_args(e, db));
+    iris_device *d = e->dev;
+    std::lock_guard<std::recursive_mutex> g(d->mu);
+    CHK(set_device(d));
+    CHK(range_ok(db, first, n));
+    if (n == 0 || (!num_out && !den_out)) return 0;
+    const uint64_t ch = 4ull << 20;
+    const size_t bytes = std::min<uint64_t>(n, ch) * kRot * 2;
+    CHK(ensure(d->out_a, bytes));
+    CHK(ensure(d->out_b, bytes));
+    for (uint64_t done = 0; done < n; done += ch) {
+        const uint64_t m = std::min<uint64_t>(ch, n - done);
+        LaunchRange r{first + done, m};
+        uint16_t *na = num_out ? (uint16_t *)d->out_a.p : nullptr;
+        uint16_t *da = den_out ? (uint16_t *)d->out_b.p : nullptr;
+        CHK(timed(d, "template_counts", m, [&] { return launch_template_counts(d->stream, db->data, e->qtab, r, na, da); }));
+        if (num_out)
+            HIPCHK(hipMemcpyAsync(num_out + done * kRot, d->out_a.p, m * kRot * 2, hipMemcpyDeviceToHost, d->stream));
+        if (den_out)
+            HIPCHK(hipMemcpyAsync(den_out + done * kRot, d->out_b.p, m * kRot * 2, hipMemcpyDeviceToHost, d->stream));
+        CHK(sync(d));
+    }
+    return 0;
+}
+
+static int search_locked(iris_engine_t *e, const iris_db_t *db, uint64_t first, uint64_t n, uint64_t index_base,
+                         double *dist_dev, iris_match_t *out) {
+    iris_device *d = e->dev;
+    LaunchRange r{first, n};
+    const uint32_t np = search_partials(r);
+    CHK(ensure(d->partials, (size_t)std::max<uint32_t>(np, 1) * sizeof(Partial)));
+    CHK(ensure(d->result, sizeof(Partial)));
+    uint32_t written = 0;
+    CHK(timed(d, "template_search", n, [&] {
+        return launch_template_search(d->stream, db->data, e->qtab, r, dist_dev, (Partial *)d->partials.p, &written);
+    }));
+    Partial res{};
+    if (n > 0) {
+        CHK(timed(d, "reduce", written, [&] { return launch_reduce(d->stream, (Partial *)d->partials.p, written, (Partial *)d->result.p); }));
+        HIPCHK(hipMemcpyAsync(&res, d->result.p, sizeof(Partial), hipMemcpyDeviceToHost, d->stream));
+    }
+    CHK(sync(d));
+    if (out) {
+        if (n == 0 || res.den == 0) {
+            out->distance = INFINITY;
+            out->index = UINT64_MAX;
+            out->num = 0;
+            out->den = 0;
+            out->rotation = 0;
+        } else {
+            out->distance = (double)res.num / (double)res.den;
+            out->index = index_base + first + res.idx;
+            out->num = res.num;
+            out->den = res.den;
+            out->rotation = res.rot - IRIS_MAX_ROTATION;
+        }
+        out->reserved = 0;
+    }
+    return 0;
+}
+
+int iris_template_search(iris_engine_t *e, const iris_db_t *db, uint64_t first, uint64_t n, uint64_t index_base,
+                         double *dist_out_device, iris_match_t *out) {
+    CHK(template_args(e, db));
+    std::lock_guard<std::recursive_mutex> g(e->dev->mu);
+    CHK(set_device(e->dev));
+    CHK(range_ok(db, first, n));
+    ARG(out, "out is NULL");
+    return search_locked(e, db, first, n, index_base, dist_out_device, out);
+}
+
+int iris_template_distances(iris_engine_t *e, const iris_db_t *db, uint64_t first, uint64_t n, double *out) {
+    CHK(template_args(e, db));
+    iris_device *d = e->dev;
+    std::lock_guard<std::recursive_mutex> g(d->mu);
+    CHK(set_device(d));
+    CHK(range_ok(db, first, n));
+    if (n == 0) return 0;
+    ARG(out, "out is NULL");
+    const uint64_t ch = 16ull << 20;
+    CHK(ensure(d->out_a, std::min<uint64_t>(n, ch) * sizeof(double)));
+    for (uint64_t done = 0; done < n; done += ch) {
+        const uint64_t m = std::min<uint64_t>(ch, n - done);
+        iris_match_t ignored;
+        CHK(search_locked(e, db, first + done, m, 0, (double *)d->out_a.p, &ignored));
+        HIPCHK(hipMemcpyAsync(out + done, d->out_a.p, m * sizeof(double), hipMemcpyDeviceToHost, d->stream));
+        CHK(sync(d));
+    }
+    return 0;
+}
+
+// ------------------------------------------------------------------ arch plugin
+
+int iris_dot_bool_batch(iris_device_t *d, const uint64_t *a, uint64_t na, const uint64_t *b, uint64_t nb,
+                        uint16_t *out) {
+    ARG(d, "device is NULL");
+    std::lock_guard<std::recursive_mutex> g(d->mu);
+    CHK(set_device(d));
+    if (na == 0 || nb == 0) return 0;
+    ARG(a && b && out, "NULL argument");
+    TempDb t;
+    CHK(temp_db(d, IRIS_KIND_MASKS, nb, t));
+    CHK(db_write_locked(&t.db, 0, b, nb));
+    std::vector<uint16_t> tmp(nb * kRot);
+    std::vector<uint32_t> tab((size_t)kPlaneDwords * kSlotTabStride);
+    for (uint64_t i0 = 0; i0 < na; i0 += kRot) {
+        const int cnt = (int)std::min<uint64_t>(kRot, na - i0);
+        const uint64_t *ptrs[kRot];
+        for (int k = 0; k < cnt; ++k) ptrs[k] = a + (i0 + k) * IRIS_LIMBS;
+        build_masks_table(ptrs, cnt, tab.data());
+        iris_engine *e = nullptr;
+        CHK(engine_new(d, IRIS_KIND_MASKS, tab.data(), tab.size() * 4, &e));
+        int rc = run_u16_engine(e, &t.db, 0, nb, tmp.data());
+        (void)hipFree(e->qtab);
+        delete e;
+        CHK(rc);
+        for (uint64_t j = 0; j < nb; ++j)
+            for (int k = 0; k < cnt; ++k) out[j * na + i0 + k] = tmp[j * kRot + k];
+    }
+    return 0;
+}
+
+int iris_dot_u16_batch(iris_device_t *d, const uint16_t *a, uint64_t na, const uint16_t *b, uint64_t nb,
+                       uint16_t *out) {
+    ARG(d, "device is NULL");
+    std::lock_guard<std::recursive_mutex> g(d->mu);
+    CHK(set_device(d));
+    if (na == 0 || nb == 0) return 0;
+    ARG(a && b && out, "NULL argument");
+    TempDb t;
+    CHK(temp_db(d, IRIS_KIND_SHARES, nb, t));
+    CHK(db_write_locked(&t.db, 0, b, nb));
+    std::vector<uint16_t> tmp(nb * kRot);
+    std::vector<uint32_t> tab((size_t)kShareDwords * kSlotTabStride);
+    for (uint64_t i0 = 0; i0 < na; i0 += kRot) {
+        const int cnt = (int)std::min<uint64_t>(kRot, na - i0);
+        const uint16_t *ptrs[kRot];
+        for (int k = 0; k < cnt; ++k) ptrs[k] = a + (i0 + k) * IRIS_BITS;
+        build_shares_table(ptrs, cnt, tab.data());
+        iris_engine *e = nullptr;
+        CHK(engine_new(d, IRIS_KIND_SHARES, tab.data(), tab.size() * 4, &e));
+        int rc = run_u16_engine(e, &t.db, 0, nb, tmp.data());
+        (void)hipFree(e->qtab);
+        delete e;
+        CHK(rc);
+        for (uint64_t j = 0; j < nb; ++j)
+            for (int k = 0; k < cnt; ++k) out[j * na + i0 + k] = tmp[j * kRot + k];
+    }
+    return 0;
+}
+
+// ------------------------------------------------------------------ host helpers
+
+int iris_bits_rotated(const uint64_t in[IRIS_LIMBS], int32_t amount, uint64_t out[IRIS_LIMBS]) {
+    ARG(in && out, "NULL argument");
+    bits_rotated(in, amount, out);
+    return 0;
+}
+
+int iris_encoded_rotated(const uint16_t in[IRIS_BITS], int32_t amount, uint16_t out[IRIS_BITS]) {
+    ARG(in && out, "NULL argument");
+    if (in == out) {
+        std::vector<uint16_t> tmp(in, in + IRIS_BITS);
+        encoded_rotated(tmp.data(), amount, out);
+    } else {
+        encoded_rotated(in, amount, out);
+    }
+    return 0;
+}
+
+int iris_encode(const iris_template_t *t, uint16_t out[IRIS_BITS]) {
+    ARG(t && out, "NULL argument");
+    encode_template(t, out);
+    return 0;
+}
+
+int iris_decode_distance(const uint16_t distances[IRIS_ROTATIONS], const uint16_t denominators[IRIS_ROTATIONS],
+                         double *out) {
+    ARG(distances && denominators && out, "NULL argument");
+    double acc = INFINITY;
+    for (int k = 0; k < kRot; ++k) {
+        const uint16_t n = distances[k], dd = denominators[k];
+        const uint16_t uneq = (uint16_t)((uint16_t)(dd - n) / 2);  // src/lib.rs:104
+        acc = rust_f64_min(acc, (double)uneq / (double)dd);        // src/lib.rs:105-106
+    }
+    *out = acc;
+    return 0;
+}
+
+int iris_match_merge(const iris_match_t *recs, uint64_t count, iris_match_t *out) {
+    ARG(out && (count == 0 || recs), "NULL argument");
+    iris_match_t best;
+    best.distance = INFINITY;
+    best.index = UINT64_MAX;
+    best.num = 0;
+    best.den = 0;
+    best.rotation = 0;
+    best.reserved = 0;
+    for (uint64_t i = 0; i < count; ++i) {
+        const iris_match_t &c = recs[i];
+        if (c.den == 0 || c.index == UINT64_MAX) continue;
+        bool take = best.den == 0;
+        if (!take) {
+            const uint64_t l = (uint64_t)c.num * best.den, r = (uint64_t)best.num * c.den;
+            take = l < r || (l == r && c.index < best.index);
+        }
+        if (take) best = c;
+    }
+    *out = best;
+    return 0;
+}
+
+}  // extern "C"

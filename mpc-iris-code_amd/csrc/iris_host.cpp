@@ -1,0 +1,109 @@
+// iris_host.cpp — host-side value-type operations and rotated-query tables.
+//
+// These run once per engine (31 rotations of one query), never per template.
+// Rotation is implemented by its defining formula
+//     rot(b, r)[row, col] = b[row, (col - r) mod 200]
+// (the reference reaches the same permutation with whole-byte rotates plus a
+// carry chain, src/bits.rs:178-205; tests pin the two against each other).
+#include <math.h>
+#include <string.h>
+
+#include "iris_internal.hpp"
+
+namespace iris {
+
+static inline int wrap_col(int c) {
+    c %= IRIS_COLS;
+    return c < 0 ? c + IRIS_COLS : c;
+}
+
+static inline int get_bit(const uint64_t *b, int i) { return (int)((b[i >> 6] >> (i & 63)) & 1u); }
+
+// Bits::rotated (src/bits.rs:18-29)
+void bits_rotated(const uint64_t *in, int amount, uint64_t *out) {
+    uint64_t tmp[IRIS_LIMBS];
+    memset(tmp, 0, sizeof(tmp));
+    for (int row = 0; row < IRIS_ROWS; ++row)
+        for (int col = 0; col < IRIS_COLS; ++col) {
+            const int src = row * IRIS_COLS + wrap_col(col - amount);
+            const int dst = row * IRIS_COLS + col;
+            tmp[dst >> 6] |= (uint64_t)get_bit(in, src) << (dst & 63);
+        }
+    memcpy(out, tmp, sizeof(tmp));
+}
+
+// EncodedBits::rotated (src/encoded_bits.rs:40-58)
+void encoded_rotated(const uint16_t *in, int amount, uint16_t *out) {
+    for (int row = 0; row < IRIS_ROWS; ++row)
+        for (int col = 0; col < IRIS_COLS; ++col)
+            out[row * IRIS_COLS + col] = in[row * IRIS_COLS + wrap_col(col - amount)];
+}
+
+// encode (src/lib.rs:16-26): mask - 2 * (pattern & mask), wrapping u16
+void encode_template(const iris_template_t *t, uint16_t *out) {
+    for (int i = 0; i < IRIS_BITS; ++i) {
+        const int m = get_bit(t->mask, i);
+        const int p = get_bit(t->pattern, i) & m;
+        out[i] = (uint16_t)(m - 2 * p);
+    }
+}
+
+static inline uint32_t dword_of(const uint64_t *limbs, int w) { return (uint32_t)(limbs[w >> 1] >> (32 * (w & 1))); }
+
+// Rotations of DistanceEngine::new / MasksEngine::new (src/lib.rs:33-40, 60-67),
+// k = 0..30 <-> r = k - 15, laid out for the SGPR-operand kernels.
+void build_template_table(const iris_template_t *q, uint32_t *tab) {
+    memset(tab, 0, sizeof(uint32_t) * kPlaneDwords * kTemplateTabStride);
+    for (int k = 0; k < kRot; ++k) {
+        uint64_t m[IRIS_LIMBS], p[IRIS_LIMBS];
+        bits_rotated(q->mask, k - 15, m);
+        bits_rotated(q->pattern, k - 15, p);
+        for (int w = 0; w < kPlaneDwords; ++w) {
+            tab[w * kTemplateTabStride + 2 * k] = dword_of(m, w);
+            tab[w * kTemplateTabStride + 2 * k + 1] = dword_of(p, w);
+        }
+    }
+}
+
+void build_masks_table(const uint64_t *const *vectors, int count, uint32_t *tab) {
+    memset(tab, 0, sizeof(uint32_t) * kPlaneDwords * kSlotTabStride);
+    for (int k = 0; k < count && k < kRot; ++k)
+        for (int w = 0; w < kPlaneDwords; ++w) tab[w * kSlotTabStride + k] = dword_of(vectors[k], w);
+}
+
+void build_shares_table(const uint16_t *const *vectors, int count, uint32_t *tab) {
+    memset(tab, 0, sizeof(uint32_t) * kShareDwords * kSlotTabStride);
+    for (int k = 0; k < count && k < kRot; ++k)
+        for (int d = 0; d < kShareDwords; ++d)
+            tab[d * kSlotTabStride + k] = (uint32_t)vectors[k][2 * d] | ((uint32_t)vectors[k][2 * d + 1] << 16);
+}
+
+void build_masks_rotations(const uint64_t *query, uint32_t *tab) {
+    static thread_local uint64_t rot[kRot][IRIS_LIMBS];
+    const uint64_t *ptrs[kRot];
+    for (int k = 0; k < kRot; ++k) {
+        bits_rotated(query, k - 15, rot[k]);
+        ptrs[k] = rot[k];
+    }
+    build_masks_table(ptrs, kRot, tab);
+}
+
+void build_shares_rotations(const uint16_t *query, uint32_t *tab) {
+    static thread_local uint16_t rot[kRot][IRIS_BITS];
+    const uint16_t *ptrs[kRot];
+    for (int k = 0; k < kRot; ++k) {
+        encoded_rotated(query, k - 15, rot[k]);
+        ptrs[k] = rot[k];
+    }
+    build_shares_table(ptrs, kRot, tab);
+}
+
+bool partial_better(const Partial &a, const Partial &b) {
+    if (a.den == 0) return false;
+    if (b.den == 0) return true;
+    const uint64_t l = (uint64_t)a.num * b.den, r = (uint64_t)b.num * a.den;
+    if (l != r) return l < r;
+    return a.idx < b.idx;
+}
+
+}  // namespace iris

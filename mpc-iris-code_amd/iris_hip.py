@@ -1,0 +1,651 @@
+"""iris_hip — Python mirror of the reference's engine API over the C ABI.
+
+Mirrors recmo/mpc-iris-code (v0.8.0) names and argument meaning:
+
+    reference (Rust)                              here
+    Bits / EncodedBits / Template (value types)   Bits / EncodedBits / Template
+    encode(&Template) -> EncodedBits              encode(template)          src/lib.rs:16-26
+    DistanceEngine::new / batch_process           DistanceEngine            src/lib.rs:28-53
+    MasksEngine::new / batch_process              MasksEngine               src/lib.rs:55-80
+    distances / denominators                      distances / denominators  src/lib.rs:82-94
+    decode_distance                               decode_distance           src/lib.rs:97-107
+    Template::distance / fraction_hamming         TemplateEngine            src/template.rs:43-64
+    arch::dot_bool / arch::dot_u16                dot_bool / dot_u16        src/arch/generic.rs:4-16
+
+Every compute call goes to libiris_hip.so (hand-written gfx950 kernels).  If
+the library or a gfx950 device is missing the calls raise — there is no CPU
+fallback in this module.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import pathlib
+import threading
+
+import numpy as np
+
+HERE = pathlib.Path(__file__).resolve().parent
+LIB_PATH = HERE / "libiris_hip.so"
+
+COLS, ROWS, BITS, LIMBS, ROTATIONS = 200, 64, 12800, 200, 31
+KIND_MASKS, KIND_SHARES, KIND_TEMPLATES = 1, 2, 3
+_REC_DTYPE = {KIND_MASKS: (np.uint64, LIMBS), KIND_SHARES: (np.uint16, BITS), KIND_TEMPLATES: (np.uint64, 2 * LIMBS)}
+
+
+class IrisError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"iris_hip error {code}: {msg}")
+        self.code = code
+
+
+class Match(ctypes.Structure):
+    """iris_match_t: the resolver's (min_distance, min_index) (src/main.rs:581-621)."""
+
+    _fields_ = [("distance", ctypes.c_double), ("index", ctypes.c_uint64), ("num", ctypes.c_uint32),
+                ("den", ctypes.c_uint32), ("rotation", ctypes.c_int32), ("reserved", ctypes.c_uint32)]
+
+    def __repr__(self):
+        return (f"Match(distance={self.distance!r}, index={self.index}, num={self.num}, den={self.den}, "
+                f"rotation={self.rotation})")
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load_library(path=None):
+    """Load libiris_hip.so (fails loudly when it is absent)."""
+    global _lib
+    with _lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = pathlib.Path(path) if path else LIB_PATH
+        if not p.exists():
+            raise IrisError(-4, f"{p} not built: run `make -C {HERE}` (or __graft_entry__.build())")
+        lib = ctypes.CDLL(str(p))
+        P, u64, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int32
+        PP = ctypes.POINTER(ctypes.c_void_p)
+        sig = {
+            "iris_last_error": ([], ctypes.c_char_p),
+            "iris_version": ([], ctypes.c_char_p),
+            "iris_device_count": ([ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
+            "iris_device_open": ([ctypes.c_int, PP], ctypes.c_int),
+            "iris_device_close": ([P], ctypes.c_int),
+            "iris_device_synchronize": ([P], ctypes.c_int),
+            "iris_device_stream": ([P, PP], ctypes.c_int),
+            "iris_device_set_profiling": ([P, ctypes.c_int], ctypes.c_int),
+            "iris_device_kernel_stats": ([P, ctypes.c_char_p, ctypes.POINTER(u64), ctypes.POINTER(ctypes.c_double),
+                                          ctypes.POINTER(u64)], ctypes.c_int),
+            "iris_device_reset_stats": ([P], ctypes.c_int),
+            "iris_device_alloc": ([P, ctypes.c_size_t, PP], ctypes.c_int),
+            "iris_device_free": ([P, P], ctypes.c_int),
+            "iris_memcpy_d2h": ([P, P, P, ctypes.c_size_t], ctypes.c_int),
+            "iris_db_create": ([P, ctypes.c_int, u64, PP], ctypes.c_int),
+            "iris_db_destroy": ([P], ctypes.c_int),
+            "iris_db_len": ([P, ctypes.POINTER(u64)], ctypes.c_int),
+            "iris_db_capacity": ([P, ctypes.POINTER(u64)], ctypes.c_int),
+            "iris_db_kind": ([P, ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
+            "iris_db_append": ([P, P, u64], ctypes.c_int),
+            "iris_db_write": ([P, u64, P, u64], ctypes.c_int),
+            "iris_db_read": ([P, u64, u64, P], ctypes.c_int),
+            "iris_db_generate": ([P, u64, u64, u64], ctypes.c_int),
+            "iris_db_clear": ([P], ctypes.c_int),
+            "iris_masks_engine_new": ([P, P, PP], ctypes.c_int),
+            "iris_distance_engine_new": ([P, P, PP], ctypes.c_int),
+            "iris_template_engine_new": ([P, P, PP], ctypes.c_int),
+            "iris_engine_destroy": ([P], ctypes.c_int),
+            "iris_engine_batch_process": ([P, P, u64, u64, P], ctypes.c_int),
+            "iris_engine_batch_process_host": ([P, P, u64, P], ctypes.c_int),
+            "iris_template_counts": ([P, P, u64, u64, P, P], ctypes.c_int),
+            "iris_template_distances": ([P, P, u64, u64, P], ctypes.c_int),
+            "iris_template_search": ([P, P, u64, u64, u64, P, ctypes.POINTER(Match)], ctypes.c_int),
+            "iris_dot_bool_batch": ([P, P, u64, P, u64, P], ctypes.c_int),
+            "iris_dot_u16_batch": ([P, P, u64, P, u64, P], ctypes.c_int),
+            "iris_bits_rotated": ([P, i32, P], ctypes.c_int),
+            "iris_encoded_rotated": ([P, i32, P], ctypes.c_int),
+            "iris_encode": ([P, P], ctypes.c_int),
+            "iris_decode_distance": ([P, P, ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
+            "iris_match_merge": ([ctypes.POINTER(Match), u64, ctypes.POINTER(Match)], ctypes.c_int),
+        }
+        for name, (args, res) in sig.items():
+            f = getattr(lib, name)
+            f.argtypes = args
+            f.restype = res
+        if path is None:
+            _lib = lib
+        return lib
+
+
+def exported_symbols():
+    return [
+        "iris_last_error", "iris_version", "iris_device_count", "iris_device_open", "iris_device_close",
+        "iris_device_synchronize", "iris_device_stream", "iris_device_set_profiling", "iris_device_kernel_stats",
+        "iris_device_reset_stats", "iris_device_alloc", "iris_device_free", "iris_memcpy_d2h", "iris_db_create",
+        "iris_db_destroy", "iris_db_len", "iris_db_capacity", "iris_db_kind", "iris_db_append", "iris_db_write",
+        "iris_db_read", "iris_db_generate", "iris_db_clear", "iris_masks_engine_new", "iris_distance_engine_new",
+        "iris_template_engine_new", "iris_engine_destroy", "iris_engine_batch_process",
+        "iris_engine_batch_process_host", "iris_template_counts", "iris_template_distances", "iris_template_search",
+        "iris_dot_bool_batch", "iris_dot_u16_batch", "iris_bits_rotated", "iris_encoded_rotated", "iris_encode",
+        "iris_decode_distance", "iris_match_merge",
+    ]
+
+
+def _check(rc):
+    if rc != 0:
+        raise IrisError(rc, load_library().iris_last_error().decode(errors="replace"))
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _c(a, dtype):
+    return np.ascontiguousarray(a, dtype=dtype)
+
+
+# ====================================================================== value types
+
+
+class Bits:
+    """12 800-bit vector, `[u64; 200]` (src/bits.rs:13-15)."""
+
+    __slots__ = ("limbs",)
+
+    def __init__(self, limbs=None):
+        self.limbs = np.zeros(LIMBS, np.uint64) if limbs is None else _c(limbs, np.uint64).reshape(LIMBS).copy()
+
+    @classmethod
+    def random(cls, rng):
+        return cls(rng.integers(0, 2**64, LIMBS, dtype=np.uint64))
+
+    def __getitem__(self, i):  # Index<usize> (src/bits.rs:44-57)
+        if not 0 <= i < BITS:
+            raise IndexError(i)
+        return bool((int(self.limbs[i // 64]) >> (i % 64)) & 1)
+
+    def __eq__(self, other):
+        return isinstance(other, Bits) and bool((self.limbs == other.limbs).all())
+
+    def rotated(self, amount):
+        out = np.empty(LIMBS, np.uint64)
+        _check(load_library().iris_bits_rotated(_ptr(self.limbs), int(amount), _ptr(out)))
+        return Bits(out)
+
+    def count_ones(self):
+        return int(np.unpackbits(self.limbs.view(np.uint8)).sum())
+
+    def __and__(self, other):
+        return Bits(self.limbs & other.limbs)
+
+    def __or__(self, other):
+        return Bits(self.limbs | other.limbs)
+
+    def __xor__(self, other):
+        return Bits(self.limbs ^ other.limbs)
+
+    def __invert__(self):
+        return Bits(~self.limbs)
+
+    def dot(self, other):  # Bits::dot -> arch::dot_bool (src/bits.rs:35-37)
+        return dot_bool(self, other)
+
+    def to_hex(self):  # serde: hex of the LE bytes (src/bits.rs:74-81)
+        return self.limbs.astype("<u8").tobytes().hex()
+
+    @classmethod
+    def from_hex(cls, s):
+        b = bytes.fromhex(s)
+        if len(b) != 1600:
+            raise ValueError("expected 1600 bytes")
+        return cls(np.frombuffer(b, "<u8"))
+
+
+class EncodedBits:
+    """`[u16; 12800]` ring vector (src/encoded_bits.rs:13-15)."""
+
+    __slots__ = ("values",)
+
+    def __init__(self, values=None):
+        self.values = np.zeros(BITS, np.uint16) if values is None else _c(values, np.uint16).reshape(BITS).copy()
+
+    @classmethod
+    def random(cls, rng):
+        return cls(rng.integers(0, 2**16, BITS, dtype=np.uint16))
+
+    @classmethod
+    def from_bits(cls, bits):  # From<&Bits> (src/encoded_bits.rs:75-79)
+        return cls(np.unpackbits(bits.limbs.view(np.uint8), bitorder="little").astype(np.uint16))
+
+    def __eq__(self, other):
+        return isinstance(other, EncodedBits) and bool((self.values == other.values).all())
+
+    def rotated(self, amount):
+        out = np.empty(BITS, np.uint16)
+        _check(load_library().iris_encoded_rotated(_ptr(self.values), int(amount), _ptr(out)))
+        return EncodedBits(out)
+
+    def sum(self):
+        return int(self.values.astype(np.uint64).sum() & 0xFFFF)
+
+    def __add__(self, other):
+        return EncodedBits(self.values + other.values)
+
+    def __sub__(self, other):
+        return EncodedBits(self.values - other.values)
+
+    def __mul__(self, other):
+        return EncodedBits(self.values * other.values)
+
+    def __neg__(self):
+        return EncodedBits(np.uint16(0) - self.values)
+
+    def dot(self, other):  # EncodedBits::dot -> arch::dot_u16 (src/encoded_bits.rs:64-66)
+        return dot_u16(self, other)
+
+    def share(self, n, rng):
+        """n additive shares mod 2^16 (src/encoded_bits.rs:23-38); host-side offline prep."""
+        assert n > 0
+        shares = [EncodedBits.random(rng) for _ in range(n - 1)]
+        acc = np.zeros(BITS, np.uint16)
+        for s in shares:
+            acc = acc + s.values
+        shares.append(EncodedBits(self.values - acc))
+        return shares
+
+
+class Template:
+    """`#[repr(C)] { pattern: Bits, mask: Bits }` (src/template.rs:11-29)."""
+
+    __slots__ = ("pattern", "mask")
+
+    def __init__(self, pattern=None, mask=None):
+        self.pattern = pattern if isinstance(pattern, Bits) else Bits(pattern)
+        self.mask = mask if isinstance(mask, Bits) else Bits(mask)
+
+    @classmethod
+    def random(cls, rng):
+        return cls(Bits.random(rng), Bits.random(rng))
+
+    @classmethod
+    def from_array(cls, a):
+        a = _c(a, np.uint64).reshape(2 * LIMBS)
+        return cls(a[:LIMBS], a[LIMBS:])
+
+    def to_array(self):
+        return np.concatenate([self.pattern.limbs, self.mask.limbs])
+
+    def rotated(self, amount):
+        return Template(self.pattern.rotated(amount), self.mask.rotated(amount))
+
+    def __eq__(self, other):
+        return isinstance(other, Template) and self.pattern == other.pattern and self.mask == other.mask
+
+    def distance(self, other, device=None):
+        """Template::distance (src/template.rs:43-47), on the GPU."""
+        dev = device or default_device()
+        with TemplateEngine(dev, self) as eng:
+            return float(eng.distances_host(other.to_array()[None, :])[0])
+
+
+def encode(template):
+    """encode(&Template) -> EncodedBits (src/lib.rs:16-26)."""
+    t = template.to_array() if isinstance(template, Template) else _c(template, np.uint64)
+    out = np.empty(BITS, np.uint16)
+    _check(load_library().iris_encode(_ptr(_c(t, np.uint64)), _ptr(out)))
+    return EncodedBits(out)
+
+
+def decode_distance(distances, denominators):
+    """decode_distance(&[u16;31], &[u16;31]) -> f64 (src/lib.rs:97-107)."""
+    out = ctypes.c_double()
+    _check(load_library().iris_decode_distance(_ptr(_c(distances, np.uint16)), _ptr(_c(denominators, np.uint16)),
+                                               ctypes.byref(out)))
+    return out.value
+
+
+def merge_matches(matches):
+    """Cross-shard argmin merge (src/main.rs:616-621 semantics)."""
+    arr = (Match * max(1, len(matches)))(*matches) if matches else (Match * 1)()
+    out = Match()
+    _check(load_library().iris_match_merge(arr, len(matches), ctypes.byref(out)))
+    return out
+
+
+# ====================================================================== devices / databases
+
+
+class Device:
+    """One HIP device (gfx950) and its stream."""
+
+    def __init__(self, ordinal=0):
+        lib = load_library()
+        h = ctypes.c_void_p()
+        _check(lib.iris_device_open(int(ordinal), ctypes.byref(h)))
+        self.handle = h
+        self.ordinal = ordinal
+
+    @staticmethod
+    def count():
+        n = ctypes.c_int()
+        _check(load_library().iris_device_count(ctypes.byref(n)))
+        return n.value
+
+    def close(self):
+        if self.handle:
+            load_library().iris_device_close(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def synchronize(self):
+        _check(load_library().iris_device_synchronize(self.handle))
+
+    def stream(self):
+        s = ctypes.c_void_p()
+        _check(load_library().iris_device_stream(self.handle, ctypes.byref(s)))
+        return s.value
+
+    def set_profiling(self, enabled=True):
+        _check(load_library().iris_device_set_profiling(self.handle, 1 if enabled else 0))
+
+    def reset_stats(self):
+        _check(load_library().iris_device_reset_stats(self.handle))
+
+    def kernel_stats(self, name):
+        """-> (launches, total_ms, items) recorded with HIP events on the device stream."""
+        l, ms, it = ctypes.c_uint64(), ctypes.c_double(), ctypes.c_uint64()
+        _check(load_library().iris_device_kernel_stats(self.handle, name.encode(), ctypes.byref(l), ctypes.byref(ms),
+                                                        ctypes.byref(it)))
+        return l.value, ms.value, it.value
+
+    def alloc(self, nbytes):
+        p = ctypes.c_void_p()
+        _check(load_library().iris_device_alloc(self.handle, int(nbytes), ctypes.byref(p)))
+        return p.value
+
+    def free(self, ptr):
+        _check(load_library().iris_device_free(self.handle, ctypes.c_void_p(ptr)))
+
+    def d2h(self, host_array, device_ptr):
+        _check(load_library().iris_memcpy_d2h(self.handle, _ptr(host_array), ctypes.c_void_p(device_ptr),
+                                               host_array.nbytes))
+
+
+_default = None
+
+
+def default_device():
+    global _default
+    if _default is None:
+        _default = Device(0)
+    return _default
+
+
+def _records(kind, records):
+    dt, width = _REC_DTYPE[kind]
+    if isinstance(records, (Bits, EncodedBits, Template)):
+        records = [records]
+    if isinstance(records, (list, tuple)):
+        rows = []
+        for r in records:
+            if isinstance(r, Bits):
+                rows.append(r.limbs)
+            elif isinstance(r, EncodedBits):
+                rows.append(r.values)
+            elif isinstance(r, Template):
+                rows.append(r.to_array())
+            else:
+                rows.append(np.asarray(r))
+        records = np.stack(rows) if rows else np.zeros((0, width), dt)
+    a = _c(records, dt)
+    if a.ndim == 1:
+        a = a.reshape(1, -1)
+    if a.shape[-1] != width:
+        raise IrisError(-1, f"records must have {width} {np.dtype(dt).name} per row, got shape {a.shape}")
+    return a
+
+
+class Database:
+    """Device-resident database (replaces the reference's mmap'd share/masks files)."""
+
+    def __init__(self, device, kind, capacity):
+        self.device = device
+        self.kind = kind
+        h = ctypes.c_void_p()
+        _check(load_library().iris_db_create(device.handle, int(kind), int(capacity), ctypes.byref(h)))
+        self.handle = h
+
+    def close(self):
+        if self.handle:
+            load_library().iris_db_destroy(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __len__(self):
+        n = ctypes.c_uint64()
+        _check(load_library().iris_db_len(self.handle, ctypes.byref(n)))
+        return n.value
+
+    @property
+    def capacity(self):
+        n = ctypes.c_uint64()
+        _check(load_library().iris_db_capacity(self.handle, ctypes.byref(n)))
+        return n.value
+
+    def append(self, records):
+        a = _records(self.kind, records)
+        _check(load_library().iris_db_append(self.handle, _ptr(a), a.shape[0]))
+
+    def write(self, index, records):
+        a = _records(self.kind, records)
+        _check(load_library().iris_db_write(self.handle, int(index), _ptr(a), a.shape[0]))
+
+    def read(self, first, n):
+        dt, width = _REC_DTYPE[self.kind]
+        out = np.empty((n, width), dt)
+        _check(load_library().iris_db_read(self.handle, int(first), int(n), _ptr(out)))
+        return out
+
+    def generate(self, n, seed, global_index0=None):
+        """Append n synthetic records; generator index defaults to the DB position."""
+        g0 = len(self) if global_index0 is None else global_index0
+        _check(load_library().iris_db_generate(self.handle, int(n), int(seed), int(g0)))
+
+    def clear(self):
+        _check(load_library().iris_db_clear(self.handle))
+
+
+# ====================================================================== engines
+
+
+class _Engine:
+    kind = 0
+
+    def close(self):
+        if getattr(self, "handle", None):
+            load_library().iris_engine_destroy(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def batch_process(self, out, db, first=0, n=None):
+        """batch_process(&self, out: &mut [[u16;31]], db: &[T]) (src/lib.rs:42-52, 69-79).
+
+        `db` is a Database (records [first, first+n)) or a host array / list of records.
+        `out` is a [n, 31] uint16 array (filled in place)."""
+        lib = load_library()
+        if out.dtype != np.uint16 or not out.flags["C_CONTIGUOUS"] or out.ndim != 2 or out.shape[1] != ROTATIONS:
+            raise IrisError(-1, "out must be a C-contiguous [n, 31] uint16 array")
+        if isinstance(db, Database):
+            n = (len(db) - first) if n is None else n
+            if out.shape[0] != n:  # assert_eq!(out.len(), db.len()) (src/lib.rs:43,70)
+                raise IrisError(-1, f"assertion `out.len() == db.len()` failed: {out.shape[0]} != {n}")
+            _check(lib.iris_engine_batch_process(self.handle, db.handle, int(first), int(n), _ptr(out)))
+        else:
+            a = _records(self.kind, db)
+            if out.shape[0] != a.shape[0]:
+                raise IrisError(-1, f"assertion `out.len() == db.len()` failed: {out.shape[0]} != {a.shape[0]}")
+            _check(lib.iris_engine_batch_process_host(self.handle, _ptr(a), a.shape[0], _ptr(out)))
+        return out
+
+
+class MasksEngine(_Engine):
+    """MasksEngine (src/lib.rs:55-80): out[k] = dot_bool(rot(query, k-15), entry)."""
+
+    kind = KIND_MASKS
+
+    def __init__(self, device, query):
+        self.device = device
+        q = query.limbs if isinstance(query, Bits) else _c(query, np.uint64)
+        h = ctypes.c_void_p()
+        _check(load_library().iris_masks_engine_new(device.handle, _ptr(_c(q, np.uint64)), ctypes.byref(h)))
+        self.handle = h
+
+
+class DistanceEngine(_Engine):
+    """DistanceEngine (src/lib.rs:28-53): out[k] = dot_u16(rot(query, k-15), entry)."""
+
+    kind = KIND_SHARES
+
+    def __init__(self, device, query):
+        self.device = device
+        q = query.values if isinstance(query, EncodedBits) else _c(query, np.uint16)
+        h = ctypes.c_void_p()
+        _check(load_library().iris_distance_engine_new(device.handle, _ptr(_c(q, np.uint16)), ctypes.byref(h)))
+        self.handle = h
+
+
+class TemplateEngine(_Engine):
+    """Masked fractional Hamming of one query Template against a Template DB
+    (src/template.rs:43-64): counts per rotation, distances, fused argmin."""
+
+    kind = KIND_TEMPLATES
+
+    def __init__(self, device, query):
+        self.device = device
+        q = query.to_array() if isinstance(query, Template) else _c(query, np.uint64)
+        h = ctypes.c_void_p()
+        _check(load_library().iris_template_engine_new(device.handle, _ptr(_c(q, np.uint64)), ctypes.byref(h)))
+        self.handle = h
+
+    def counts(self, db, first=0, n=None):
+        """-> (num [n,31] u16, den [n,31] u16)."""
+        n = (len(db) - first) if n is None else n
+        num = np.empty((n, ROTATIONS), np.uint16)
+        den = np.empty((n, ROTATIONS), np.uint16)
+        _check(load_library().iris_template_counts(self.handle, db.handle, int(first), int(n), _ptr(num), _ptr(den)))
+        return num, den
+
+    def distances(self, db, first=0, n=None):
+        """Template::distance(query, db[i]) for every i -> [n] f64."""
+        n = (len(db) - first) if n is None else n
+        out = np.empty(n, np.float64)
+        _check(load_library().iris_template_distances(self.handle, db.handle, int(first), int(n), _ptr(out)))
+        return out
+
+    def distances_host(self, records):
+        a = _records(KIND_TEMPLATES, records)
+        with Database(self.device, KIND_TEMPLATES, max(1, a.shape[0])) as db:
+            db.append(a)
+            return self.distances(db)
+
+    def search(self, db, first=0, n=None, index_base=0, dist_out_device=None):
+        """Fused min/argmin (src/main.rs:581-621) -> Match."""
+        n = (len(db) - first) if n is None else n
+        m = Match()
+        _check(load_library().iris_template_search(self.handle, db.handle, int(first), int(n), int(index_base),
+                                                   ctypes.c_void_p(dist_out_device or 0), ctypes.byref(m)))
+        return m
+
+
+def distances(query, entry, device=None):
+    """distances(&EncodedBits, &EncodedBits) -> [u16; 31] (src/lib.rs:82-87)."""
+    dev = device or default_device()
+    out = np.empty((1, ROTATIONS), np.uint16)
+    with DistanceEngine(dev, query) as eng:
+        eng.batch_process(out, [entry])
+    return out[0]
+
+
+def denominators(query, entry, device=None):
+    """denominators(&Bits, &Bits) -> [u16; 31] (src/lib.rs:89-94)."""
+    dev = device or default_device()
+    out = np.empty((1, ROTATIONS), np.uint16)
+    with MasksEngine(dev, query) as eng:
+        eng.batch_process(out, [entry])
+    return out[0]
+
+
+# ====================================================================== arch plugin
+
+
+def dot_bool_batch(a, b, device=None):
+    """out[j, i] = dot_bool(a[i], b[j]) (src/arch/generic.rs:4-9)."""
+    dev = device or default_device()
+    a = _records(KIND_MASKS, a)
+    b = _records(KIND_MASKS, b)
+    out = np.empty((b.shape[0], a.shape[0]), np.uint16)
+    _check(load_library().iris_dot_bool_batch(dev.handle, _ptr(a), a.shape[0], _ptr(b), b.shape[0], _ptr(out)))
+    return out
+
+
+def dot_u16_batch(a, b, device=None):
+    """out[j, i] = dot_u16(a[i], b[j]) (src/arch/generic.rs:11-16)."""
+    dev = device or default_device()
+    a = _records(KIND_SHARES, a)
+    b = _records(KIND_SHARES, b)
+    out = np.empty((b.shape[0], a.shape[0]), np.uint16)
+    _check(load_library().iris_dot_u16_batch(dev.handle, _ptr(a), a.shape[0], _ptr(b), b.shape[0], _ptr(out)))
+    return out
+
+
+def dot_bool(a, b, device=None):
+    return int(dot_bool_batch([a], [b], device)[0, 0])
+
+
+def dot_u16(a, b, device=None):
+    return int(dot_u16_batch([a], [b], device)[0, 0])
+
+
+def f64_bits(x):
+    return int(np.float64(x).view(np.uint64))
+
+
+__all__ = [
+    "Bits", "EncodedBits", "Template", "encode", "decode_distance", "distances", "denominators", "MasksEngine",
+    "DistanceEngine", "TemplateEngine", "Device", "Database", "Match", "merge_matches", "dot_bool", "dot_u16",
+    "dot_bool_batch", "dot_u16_batch", "IrisError", "load_library", "KIND_MASKS", "KIND_SHARES", "KIND_TEMPLATES",
+    "ROTATIONS", "BITS", "LIMBS", "COLS", "ROWS",
+]

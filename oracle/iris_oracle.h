@@ -1,0 +1,71 @@
+/*
+ * iris_oracle.h — TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of the reference (recmo/mpc-iris-code v0.8.0) hot path,
+ * used as the parity checker in tests/, in __graft_entry__.smoke() and as the
+ * `cpu_baseline` leg of bench.py.  Nothing in the product (mpc-iris-code_amd/)
+ * links, imports or calls this code.
+ *
+ * Parity status: the reference is Rust and cannot be compiled in this image
+ * (no cargo/rustc), and its real-data fixtures (data/templates.json,
+ * data/distances.json) are git-ignored and absent.  This restatement is
+ * pinned by (a) the reference's own known-answer / property tests, ported in
+ * tests/test_oracle.py (src/bits.rs:213-247, src/encoded_bits.rs:190-236,
+ * src/lib.rs:117-163, src/arch/sve.rs:79-108), and (b) agreement with an
+ * independent numpy restatement (oracle/oracle_np.py) on every committed
+ * golden vector (tests/golden/).
+ */
+#ifndef IRIS_ORACLE_H
+#define IRIS_ORACLE_H
+#include <stdint.h>
+
+#define ORC_COLS 200
+#define ORC_ROWS 64
+#define ORC_BITS 12800
+#define ORC_LIMBS 200
+#define ORC_BYTES_PER_ROW 25
+#define ORC_ROT 31
+
+typedef struct {
+    uint64_t pattern[ORC_LIMBS];
+    uint64_t mask[ORC_LIMBS];
+} orc_template;
+
+/* value types */
+void orc_bits_rotated(const uint64_t in[ORC_LIMBS], int amount, uint64_t out[ORC_LIMBS]);
+void orc_encoded_rotated(const uint16_t in[ORC_BITS], int amount, uint16_t out[ORC_BITS]);
+void orc_encoded_from_bits(const uint64_t in[ORC_LIMBS], uint16_t out[ORC_BITS]);
+void orc_encode(const orc_template *t, uint16_t out[ORC_BITS]);
+
+/* arch kernels */
+uint16_t orc_dot_bool(const uint64_t a[ORC_LIMBS], const uint64_t b[ORC_LIMBS]);
+uint16_t orc_dot_u16(const uint16_t a[ORC_BITS], const uint16_t b[ORC_BITS]);
+
+/* engines (batch_process); out is [n][31] */
+void orc_masks_batch(const uint64_t query[ORC_LIMBS], const uint64_t *db, uint64_t n, uint16_t *out, int threads);
+void orc_distance_batch(const uint16_t query[ORC_BITS], const uint16_t *db, uint64_t n, uint16_t *out, int threads);
+
+/* Template */
+void orc_fraction_hamming_counts(const orc_template *a, const orc_template *b, uint32_t *num, uint32_t *den);
+double orc_fraction_hamming(const orc_template *a, const orc_template *b);
+double orc_template_distance(const orc_template *a, const orc_template *b);
+void orc_template_counts_batch(const orc_template *query, const orc_template *db, uint64_t n, uint16_t *num_out,
+                               uint16_t *den_out, int threads);
+void orc_template_distances_batch(const orc_template *query, const orc_template *db, uint64_t n, double *out,
+                                  int threads);
+
+/* decode + resolver */
+double orc_decode_distance(const uint16_t distances[ORC_ROT], const uint16_t denominators[ORC_ROT]);
+void orc_argmin(const double *dist, uint64_t n, double *min_distance, uint64_t *min_index);
+void orc_resolver_combine(const uint16_t *shares, uint32_t parts, const uint16_t *denoms, uint64_t n,
+                          double *dist_out);
+
+/* synthetic data generator */
+uint64_t orc_gen_limb(uint64_t seed, uint64_t stream, uint64_t ctr);
+void orc_gen_template(uint64_t seed, uint64_t t, orc_template *out);
+void orc_gen_share(uint64_t seed, uint64_t t, uint16_t out[ORC_BITS]);
+void orc_gen_templates(uint64_t seed, uint64_t t0, uint64_t n, orc_template *out);
+void orc_gen_masks(uint64_t seed, uint64_t t0, uint64_t n, uint64_t *out);
+void orc_gen_shares(uint64_t seed, uint64_t t0, uint64_t n, uint16_t *out);
+
+#endif

@@ -1,0 +1,103 @@
+"""CPU: the C-ABI library loads, exports every symbol include/iris_hip.h
+declares, and its host-side helpers (no GPU needed) match the oracle."""
+import ctypes
+import pathlib
+import re
+
+import numpy as np
+import pytest
+
+import iris_hip as ih
+from oracle import oracle_c as oc
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+
+
+def header_symbols():
+    text = (ROOT / "include" / "iris_hip.h").read_text()
+    return sorted(set(re.findall(r"^\s*(?:const char \*|int )\s*(iris_\w+)\s*\(", text, flags=re.M)))
+
+
+def test_header_symbols_exported():
+    lib = ctypes.CDLL(str(ih.LIB_PATH))
+    syms = header_symbols()
+    assert len(syms) >= 35
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert not missing, missing
+    assert sorted(ih.exported_symbols()) == syms
+
+
+def test_version():
+    assert b"gfx950" in ih.load_library().iris_version()
+
+
+def test_no_device_fails_loudly():
+    if ih.Device.count() > 0:
+        pytest.skip("a GPU is visible")
+    with pytest.raises(ih.IrisError):
+        ih.Device(0)
+
+
+def test_bits_rotated_matches_oracle():
+    rng = np.random.default_rng(1)
+    for _ in range(5):
+        b = ih.Bits.random(rng)
+        for r in range(-15, 16):
+            assert (b.rotated(r).limbs == oc.bits_rotated(b.limbs, r)).all()
+            assert b.rotated(r).rotated(-r) == b
+
+
+def test_encoded_rotated_matches_oracle():
+    rng = np.random.default_rng(2)
+    e = ih.EncodedBits.random(rng)
+    for r in range(-15, 16):
+        assert (e.rotated(r).values == oc.encoded_rotated(e.values, r)).all()
+    b = ih.Bits.random(rng)
+    for r in (-15, -1, 3, 15):  # src/encoded_bits.rs:222-236
+        assert ih.EncodedBits.from_bits(b.rotated(r)) == ih.EncodedBits.from_bits(b).rotated(r)
+
+
+def test_encode_matches_oracle(golden):
+    t = ih.Template.from_array(golden["query"])
+    assert (ih.encode(t).values == golden["enc_query"]).all()
+    rng = np.random.default_rng(3)
+    for _ in range(5):
+        t = ih.Template.random(rng)
+        assert (ih.encode(t).values == oc.encode(t.to_array())).all()
+
+
+def test_decode_distance_matches_oracle(golden):
+    rng = np.random.default_rng(4)
+    for _ in range(200):
+        n = rng.integers(0, 2**16, 31, dtype=np.uint16)
+        d = rng.integers(0, 2**16, 31, dtype=np.uint16)
+        if rng.random() < 0.2:
+            d[:] = 0
+        got, want = ih.decode_distance(n, d), oc.decode_distance(n, d)
+        assert np.float64(got).view(np.uint64) == np.float64(want).view(np.uint64)
+    share_sum = golden["share_out"].astype(np.uint64).sum(0).astype(np.uint16)
+    for i in range(share_sum.shape[0]):
+        got = ih.decode_distance(share_sum[i], golden["masks_out"][i])
+        assert np.float64(got).view(np.uint64) == golden["dist_bits"][i]
+
+
+def test_match_merge_rules():
+    M = ih.Match
+    inf = float("inf")
+    recs = [M(inf, 2**64 - 1, 0, 0, 0, 0), M(0.5, 40, 2, 4, 0, 0), M(0.5, 12, 3, 6, 2, 0), M(0.75, 1, 3, 4, 0, 0)]
+    best = ih.merge_matches(recs)
+    assert (best.index, best.num, best.den) == (12, 3, 6)  # equal fraction, lowest index
+    none = ih.merge_matches([M(inf, 2**64 - 1, 0, 0, 0, 0)])
+    assert none.index == 2**64 - 1 and none.distance == inf
+    assert ih.merge_matches([]).index == 2**64 - 1
+
+
+def test_value_types():
+    rng = np.random.default_rng(5)
+    b = ih.Bits.random(rng)
+    assert ih.Bits.from_hex(b.to_hex()) == b
+    for i in (0, 1, 63, 64, 12799):
+        assert b[i] == bool((int(b.limbs[i // 64]) >> (i % 64)) & 1)
+    e = ih.EncodedBits.random(rng)
+    shares = e.share(3, rng)
+    assert (sum((s.values.astype(np.uint64) for s in shares)) & 0xFFFF == e.values).all()

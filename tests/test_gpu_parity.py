@@ -1,0 +1,280 @@
+"""GPU parity: every hot-path entry point of libiris_hip.so (called through the
+C ABI) is compared bit-exactly with the CPU oracle on the same seeded inputs,
+on the committed golden vectors, and — at sizes the oracle cannot cover — via
+size-independent properties (planted known answers, sampled oracle checks)."""
+import numpy as np
+import pytest
+
+import iris_hip as ih
+from oracle import oracle_c as oc
+
+pytestmark = pytest.mark.gpu
+ROT = 31
+SEED = 42
+
+
+def bits_eq(a, b):
+    return (np.asarray(a, np.float64).view(np.uint64) == np.asarray(b, np.float64).view(np.uint64)).all()
+
+
+@pytest.fixture(scope="module")
+def tdb(device):
+    """1000 generated templates (not a multiple of 64)."""
+    db = ih.Database(device, ih.KIND_TEMPLATES, 1000)
+    db.generate(1000, SEED)
+    yield db
+    db.close()
+
+
+# ---------------------------------------------------------------- storage
+
+
+def test_generate_matches_oracle(device, tdb):
+    got = tdb.read(0, 1000)
+    assert (got == oc.gen_templates(SEED, 0, 1000)).all()
+    with ih.Database(device, ih.KIND_MASKS, 200) as m:
+        m.generate(130, SEED, global_index0=500)
+        assert (m.read(0, 130) == oc.gen_masks(SEED, 500, 130)).all()
+    with ih.Database(device, ih.KIND_SHARES, 100) as s:
+        s.generate(70, SEED)
+        assert (s.read(0, 70) == oc.gen_shares(SEED, 0, 70)).all()
+
+
+def test_append_write_read_roundtrip(device):
+    rng = np.random.default_rng(1)
+    recs = rng.integers(0, 2**64, (150, 400), dtype=np.uint64)
+    with ih.Database(device, ih.KIND_TEMPLATES, 300) as db:
+        db.append(recs[:77])
+        db.append(recs[77:])
+        assert len(db) == 150
+        assert (db.read(0, 150) == recs).all()
+        db.write(10, recs[:5])
+        expect = recs.copy()
+        expect[10:15] = recs[:5]
+        assert (db.read(0, 150) == expect).all()
+        assert (db.read(63, 3) == expect[63:66]).all()
+        with pytest.raises(ih.IrisError):
+            db.read(100, 51)
+        with pytest.raises(ih.IrisError):
+            db.write(151, recs[:1])
+
+
+# ---------------------------------------------------------------- Template path
+
+
+def test_template_counts_match_oracle(device, tdb):
+    ref = tdb.read(0, 1000)
+    q = ref[3].copy()
+    q[:200] ^= np.uint64(0x0F0F)  # not an exact DB member
+    with ih.TemplateEngine(device, q) as eng:
+        num, den = eng.counts(tdb)
+        onum, oden = oc.template_counts(q, ref)
+        assert (num == onum).all() and (den == oden).all()
+        # ragged sub-range not aligned to the 64-record blocks
+        num2, den2 = eng.counts(tdb, first=37, n=500)
+        assert (num2 == onum[37:537]).all() and (den2 == oden[37:537]).all()
+
+
+def test_template_distances_and_search(device, tdb):
+    ref = tdb.read(0, 1000)
+    q = oc.gen_templates(SEED + 1, 0, 1)[0]
+    with ih.TemplateEngine(device, q) as eng:
+        d = eng.distances(tdb)
+        od = oc.template_distances(q, ref)
+        assert bits_eq(d, od)
+        m = eng.search(tdb)
+        best, idx = oc.argmin(od)
+        assert m.index == idx and bits_eq(m.distance, best)
+        assert m.den > 0 and bits_eq(m.num / m.den, best)
+        num, den = oc.template_counts(q, ref[idx:idx + 1])
+        assert num[0, m.rotation + 15] == m.num and den[0, m.rotation + 15] == m.den
+        # sub-range + index base
+        m2 = eng.search(tdb, first=100, n=333, index_base=10_000)
+        b2, i2 = oc.argmin(od[100:433])
+        assert m2.index == 10_000 + 100 + i2 and bits_eq(m2.distance, b2)
+
+
+def test_planted_rotated_copies(device):
+    """A rotated, lightly flipped copy of the query is the unique best match."""
+    rng = np.random.default_rng(3)
+    n = 5000
+    with ih.Database(device, ih.KIND_TEMPLATES, n) as db:
+        db.generate(n, 9)
+        q = oc.gen_templates(1234, 0, 1)[0]
+        for pos, r in ((4321, 15), (17, -15), (2500, 0)):
+            p = oc.bits_rotated(q[:200], r)  # entry = rot(q, r): engine rotation r matches
+            mk = oc.bits_rotated(q[200:], r)
+            flips = np.zeros(200, np.uint64)
+            for b in map(int, rng.choice(12800, 25, replace=False)):
+                flips[b // 64] |= np.uint64(1 << (b % 64))
+            db.write(pos, np.concatenate([p ^ flips, mk])[None, :])
+        ref = db.read(0, n)
+        with ih.TemplateEngine(device, q) as eng:
+            m = eng.search(db)
+            best, idx = oc.argmin(oc.template_distances(q, ref))
+            assert m.index == idx and bits_eq(m.distance, best)
+            d = eng.distances(db)
+            for pos, r in ((4321, 15), (17, -15), (2500, 0)):
+                num, den = eng.counts(db, first=pos, n=1)
+                k = int(np.argmin(num[0] / den[0]))
+                assert k - 15 == r and d[pos] < 0.01
+
+
+def test_template_edge_cases(device, golden):
+    q, db_ref = golden["query"], golden["db"]
+    with ih.Database(device, ih.KIND_TEMPLATES, db_ref.shape[0]) as db:
+        db.append(db_ref)
+        with ih.TemplateEngine(device, q) as eng:
+            num, den = eng.counts(db)
+            assert (num == golden["num"]).all() and (den == golden["den"]).all()
+            d = eng.distances(db)
+            assert (d.view(np.uint64) == golden["dist_bits"]).all()
+            m = eng.search(db)
+            assert m.index == int(golden["argmin_index"])
+            assert np.float64(m.distance).view(np.uint64) == golden["argmin_dist_bits"]
+            # empty range
+            e = eng.search(db, first=5, n=0)
+            assert e.index == 2**64 - 1 and e.distance == np.inf
+            assert eng.distances(db, first=0, n=0).shape == (0,)
+            # empty-mask entry only -> +inf, no index (src/main.rs:581-582)
+            empty_pos = int(np.where(np.isinf(d))[0][0])
+            z = eng.search(db, first=empty_pos, n=1)
+            assert z.index == 2**64 - 1 and z.distance == np.inf
+
+
+def test_template_all_invalid_db(device):
+    with ih.Database(device, ih.KIND_TEMPLATES, 130) as db:
+        db.append(np.zeros((130, 400), np.uint64))
+        with ih.TemplateEngine(device, oc.gen_templates(1, 0, 1)[0]) as eng:
+            m = eng.search(db)
+            assert m.index == 2**64 - 1 and m.distance == np.inf
+            assert np.isinf(eng.distances(db)).all()
+
+
+def test_template_distance_value_type(device, golden):
+    a = ih.Template.from_array(golden["query"])
+    b = ih.Template.from_array(golden["db"][0])
+    assert np.float64(a.distance(b, device)).view(np.uint64) == golden["dist_bits"][0]
+    assert a.distance(b, device) == oc.template_distance(golden["query"], golden["db"][0])
+
+
+# ---------------------------------------------------------------- MasksEngine / DistanceEngine
+
+
+def test_masks_engine(device, golden):
+    q, db_ref = golden["query"], golden["db"]
+    with ih.MasksEngine(device, q[200:]) as eng:
+        out = np.empty((db_ref.shape[0], ROT), np.uint16)
+        eng.batch_process(out, db_ref[:, 200:])  # host slice, reference signature
+        assert (out == golden["masks_out"]).all()
+        with ih.Database(device, ih.KIND_MASKS, 2000) as db:
+            db.generate(1999, 5)
+            ref = db.read(0, 1999)
+            out = np.empty((1999, ROT), np.uint16)
+            eng.batch_process(out, db)
+            assert (out == oc.masks_batch(q[200:], ref)).all()
+            out2 = np.empty((100, ROT), np.uint16)
+            eng.batch_process(out2, db, first=1899, n=100)
+            assert (out2 == oc.masks_batch(q[200:], ref[1899:])).all()
+        with pytest.raises(ih.IrisError):  # assert_eq!(out.len(), db.len())
+            eng.batch_process(np.empty((3, ROT), np.uint16), db_ref[:2, 200:])
+
+
+def test_distance_engine(device, golden):
+    enc_q = golden["enc_query"]
+    with ih.DistanceEngine(device, enc_q) as eng:
+        for k in range(3):
+            out = np.empty((golden["shares"].shape[1], ROT), np.uint16)
+            eng.batch_process(out, golden["shares"][k])
+            assert (out == golden["share_out"][k]).all()
+        with ih.Database(device, ih.KIND_SHARES, 300) as db:
+            db.generate(257, 8)
+            ref = db.read(0, 257)
+            out = np.empty((257, ROT), np.uint16)
+            eng.batch_process(out, db)
+            assert (out == oc.distance_batch(enc_q, ref)).all()
+
+
+def test_resolver_decode_matches_template_distance(device, golden):
+    """src/lib.rs:165-193 on synthetic data: shares -> DistanceEngine, masks ->
+    MasksEngine, wrapping sum + decode_distance == Template::distance."""
+    q, db_ref = golden["query"], golden["db"]
+    ns = golden["enc_db"].shape[0]
+    parts = []
+    with ih.DistanceEngine(device, ih.encode(ih.Template.from_array(q))) as eng:
+        for k in range(3):
+            out = np.empty((ns, ROT), np.uint16)
+            eng.batch_process(out, golden["shares"][k])
+            parts.append(out)
+    den = ih.denominators(ih.Bits(q[200:]), ih.Bits(db_ref[0, 200:]), device)
+    assert (den == golden["masks_out"][0]).all()
+    total = (parts[0].astype(np.uint64) + parts[1] + parts[2]).astype(np.uint16)
+    for i in range(ns):
+        got = ih.decode_distance(total[i], golden["masks_out"][i])
+        assert np.float64(got).view(np.uint64) == golden["dist_bits"][i]
+
+
+def test_u16_wraparound(device, golden):
+    assert ih.dot_u16(ih.EncodedBits(golden["wrap_a"]), ih.EncodedBits(golden["wrap_b"]), device) == int(golden["wrap_dot"])
+    ones = np.full(12800, 0xFFFF, np.uint16)
+    assert ih.dot_u16(ones, ones, device) == (12800 % 65536)
+
+
+# ---------------------------------------------------------------- arch plugin (criterion shapes)
+
+
+@pytest.mark.parametrize("na,nb", [(1, 1), (1, 1000), (31, 1000), (40, 70)])
+def test_dot_bool_batch(device, na, nb):
+    rng = np.random.default_rng(na * 7 + nb)
+    a = rng.integers(0, 2**64, (na, 200), dtype=np.uint64)
+    b = rng.integers(0, 2**64, (nb, 200), dtype=np.uint64)
+    out = ih.dot_bool_batch(a, b, device)
+    for j in range(0, nb, max(1, nb // 50)):
+        for i in range(na):
+            assert out[j, i] == oc.dot_bool(a[i], b[j])
+
+
+@pytest.mark.parametrize("na,nb", [(1, 1), (1, 300), (31, 64), (33, 5)])
+def test_dot_u16_batch(device, na, nb):
+    rng = np.random.default_rng(na * 11 + nb)
+    a = rng.integers(0, 2**16, (na, 12800), dtype=np.uint16)
+    b = rng.integers(0, 2**16, (nb, 12800), dtype=np.uint16)
+    out = ih.dot_u16_batch(a, b, device)
+    for j in range(0, nb, max(1, nb // 20)):
+        for i in range(na):
+            assert out[j, i] == oc.dot_u16(a[i], b[j])
+
+
+# ---------------------------------------------------------------- large-size properties
+
+
+def test_large_search_properties(device):
+    """2M templates (6.4 GB): planted known answer + sampled oracle checks of
+    the per-template distances left on the device."""
+    n = 2_000_000
+    rng = np.random.default_rng(99)
+    with ih.Database(device, ih.KIND_TEMPLATES, n) as db:
+        db.generate(n, 2024)
+        q = oc.gen_templates(555, 0, 1)[0]
+        plant = 1_765_432
+        rec = np.concatenate([oc.bits_rotated(q[:200], 4), oc.bits_rotated(q[200:], 4)])
+        rec[5] ^= np.uint64(0xFF)
+        db.write(plant, rec[None, :])
+        with ih.TemplateEngine(device, q) as eng:
+            ptr = device.alloc(n * 8)
+            try:
+                m = eng.search(db, dist_out_device=ptr)
+                dist = np.empty(n, np.float64)
+                device.d2h(dist, ptr)
+            finally:
+                device.free(ptr)
+            assert m.index == plant and m.rotation == 4
+            assert bits_eq(m.distance, dist[plant])
+            assert dist.min() == m.distance and int(np.argmin(dist)) == plant
+            idx = np.sort(rng.choice(n, 3000, replace=False))
+            sample = db.read(0, 1)  # warm
+            for lo in range(0, 3000, 500):
+                ii = idx[lo:lo + 500]
+                recs = np.stack([db.read(int(i), 1)[0] for i in ii])
+                assert bits_eq(dist[ii], oc.template_distances(q, recs))
+            assert sample.shape == (1, 400)
