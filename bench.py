@@ -34,7 +34,10 @@ import iris_hip as ih  # noqa: E402
 METRIC = "template comparisons/sec (query×rotations×DB) + % HBM roofline, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
 HBM_MEASURED_GBS = 6290.0    # MI355X_MICROARCH.md: float4 copy
-VALU_PEAK_OPS = 256 * 4 * 32 * 2.4e9   # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz lane-ops/s
+# integer VALU issue ceiling for v_bcnt/v_bitop3 (16 lanes/clk/SIMD measured, tools/ubench_ops.hip)
+VALU_INT_PEAK_OPS = 256 * 4 * 16 * 2.4e9
+FP4_DENSE_PEAK_MACS = 10e15 / 2            # MI355X_MICROARCH.md: ~10 PF dense fp4
+MFMA_MACS_PER_TEMPLATE = 2 * 12800 * 32    # den + enc products, 32 rotation rows
 BYTES_PER_TEMPLATE = 3200    # pattern + mask planes, read once per query
 VALU_OPS_PER_TEMPLATE = 400 * 31 * 4   # words x rotations x (and, bitop3, 2x bcnt)
 ROT = 31
@@ -49,6 +52,8 @@ def parse():
     ap.add_argument("--n-per-gpu", type=int, default=10_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--layout", choices=["tiles", "lanes"], default="tiles",
+                    help="tiles = fp4-MFMA kernel (default), lanes = VALU popcount kernel")
     return ap.parse_args()
 
 
@@ -131,7 +136,8 @@ def main():
     lo = rank * n
     total = n * world
     dev = ih.Device(local)
-    db = ih.Database(dev, ih.KIND_TEMPLATES, n)
+    layout = ih.LAYOUT_TILES if args.layout == "tiles" else ih.LAYOUT_LANES
+    db = ih.Database(dev, ih.KIND_TEMPLATES, n, layout)
     t0 = time.time()
     db.generate(n, SEED, global_index0=lo)
     gen_s = time.time() - t0
@@ -218,10 +224,15 @@ def main():
                 "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
             },
             "kernel": {
-                "name": "template_kernel<MODE_SEARCH>", "avg_ms": avg_ms, "launches": launches,
+                "name": "template_mfma_kernel<MF_SEARCH> (fp4 MFMA)" if args.layout == "tiles"
+                        else "template_kernel<MODE_SEARCH> (VALU popcount)",
+                "avg_ms": avg_ms, "launches": launches,
                 "reduce_avg_ms": rms / max(1, launches),
                 "frac_of_measured_hbm": achieved / HBM_MEASURED_GBS,
-                "valu_frac": VALU_OPS_PER_TEMPLATE * n / (avg_ms * 1e-3) / VALU_PEAK_OPS,
+                "valu_int_frac": (VALU_OPS_PER_TEMPLATE * n / (avg_ms * 1e-3) / VALU_INT_PEAK_OPS
+                                  if args.layout == "lanes" else None),
+                "mfma_fp4_frac": (MFMA_MACS_PER_TEMPLATE * n / (avg_ms * 1e-3) / FP4_DENSE_PEAK_MACS
+                                  if args.layout == "tiles" else None),
                 "traffic_source": traffic_src,
             },
             "cpu_baseline": cpu,
@@ -236,6 +247,7 @@ def main():
     if dist is not None:
         dist.destroy_process_group()
     if not ok:
+        print(f"planted answer not found: {m}", file=sys.stderr)
         sys.exit(3)
 
 

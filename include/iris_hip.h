@@ -56,6 +56,11 @@ extern "C" {
 #define IRIS_KIND_SHARES 2    /* records are EncodedBits (a participant's share file, src/main.rs:386-400) */
 #define IRIS_KIND_TEMPLATES 3 /* records are Template (plaintext masked Hamming, src/template.rs) */
 
+/* Device layouts of a database (iris_db_create_ex) */
+#define IRIS_LAYOUT_DEFAULT 0 /* TILES for templates, LANES otherwise          */
+#define IRIS_LAYOUT_LANES 1   /* record-per-lane blocks of 64 (VALU kernels)   */
+#define IRIS_LAYOUT_TILES 2   /* 32-record fp4-MFMA tiles (templates only)     */
+
 typedef struct iris_template {
     uint64_t pattern[IRIS_LIMBS];
     uint64_t mask[IRIS_LIMBS];
@@ -104,6 +109,10 @@ int iris_memcpy_d2h(iris_device_t *dev, void *host, const void *device, size_t b
  * Device-resident database of `kind` records.  Replaces the mmap'd share /
  * masks files the reference keeps in host memory (src/main.rs:389,458).     */
 int iris_db_create(iris_device_t *dev, int kind, uint64_t capacity, iris_db_t **out);
+/* As iris_db_create with an explicit device layout (IRIS_LAYOUT_*).  The
+ * layout only selects the kernel family; results are identical. */
+int iris_db_create_ex(iris_device_t *dev, int kind, uint64_t capacity, int layout, iris_db_t **out);
+int iris_db_layout(const iris_db_t *db, int *layout);
 int iris_db_destroy(iris_db_t *db);
 int iris_db_len(const iris_db_t *db, uint64_t *len);
 int iris_db_capacity(const iris_db_t *db, uint64_t *cap);

@@ -84,8 +84,9 @@ struct iris_db {
 
 struct iris_engine {
     iris_device *dev = nullptr;
-    int kind = 0;  // IRIS_KIND_* of the DB it runs against
-    void *qtab = nullptr;
+    int kind = 0;             // IRIS_KIND_* of the DB it runs against
+    void *qtab = nullptr;     // SGPR rotated-query table (LANES kernels)
+    void *qfrag = nullptr;    // fp4 query fragments (TILES kernel, templates only)
 };
 
 namespace {
@@ -194,10 +195,10 @@ struct TempDb {
 
 int temp_db(iris_device *d, int kind, uint64_t cap, TempDb &t) {
     t.db.dev = d;
-    t.db.k = kind_info(kind);
-    t.db.cap = (cap + kLanes - 1) / kLanes * kLanes;
+    t.db.k = kind_info(kind, IRIS_LAYOUT_LANES);
+    t.db.cap = (cap + t.db.k.block - 1) / t.db.k.block * t.db.k.block;
     t.db.len = 0;
-    const size_t bytes = std::max<uint64_t>(1, t.db.cap / kLanes) * block_bytes(t.db.k);
+    const size_t bytes = std::max<uint64_t>(1, t.db.cap / t.db.k.block) * block_bytes(t.db.k);
     hipError_t e = hipMalloc(&t.db.data, bytes);
     if (e != hipSuccess) return fail(IRIS_E_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
     HIPCHK(hipMemsetAsync(t.db.data, 0, bytes, d->stream));
@@ -380,23 +381,30 @@ int iris_memcpy_d2h(iris_device_t *d, void *host, const void *device, size_t byt
 // ------------------------------------------------------------------ databases
 
 int iris_db_create(iris_device_t *d, int kind, uint64_t capacity, iris_db_t **out) {
+    return iris_db_create_ex(d, kind, capacity, IRIS_LAYOUT_DEFAULT, out);
+}
+
+int iris_db_create_ex(iris_device_t *d, int kind, uint64_t capacity, int layout, iris_db_t **out) {
     ARG(d && out, "NULL argument");
     CHK(check_kind(kind));
+    if (layout == IRIS_LAYOUT_DEFAULT) layout = kind == IRIS_KIND_TEMPLATES ? IRIS_LAYOUT_TILES : IRIS_LAYOUT_LANES;
+    ARG(layout == IRIS_LAYOUT_LANES || (layout == IRIS_LAYOUT_TILES && kind == IRIS_KIND_TEMPLATES),
+        "unsupported layout for this record kind");
     std::lock_guard<std::recursive_mutex> g(d->mu);
     CHK(set_device(d));
     iris_db *db = new (std::nothrow) iris_db();
     if (!db) return fail(IRIS_E_NOMEM, "out of host memory");
     db->dev = d;
-    db->k = kind_info(kind);
-    db->cap = (capacity + kLanes - 1) / kLanes * kLanes;
-    const size_t bytes = std::max<uint64_t>(1, db->cap / kLanes) * block_bytes(db->k);
+    db->k = kind_info(kind, layout);
+    db->cap = (capacity + db->k.block - 1) / db->k.block * db->k.block;
+    const size_t bytes = std::max<uint64_t>(1, db->cap / db->k.block) * block_bytes(db->k);
     hipError_t e = hipMalloc(&db->data, bytes);
     if (e != hipSuccess) {
         delete db;
         return fail(IRIS_E_NOMEM, std::string("hipMalloc database (") + std::to_string(bytes) +
                                       " B): " + hipGetErrorString(e));
     }
-    // zeroed padding lanes: a zero mask gives den = 0, i.e. "no candidate"
+    // zeroed padding records: a zero mask gives den = 0, i.e. "no candidate"
     e = hipMemsetAsync(db->data, 0, bytes, d->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(d->stream);
     if (e != hipSuccess) {
@@ -405,6 +413,12 @@ int iris_db_create(iris_device_t *d, int kind, uint64_t capacity, iris_db_t **ou
         return fail(IRIS_E_HIP, std::string("memset database: ") + hipGetErrorString(e));
     }
     *out = db;
+    return 0;
+}
+
+int iris_db_layout(const iris_db_t *db, int *layout) {
+    ARG(db && layout, "NULL argument");
+    *layout = db->k.layout;
     return 0;
 }
 
@@ -490,7 +504,7 @@ int iris_db_clear(iris_db_t *db) {
     ARG(db, "database is NULL");
     std::lock_guard<std::recursive_mutex> g(db->dev->mu);
     CHK(set_device(db->dev));
-    const size_t bytes = std::max<uint64_t>(1, db->cap / kLanes) * block_bytes(db->k);
+    const size_t bytes = std::max<uint64_t>(1, db->cap / db->k.block) * block_bytes(db->k);
     HIPCHK(hipMemsetAsync(db->data, 0, bytes, db->dev->stream));
     CHK(sync(db->dev));
     db->len = 0;
@@ -523,7 +537,19 @@ int iris_template_engine_new(iris_device_t *d, const iris_template_t *query, iri
     CHK(set_device(d));
     std::vector<uint32_t> tab((size_t)kPlaneDwords * kTemplateTabStride);
     build_template_table(query, tab.data());
-    return engine_new(d, IRIS_KIND_TEMPLATES, tab.data(), tab.size() * 4, out);
+    std::vector<uint32_t> frag(kTemplateFragDwords);
+    build_template_frags(query, frag.data());
+    iris_engine *e = nullptr;
+    CHK(engine_new(d, IRIS_KIND_TEMPLATES, tab.data(), tab.size() * 4, &e));
+    hipError_t err = hipMalloc(&e->qfrag, frag.size() * 4);
+    if (err == hipSuccess) err = hipMemcpyAsync(e->qfrag, frag.data(), frag.size() * 4, hipMemcpyHostToDevice, d->stream);
+    if (err == hipSuccess) err = hipStreamSynchronize(d->stream);
+    if (err != hipSuccess) {
+        iris_engine_destroy(e);
+        return fail(IRIS_E_HIP, std::string("upload query fragments: ") + hipGetErrorString(err));
+    }
+    *out = e;
+    return 0;
 }
 
 int iris_engine_destroy(iris_engine_t *e) {
@@ -533,6 +559,7 @@ int iris_engine_destroy(iris_engine_t *e) {
         (void)hipSetDevice(e->dev->ordinal);
         (void)hipStreamSynchronize(e->dev->stream);
         if (e->qtab) (void)hipFree(e->qtab);
+        if (e->qfrag) (void)hipFree(e->qfrag);
     }
     delete e;
     return 0;
@@ -597,7 +624,11 @@ int iris_template_counts(iris_engine_t *e, const iris_db_t *db, uint64_t first, 
         LaunchRange r{first + done, m};
         uint16_t *na = num_out ? (uint16_t *)d->out_a.p : nullptr;
         uint16_t *da = den_out ? (uint16_t *)d->out_b.p : nullptr;
-        CHK(timed(d, "template_counts", m, [&] { return launch_template_counts(d->stream, db->data, e->qtab, r, na, da); }));
+        CHK(timed(d, "template_counts", m, [&] {
+            return db->k.layout == IRIS_LAYOUT_TILES
+                       ? launch_template_mfma_counts(d->stream, db->data, e->qfrag, r, na, da)
+                       : launch_template_counts(d->stream, db->data, e->qtab, r, na, da);
+        }));
         if (num_out)
             HIPCHK(hipMemcpyAsync(num_out + done * kRot, d->out_a.p, m * kRot * 2, hipMemcpyDeviceToHost, d->stream));
         if (den_out)
@@ -611,12 +642,14 @@ static int search_locked(iris_engine_t *e, const iris_db_t *db, uint64_t first, 
                          double *dist_dev, iris_match_t *out) {
     iris_device *d = e->dev;
     LaunchRange r{first, n};
-    const uint32_t np = search_partials(r);
+    const bool tiles = db->k.layout == IRIS_LAYOUT_TILES;
+    const uint32_t np = tiles ? mfma_search_partials(r) : search_partials(r);
     CHK(ensure(d->partials, (size_t)std::max<uint32_t>(np, 1) * sizeof(Partial)));
     CHK(ensure(d->result, sizeof(Partial)));
     uint32_t written = 0;
     CHK(timed(d, "template_search", n, [&] {
-        return launch_template_search(d->stream, db->data, e->qtab, r, dist_dev, (Partial *)d->partials.p, &written);
+        return tiles ? launch_template_mfma_search(d->stream, db->data, e->qfrag, r, dist_dev, (Partial *)d->partials.p, &written)
+                     : launch_template_search(d->stream, db->data, e->qtab, r, dist_dev, (Partial *)d->partials.p, &written);
     }));
     Partial res{};
     if (n > 0) {

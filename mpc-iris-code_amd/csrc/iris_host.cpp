@@ -107,3 +107,29 @@ bool partial_better(const Partial &a, const Partial &b) {
 }
 
 }  // namespace iris
+
+namespace iris {
+
+// Query A-fragments of the fp4 MFMA template kernel (iris_mfma.hip).
+void build_template_frags(const iris_template_t *q, uint32_t *frag) {
+    memset(frag, 0, sizeof(uint32_t) * kTemplateFragDwords);
+    for (int k = 0; k < kRot; ++k) {
+        uint64_t m[IRIS_LIMBS], p[IRIS_LIMBS];
+        bits_rotated(q->mask, k - 15, m);
+        bits_rotated(q->pattern, k - 15, p);
+        for (int c = 0; c < kPlaneDwords / 2; ++c)
+            for (int h = 0; h < 2; ++h) {
+                const int w = 2 * c + h;
+                const uint32_t mw = dword_of(m, w), pw = dword_of(p, w);
+                uint32_t *f = frag + ((size_t)c * 64 + k + 32 * h) * kFragDwords;
+                for (int j = 0; j < 32; ++j) {
+                    const int b = frag_bit(j);
+                    if (!((mw >> b) & 1u)) continue;
+                    const uint32_t code = ((pw >> b) & 1u) ? 0xAu : 0x2u;  // -1.0 / +1.0
+                    f[j / 8] |= code << (4 * (j % 8));
+                }
+            }
+    }
+}
+
+}  // namespace iris

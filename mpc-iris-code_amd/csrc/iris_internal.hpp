@@ -32,29 +32,76 @@ constexpr int kPlaneGroups = kPlaneDwords / 4;   // 100
 constexpr int kShareDwords = IRIS_BITS / 2;      // 6400 (two u16 per dword)
 constexpr int kShareGroups = kShareDwords / 4;   // 1600
 
-// Groups of 16 B per record on the device ("G" index) and planes per group row.
-//   TEMPLATES: G = 2*g + p, p = 0 mask plane, p = 1 pattern plane  (200 groups)
-//   MASKS:     G = g                                               (100 groups)
-//   SHARES:    G = g                                               (1600 groups)
+// Device layouts.
+//  LANES (VALU kernels): blocks of 64 records, one per lane; for each 16-byte
+//    group G of a record the 64 lanes' 16 B are contiguous (1 KiB):
+//      TEMPLATES: G = 2*g + p, p = 0 mask plane, p = 1 pattern plane  (200 groups)
+//      MASKS:     G = g                                               (100 groups)
+//      SHARES:    G = g                                               (1600 groups)
+//  TILES (MFMA kernels, TEMPLATES only): tiles of 32 records.  For chunk pair
+//    g (template bits [128g, 128g+128) of both planes) lane L = t + 32h holds
+//    one uint4 {X0(2g,h), X1(2g,h), X0(2g+1,h), X1(2g+1,h)}: the interleaved
+//    mask/pattern bits of plane dword w = 2c + h (see xpack below), which is
+//    exactly the fp4 B-operand fragment source of lane L for chunk c.
 struct KindInfo {
     int kind;
-    int groups;         // 16-byte groups per record
-    int planes;         // planes interleaved per g
+    int layout;         // IRIS_LAYOUT_LANES or IRIS_LAYOUT_TILES
+    int block;          // records per block (64 lanes or 32-record tiles)
+    int groups;         // 16-byte groups per record (LANES) / per lane (TILES)
+    int planes;         // planes interleaved per g (LANES)
     int rec_dwords;     // dwords per record in the reference layout
     int plane_src[2];   // dword offset of plane p inside the reference record
     size_t rec_bytes;   // bytes per reference record
 };
 
-inline KindInfo kind_info(int kind) {
+inline KindInfo kind_info(int kind, int layout = IRIS_LAYOUT_LANES) {
     switch (kind) {
-    case IRIS_KIND_TEMPLATES: return {kind, 2 * kPlaneGroups, 2, 2 * kPlaneDwords, {kPlaneDwords, 0}, 3200};
-    case IRIS_KIND_MASKS: return {kind, kPlaneGroups, 1, kPlaneDwords, {0, 0}, 1600};
-    case IRIS_KIND_SHARES: return {kind, kShareGroups, 1, kShareDwords, {0, 0}, 25600};
-    default: return {0, 0, 0, 0, {0, 0}, 0};
+    case IRIS_KIND_TEMPLATES:
+        if (layout == IRIS_LAYOUT_TILES) return {kind, layout, 32, kPlaneGroups, 2, 2 * kPlaneDwords, {kPlaneDwords, 0}, 3200};
+        return {kind, IRIS_LAYOUT_LANES, 64, 2 * kPlaneGroups, 2, 2 * kPlaneDwords, {kPlaneDwords, 0}, 3200};
+    case IRIS_KIND_MASKS: return {kind, IRIS_LAYOUT_LANES, 64, kPlaneGroups, 1, kPlaneDwords, {0, 0}, 1600};
+    case IRIS_KIND_SHARES: return {kind, IRIS_LAYOUT_LANES, 64, kShareGroups, 1, kShareDwords, {0, 0}, 25600};
+    default: return {0, 0, 0, 0, 0, 0, {0, 0}, 0};
     }
 }
 
-inline size_t block_bytes(const KindInfo &k) { return (size_t)k.groups * kLanes * 16; }
+inline size_t block_bytes(const KindInfo &k) { return (size_t)k.block * k.rec_bytes; }
+
+// TILES interleave of 16 mask bits and 16 pattern bits into one dword:
+//   nibble p: bit0 = em[2p+1], bit1 = em[2p], bit2 = ep[2p+1], bit3 = ep[2p]
+// so that (x & 0xAAAAAAAA) and ((x+x) & 0xAAAAAAAA) are fp4 e2m1 values
+// {0, +1, -1} = encode() of K positions 2p and 2p+1, and (x & 0x22222222),
+// (x & 0x11111111) are the mask bits as fp4 1.0 and 0.5.
+IRIS_HD inline uint32_t xpack(uint32_t em16, uint32_t ep16) {
+    uint32_t x = 0;
+    for (int p = 0; p < 8; ++p) {
+        x |= ((em16 >> (2 * p + 1)) & 1u) << (4 * p);
+        x |= ((em16 >> (2 * p)) & 1u) << (4 * p + 1);
+        x |= ((ep16 >> (2 * p + 1)) & 1u) << (4 * p + 2);
+        x |= ((ep16 >> (2 * p)) & 1u) << (4 * p + 3);
+    }
+    return x;
+}
+IRIS_HD inline void xunpack(uint32_t x, uint32_t &em16, uint32_t &ep16) {
+    em16 = 0;
+    ep16 = 0;
+    for (int p = 0; p < 8; ++p) {
+        em16 |= ((x >> (4 * p)) & 1u) << (2 * p + 1);
+        em16 |= ((x >> (4 * p + 1)) & 1u) << (2 * p);
+        ep16 |= ((x >> (4 * p + 2)) & 1u) << (2 * p + 1);
+        ep16 |= ((x >> (4 * p + 3)) & 1u) << (2 * p);
+    }
+}
+// fp4 K index j (0..31) of a lane's fragment <-> bit of the lane's plane dword
+IRIS_HD inline int frag_bit(int j) { return (j & 16) + 2 * (j & 7) + ((j >> 3) & 1); }
+
+// MFMA query fragments: for chunk c (template bits [64c, 64c+64)) and lane
+// L = k + 32h (k = rotation index 0..30, 31 = zero row), one uint4 at
+// [c * 64 + L]: fp4 e2m1 of encode(q rotated by k - 15) at bit frag_bit(j) of
+// plane dword 2c + h (+1.0 = 0x2, -1.0 = 0xA, 0).  The den operand is derived
+// from it in-kernel (|enc|, doubled where the template side carries 0.5).
+constexpr int kFragDwords = 4;
+constexpr size_t kTemplateFragDwords = (size_t)(kPlaneDwords / 2) * 64 * kFragDwords;  // 200 chunks
 
 // Rotated-query tables (built on the host, uploaded once per engine):
 //   TEMPLATES: dword [w*64 + 2k] = mask_k word w, [w*64 + 2k+1] = pattern_k word w   (400 x 64)
@@ -103,6 +150,14 @@ int launch_generate(void *stream, const KindInfo &k, void *db, uint64_t t_first,
                     uint64_t global_index0);
 int launch_template_counts(void *stream, const void *db, const void *qtab, LaunchRange r, uint16_t *num_out,
                            uint16_t *den_out);
+int launch_template_mfma_counts(void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *num_out,
+                                uint16_t *den_out);
+int launch_template_mfma_search(void *stream, const void *db, const void *qfrag, LaunchRange r, double *dist_out,
+                                Partial *partials, uint32_t *n_partials);
+uint32_t mfma_search_partials(LaunchRange r);
+int launch_pack_tiles(void *stream, const void *staging, void *db, uint64_t t_first, uint64_t n);
+int launch_unpack_tiles(void *stream, const void *db, void *staging, uint64_t t_first, uint64_t n);
+int launch_generate_tiles(void *stream, void *db, uint64_t t_first, uint64_t n, uint64_t seed, uint64_t global_index0);
 int launch_template_search(void *stream, const void *db, const void *qtab, LaunchRange r, double *dist_out,
                            Partial *partials, uint32_t *n_partials);
 int launch_reduce(void *stream, const Partial *partials, uint32_t n_partials, Partial *out);
@@ -117,6 +172,7 @@ void bits_rotated(const uint64_t *in, int amount, uint64_t *out);
 void encoded_rotated(const uint16_t *in, int amount, uint16_t *out);
 void encode_template(const iris_template_t *t, uint16_t *out);
 void build_template_table(const iris_template_t *q, uint32_t *tab);                  // 400*64 dwords
+void build_template_frags(const iris_template_t *q, uint32_t *frag);                 // kTemplateFragDwords
 void build_masks_table(const uint64_t *const *vectors, int count, uint32_t *tab);     // 400*32
 void build_shares_table(const uint16_t *const *vectors, int count, uint32_t *tab);    // 6400*32
 void build_masks_rotations(const uint64_t *query, uint32_t *tab);

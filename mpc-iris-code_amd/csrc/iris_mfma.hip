@@ -1,0 +1,384 @@
+// iris_mfma.hip — Template masked Hamming on the gfx950 matrix cores (fp4).
+//
+// Why MFMA for bit work: on gfx950 the integer VALU ops this path needs
+// (v_bcnt, v_bitop3) issue at 16 lanes/clk, so the XOR+AND+popcount form is
+// capped near 39 T lane-ops/s = ~11 ms per 10M templates (35 % of the HBM
+// roofline; tools/ubench_ops.hip).  The same numbers are an
+// exact integer matrix product:
+//
+//   den[k][t] = sum_b qm_k[b] * em_t[b]                       (jointly valid bits)
+//   S  [k][t] = sum_b enc(q_k)[b] * enc(e_t)[b],  enc in {0,+1,-1}  (src/lib.rs:16-26)
+//   num       = (den - S) / 2                                 (src/lib.rs:134-163 identity)
+//
+// with M = 32 rotation rows (k = 0..30 + a zero row), N = 32 templates per
+// tile, K = 12800 bits: v_mfma_scale_f32_32x32x64_f8f6f4 with e2m1 operands.
+// Every product is 0 or +-1 and every sum is an integer <= 12800 < 2^24, so the
+// f32 accumulation is exact whatever the internal order.
+//
+// Operands: the 31 rotated query copies are precomputed once per engine as
+// fp4 A-fragments (iris_host.cpp, 400 KB, L2-resident).  The template side
+// is streamed from HBM once in the TILES layout (iris_internal.hpp), whose
+// interleaved dwords turn into fp4 B-fragments with four v_and + two
+// shift-and per dword pair — fast VOP2 ops, hidden under the MFMAs.
+#include <hip/hip_runtime.h>
+
+#include "iris_internal.hpp"
+
+namespace iris {
+
+typedef int v8i __attribute__((ext_vector_type(8)));
+typedef float v16f __attribute__((ext_vector_type(16)));
+
+constexpr int kTileRecs = 32;
+constexpr int kTileUint4 = kPlaneGroups * 64;  // 6400 uint4 = 102400 B per tile
+constexpr int kMfmaTiles = 4;                  // tiles per wave (128 templates)
+
+__device__ __forceinline__ v16f mfma_fp4(const v8i &a, const v8i &b, const v16f &c) {
+    // cbsz = blgp = 4: both operands e2m1; scales 127 = 2^0 (e8m0)
+    return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, c, 4, 4, 0, 127, 0, 127);
+}
+
+// Query-side den operand from the enc operand: |enc| as fp4 1.0, doubled to
+// 2.0 in the dwords whose template-side value is 0.5 (fragment dwords 1, 3).
+struct QFrag {
+    v8i am, ae;
+};
+__device__ __forceinline__ QFrag qfrag_of(const uint4 &qe) {
+    QFrag f;
+    f.ae = v8i{(int)qe.x, (int)qe.y, (int)qe.z, (int)qe.w, 0, 0, 0, 0};
+    f.am = v8i{(int)(qe.x & 0x22222222u), (int)((qe.y & 0x22222222u) << 1), (int)(qe.z & 0x22222222u),
+               (int)((qe.w & 0x22222222u) << 1), 0, 0, 0, 0};
+    return f;
+}
+
+// One 64-bit chunk of K for one tile.  x0/x1: the lane's interleaved dwords.
+__device__ __forceinline__ void chunk_step(uint32_t x0, uint32_t x1, const QFrag &q, v16f &den, v16f &s) {
+    const v8i bm = {(int)(x0 & 0x22222222u), (int)(x0 & 0x11111111u), (int)(x1 & 0x22222222u),
+                    (int)(x1 & 0x11111111u), 0, 0, 0, 0};
+    const v8i be = {(int)(x0 & 0xAAAAAAAAu), (int)((x0 << 1) & 0xAAAAAAAAu), (int)(x1 & 0xAAAAAAAAu),
+                    (int)((x1 << 1) & 0xAAAAAAAAu), 0, 0, 0, 0};
+    den = mfma_fp4(q.am, bm, den);
+    s = mfma_fp4(q.ae, be, s);
+}
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 stream_load(const uint4 *p) {
+    const u32x4 v = __builtin_nontemporal_load((const u32x4 *)p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+// candidate order inside one template: fraction, then lowest rotation
+__device__ __forceinline__ bool better_rot(uint32_t an, uint32_t ad, int ar, uint32_t bn, uint32_t bd, int br) {
+    if (ad == 0) return false;
+    if (bd == 0) return true;
+    const uint32_t l = an * bd, r = bn * ad;
+    if (l != r) return l < r;
+    return ar < br;
+}
+
+__device__ __forceinline__ bool better_idx(const Partial &a, const Partial &b) {
+    if (a.den == 0) return false;
+    if (b.den == 0) return true;
+    const uint32_t l = a.num * b.den, r = b.num * a.den;
+    if (l != r) return l < r;
+    return a.idx < b.idx;
+}
+
+__device__ __forceinline__ Partial shfl_partial(const Partial &c, int off) {
+    Partial o;
+    o.num = __shfl_xor(c.num, off);
+    o.den = __shfl_xor(c.den, off);
+    o.rot = __shfl_xor(c.rot, off);
+    o.pad = 0;
+    const uint32_t lo = __shfl_xor((uint32_t)c.idx, off), hi = __shfl_xor((uint32_t)(c.idx >> 32), off);
+    o.idx = ((uint64_t)hi << 32) | lo;
+    return o;
+}
+
+enum { MF_COUNTS = 0, MF_SEARCH = 1 };
+
+template <int MODE>
+__global__ void __launch_bounds__(256, 2)
+    template_mfma_kernel(const uint4 *__restrict__ db, const uint4 *__restrict__ qfrag, uint64_t tile0,
+                         uint64_t ntiles, uint64_t first, uint64_t end, uint16_t *__restrict__ num_out,
+                         uint16_t *__restrict__ den_out, double *__restrict__ dist_out,
+                         Partial *__restrict__ partials) {
+    constexpr int T = kMfmaTiles;
+    const int lane = threadIdx.x & 63;
+    const int wslot = threadIdx.x >> 6;
+    const uint64_t wave = (uint64_t)blockIdx.x * kWaveSlots + wslot;
+    const uint64_t tw = wave * T;  // first tile (relative to tile0) of this wave
+    const bool active = tw < ntiles;  // wave-uniform
+
+    v16f den[T], s[T];
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            den[t][i] = 0.f;
+            s[t][i] = 0.f;
+        }
+    }
+
+    if (active) {
+        // 3-stage register pipeline: the loads of step g+2 are in flight
+        // while step g computes (one step = 2 chunks = 16 MFMAs per wave).
+        const uint4 *dp[T];
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+            const uint64_t rel = (tw + t < ntiles) ? tw + t : ntiles - 1;  // clamp: extra tiles re-read a valid one
+            dp[t] = db + (tile0 + rel) * (uint64_t)kTileUint4 + lane;
+        }
+        const uint4 *qp = qfrag + lane;  // chunk c: qfrag[c * 64 + lane]
+        struct Stage {
+            uint4 d[T];
+            uint4 q0, q1;
+        };
+        auto load = [&](Stage &st, int g) {
+            g = g < kPlaneGroups ? g : kPlaneGroups - 1;
+#pragma unroll
+            for (int t = 0; t < T; ++t) st.d[t] = stream_load(dp[t] + g * 64);
+            st.q0 = qp[(2 * g) * 64];
+            st.q1 = qp[(2 * g + 1) * 64];
+            // keep this stage's loads together and ahead of the compute that
+            // follows: vmcnt retires in order, so a query load sunk next to
+            // its use would also drain the HBM prefetches issued before it
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        auto compute = [&](const Stage &st) {
+            const QFrag f0 = qfrag_of(st.q0);
+#pragma unroll
+            for (int t = 0; t < T; ++t) chunk_step(st.d[t].x, st.d[t].y, f0, den[t], s[t]);
+            const QFrag f1 = qfrag_of(st.q1);
+#pragma unroll
+            for (int t = 0; t < T; ++t) chunk_step(st.d[t].z, st.d[t].w, f1, den[t], s[t]);
+        };
+        Stage sa, sb, sc;
+        load(sa, 0);
+        load(sb, 1);
+        int g = 0;
+#pragma unroll 1
+        for (; g + 3 <= kPlaneGroups; g += 3) {
+            load(sc, g + 2);
+            compute(sa);
+            load(sa, g + 3);
+            compute(sb);
+            load(sb, g + 4);
+            compute(sc);
+        }
+        // kPlaneGroups = 100 = 33 * 3 + 1: one step left, its data is in sa
+        if (g < kPlaneGroups) compute(sa);
+    }
+
+    // C layout: lane l holds template (l & 31) of the tile and rotation rows
+    // k = (r & 3) + 8 (r >> 2) + 4 (l >> 5), r = 0..15.
+    const int h = lane >> 5;
+    Partial best;
+    best.num = 0;
+    best.den = 0;
+    best.rot = 0;
+    best.pad = 0;
+    best.idx = ~0ull;
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        const uint64_t tg = (tile0 + tw + t) * kTileRecs + (lane & 31);  // global template index
+        const bool valid = active && (tw + t < ntiles) && tg >= first && tg < end;
+        const uint64_t o = tg - first;
+        if (MODE == MF_COUNTS) {
+            if (valid) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int k = (r & 3) + 8 * (r >> 2) + 4 * h;
+                    if (k < kRot) {
+                        const uint32_t dd = (uint32_t)den[t][r];
+                        const int sv = (int)s[t][r];
+                        if (num_out) num_out[o * kRot + k] = (uint16_t)(((int)dd - sv) >> 1);
+                        if (den_out) den_out[o * kRot + k] = (uint16_t)dd;
+                    }
+                }
+            }
+        } else {
+            uint32_t bn = 0, bd = 0;
+            int br = 0;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int k = (r & 3) + 8 * (r >> 2) + 4 * h;
+                const uint32_t dd = (uint32_t)den[t][r];
+                const uint32_t nn = (uint32_t)(((int)dd - (int)s[t][r]) >> 1);
+                if (k < kRot && dd != 0 && (bd == 0 || nn * bd < bn * dd)) {
+                    bn = nn;
+                    bd = dd;
+                    br = k;
+                }
+            }
+            const uint32_t pn = __shfl_xor(bn, 32), pd = __shfl_xor(bd, 32);
+            const int pr = __shfl_xor(br, 32);
+            if (better_rot(pn, pd, pr, bn, bd, br)) {
+                bn = pn;
+                bd = pd;
+                br = pr;
+            }
+            if (valid && dist_out && h == 0) dist_out[o] = bd ? (double)bn / (double)bd : __builtin_inf();
+            Partial c;
+            c.num = bn;
+            c.den = valid ? bd : 0;
+            c.rot = br;
+            c.pad = 0;
+            c.idx = o;
+            if (better_idx(c, best)) best = c;
+        }
+    }
+    if (MODE == MF_SEARCH) {
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            const Partial ot = shfl_partial(best, off);
+            if (better_idx(ot, best)) best = ot;
+        }
+        __shared__ Partial sh[kWaveSlots];
+        if (lane == 0) sh[wslot] = best;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            Partial b = sh[0];
+#pragma unroll
+            for (int w = 1; w < kWaveSlots; ++w)
+                if (better_idx(sh[w], b)) b = sh[w];
+            partials[blockIdx.x] = b;
+        }
+    }
+}
+
+// ------------------------------------------------------------------ TILES layout plumbing
+
+// reference Template record (pattern dwords 0..399, mask dwords 400..799) ->
+// TILES uint4 of (record t, chunk pair g, half h)
+__global__ void __launch_bounds__(256) pack_tiles_kernel(const uint32_t *__restrict__ staging,
+                                                         uint4 *__restrict__ db, uint64_t t_first, uint64_t n) {
+    const uint64_t total = n * (uint64_t)(2 * kPlaneGroups);
+    for (uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; tid < total;
+         tid += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t i = tid % n, gh = tid / n;
+        const int g = (int)(gh >> 1), h = (int)(gh & 1);
+        const uint32_t *rec = staging + i * (2 * kPlaneDwords);
+        const int w0 = 4 * g + h, w1 = 4 * g + 2 + h;
+        const uint32_t em0 = rec[kPlaneDwords + w0], ep0 = rec[w0], em1 = rec[kPlaneDwords + w1], ep1 = rec[w1];
+        const uint64_t t = t_first + i;
+        uint4 v;
+        v.x = xpack(em0 & 0xFFFFu, ep0 & 0xFFFFu);
+        v.y = xpack(em0 >> 16, ep0 >> 16);
+        v.z = xpack(em1 & 0xFFFFu, ep1 & 0xFFFFu);
+        v.w = xpack(em1 >> 16, ep1 >> 16);
+        db[(t / kTileRecs) * (uint64_t)kTileUint4 + (uint64_t)g * 64 + (t % kTileRecs) + 32 * h] = v;
+    }
+}
+
+__global__ void __launch_bounds__(256) unpack_tiles_kernel(const uint4 *__restrict__ db, uint32_t *__restrict__ staging,
+                                                           uint64_t t_first, uint64_t n) {
+    const uint64_t total = n * (uint64_t)(2 * kPlaneGroups);
+    for (uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; tid < total;
+         tid += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t i = tid % n, gh = tid / n;
+        const int g = (int)(gh >> 1), h = (int)(gh & 1);
+        const uint64_t t = t_first + i;
+        const uint4 v = db[(t / kTileRecs) * (uint64_t)kTileUint4 + (uint64_t)g * 64 + (t % kTileRecs) + 32 * h];
+        uint32_t a, b, c, d;
+        xunpack(v.x, a, b);
+        xunpack(v.y, c, d);
+        uint32_t *rec = staging + i * (2 * kPlaneDwords);
+        const int w0 = 4 * g + h, w1 = 4 * g + 2 + h;
+        rec[kPlaneDwords + w0] = a | (c << 16);
+        rec[w0] = b | (d << 16);
+        xunpack(v.z, a, b);
+        xunpack(v.w, c, d);
+        rec[kPlaneDwords + w1] = a | (c << 16);
+        rec[w1] = b | (d << 16);
+    }
+}
+
+__global__ void __launch_bounds__(256) generate_tiles_kernel(uint4 *__restrict__ db, uint64_t t_first, uint64_t n,
+                                                             uint64_t key, uint64_t global_index0) {
+    const uint64_t total = n * (uint64_t)(2 * kPlaneGroups);
+    for (uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; tid < total;
+         tid += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t i = tid % n, gh = tid / n;
+        const int g = (int)(gh >> 1), h = (int)(gh & 1);
+        const uint64_t gt = global_index0 + i;
+        // dword 4g+h is half h of limb 2g, dword 4g+2+h half h of limb 2g+1
+        const uint64_t m0 = gen_limb(key, gt * 400 + 200 + 2 * g), m1 = gen_limb(key, gt * 400 + 200 + 2 * g + 1);
+        const uint64_t p0 = gen_limb(key, gt * 400 + 2 * g), p1 = gen_limb(key, gt * 400 + 2 * g + 1);
+        const uint32_t em0 = (uint32_t)(m0 >> (32 * h)), ep0 = (uint32_t)(p0 >> (32 * h));
+        const uint32_t em1 = (uint32_t)(m1 >> (32 * h)), ep1 = (uint32_t)(p1 >> (32 * h));
+        const uint64_t t = t_first + i;
+        uint4 v;
+        v.x = xpack(em0 & 0xFFFFu, ep0 & 0xFFFFu);
+        v.y = xpack(em0 >> 16, ep0 >> 16);
+        v.z = xpack(em1 & 0xFFFFu, ep1 & 0xFFFFu);
+        v.w = xpack(em1 >> 16, ep1 >> 16);
+        db[(t / kTileRecs) * (uint64_t)kTileUint4 + (uint64_t)g * 64 + (t % kTileRecs) + 32 * h] = v;
+    }
+}
+
+static int tiles_grid(uint64_t total) {
+    uint64_t b = (total + 255) / 256;
+    if (b > 256ull * 64) b = 256ull * 64;
+    return (int)(b ? b : 1);
+}
+
+int launch_pack_tiles(void *stream, const void *staging, void *db, uint64_t t_first, uint64_t n) {
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(pack_tiles_kernel, dim3(tiles_grid(n * 2 * kPlaneGroups)), dim3(256), 0, (hipStream_t)stream,
+                       (const uint32_t *)staging, (uint4 *)db, t_first, n);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_unpack_tiles(void *stream, const void *db, void *staging, uint64_t t_first, uint64_t n) {
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(unpack_tiles_kernel, dim3(tiles_grid(n * 2 * kPlaneGroups)), dim3(256), 0, (hipStream_t)stream,
+                       (const uint4 *)db, (uint32_t *)staging, t_first, n);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_generate_tiles(void *stream, void *db, uint64_t t_first, uint64_t n, uint64_t seed, uint64_t global_index0) {
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(generate_tiles_kernel, dim3(tiles_grid(n * 2 * kPlaneGroups)), dim3(256), 0,
+                       (hipStream_t)stream, (uint4 *)db, t_first, n, gen_key(seed, 0), global_index0);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+struct TileRange {
+    uint64_t tile0, ntiles, grid;
+};
+
+static TileRange tile_range(LaunchRange r) {
+    TileRange t;
+    t.tile0 = r.first / kTileRecs;
+    const uint64_t tile1 = (r.first + r.n + kTileRecs - 1) / kTileRecs;
+    t.ntiles = tile1 - t.tile0;
+    const uint64_t waves = (t.ntiles + kMfmaTiles - 1) / kMfmaTiles;
+    t.grid = (waves + kWaveSlots - 1) / kWaveSlots;
+    return t;
+}
+
+uint32_t mfma_search_partials(LaunchRange r) { return (uint32_t)tile_range(r).grid; }
+
+int launch_template_mfma_counts(void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *num_out,
+                                uint16_t *den_out) {
+    if (r.n == 0) return 0;
+    const TileRange t = tile_range(r);
+    hipLaunchKernelGGL(template_mfma_kernel<MF_COUNTS>, dim3((uint32_t)t.grid), dim3(256), 0, (hipStream_t)stream,
+                       (const uint4 *)db, (const uint4 *)qfrag, t.tile0, t.ntiles, r.first, r.first + r.n, num_out,
+                       den_out, (double *)nullptr, (Partial *)nullptr);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_template_mfma_search(void *stream, const void *db, const void *qfrag, LaunchRange r, double *dist_out,
+                                Partial *partials, uint32_t *n_partials) {
+    const TileRange t = tile_range(r);
+    *n_partials = (uint32_t)t.grid;
+    if (r.n == 0) return 0;
+    hipLaunchKernelGGL(template_mfma_kernel<MF_SEARCH>, dim3((uint32_t)t.grid), dim3(256), 0, (hipStream_t)stream,
+                       (const uint4 *)db, (const uint4 *)qfrag, t.tile0, t.ntiles, r.first, r.first + r.n,
+                       (uint16_t *)nullptr, (uint16_t *)nullptr, dist_out, partials);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace iris

@@ -30,6 +30,7 @@ LIB_PATH = HERE / "libiris_hip.so"
 
 COLS, ROWS, BITS, LIMBS, ROTATIONS = 200, 64, 12800, 200, 31
 KIND_MASKS, KIND_SHARES, KIND_TEMPLATES = 1, 2, 3
+LAYOUT_DEFAULT, LAYOUT_LANES, LAYOUT_TILES = 0, 1, 2
 _REC_DTYPE = {KIND_MASKS: (np.uint64, LIMBS), KIND_SHARES: (np.uint16, BITS), KIND_TEMPLATES: (np.uint64, 2 * LIMBS)}
 
 
@@ -82,6 +83,8 @@ def load_library(path=None):
             "iris_device_free": ([P, P], ctypes.c_int),
             "iris_memcpy_d2h": ([P, P, P, ctypes.c_size_t], ctypes.c_int),
             "iris_db_create": ([P, ctypes.c_int, u64, PP], ctypes.c_int),
+            "iris_db_create_ex": ([P, ctypes.c_int, u64, ctypes.c_int, PP], ctypes.c_int),
+            "iris_db_layout": ([P, ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
             "iris_db_destroy": ([P], ctypes.c_int),
             "iris_db_len": ([P, ctypes.POINTER(u64)], ctypes.c_int),
             "iris_db_capacity": ([P, ctypes.POINTER(u64)], ctypes.c_int),
@@ -122,6 +125,7 @@ def exported_symbols():
         "iris_last_error", "iris_version", "iris_device_count", "iris_device_open", "iris_device_close",
         "iris_device_synchronize", "iris_device_stream", "iris_device_set_profiling", "iris_device_kernel_stats",
         "iris_device_reset_stats", "iris_device_alloc", "iris_device_free", "iris_memcpy_d2h", "iris_db_create",
+        "iris_db_create_ex", "iris_db_layout",
         "iris_db_destroy", "iris_db_len", "iris_db_capacity", "iris_db_kind", "iris_db_append", "iris_db_write",
         "iris_db_read", "iris_db_generate", "iris_db_clear", "iris_masks_engine_new", "iris_distance_engine_new",
         "iris_template_engine_new", "iris_engine_destroy", "iris_engine_batch_process",
@@ -419,12 +423,19 @@ def _records(kind, records):
 class Database:
     """Device-resident database (replaces the reference's mmap'd share/masks files)."""
 
-    def __init__(self, device, kind, capacity):
+    def __init__(self, device, kind, capacity, layout=LAYOUT_DEFAULT):
         self.device = device
         self.kind = kind
         h = ctypes.c_void_p()
-        _check(load_library().iris_db_create(device.handle, int(kind), int(capacity), ctypes.byref(h)))
+        _check(load_library().iris_db_create_ex(device.handle, int(kind), int(capacity), int(layout),
+                                                ctypes.byref(h)))
         self.handle = h
+
+    @property
+    def layout(self):
+        v = ctypes.c_int()
+        _check(load_library().iris_db_layout(self.handle, ctypes.byref(v)))
+        return v.value
 
     def close(self):
         if self.handle:
@@ -575,9 +586,9 @@ class TemplateEngine(_Engine):
         _check(load_library().iris_template_distances(self.handle, db.handle, int(first), int(n), _ptr(out)))
         return out
 
-    def distances_host(self, records):
+    def distances_host(self, records, layout=LAYOUT_DEFAULT):
         a = _records(KIND_TEMPLATES, records)
-        with Database(self.device, KIND_TEMPLATES, max(1, a.shape[0])) as db:
+        with Database(self.device, KIND_TEMPLATES, max(1, a.shape[0]), layout) as db:
             db.append(a)
             return self.distances(db)
 
@@ -647,5 +658,6 @@ __all__ = [
     "Bits", "EncodedBits", "Template", "encode", "decode_distance", "distances", "denominators", "MasksEngine",
     "DistanceEngine", "TemplateEngine", "Device", "Database", "Match", "merge_matches", "dot_bool", "dot_u16",
     "dot_bool_batch", "dot_u16_batch", "IrisError", "load_library", "KIND_MASKS", "KIND_SHARES", "KIND_TEMPLATES",
+    "LAYOUT_DEFAULT", "LAYOUT_LANES", "LAYOUT_TILES",
     "ROTATIONS", "BITS", "LIMBS", "COLS", "ROWS",
 ]

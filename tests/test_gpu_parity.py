@@ -17,16 +17,40 @@ def bits_eq(a, b):
     return (np.asarray(a, np.float64).view(np.uint64) == np.asarray(b, np.float64).view(np.uint64)).all()
 
 
+LAYOUTS = [ih.LAYOUT_TILES, ih.LAYOUT_LANES]
+
+
+@pytest.fixture(scope="module", params=LAYOUTS, ids=["tiles-mfma", "lanes-valu"])
+def layout(request):
+    return request.param
+
+
 @pytest.fixture(scope="module")
-def tdb(device):
-    """1000 generated templates (not a multiple of 64)."""
-    db = ih.Database(device, ih.KIND_TEMPLATES, 1000)
+def tdb(device, layout):
+    """1000 generated templates (not a multiple of 32 or 64)."""
+    db = ih.Database(device, ih.KIND_TEMPLATES, 1000, layout)
     db.generate(1000, SEED)
+    assert db.layout == layout
     yield db
     db.close()
 
 
 # ---------------------------------------------------------------- storage
+
+
+def test_layouts_agree(device):
+    """The TILES (fp4 MFMA) and LANES (VALU popcount) kernels give identical
+    counts, distances and argmin on the same 3000 templates."""
+    q = oc.gen_templates(77, 0, 1)[0]
+    outs = []
+    for lay in LAYOUTS:
+        with ih.Database(device, ih.KIND_TEMPLATES, 3000, lay) as db, ih.TemplateEngine(device, q) as eng:
+            db.generate(3000, 31)
+            outs.append((eng.counts(db), eng.distances(db), eng.search(db)))
+    (n0, d0), dist0, m0 = outs[0]
+    (n1, d1), dist1, m1 = outs[1]
+    assert (n0 == n1).all() and (d0 == d1).all() and bits_eq(dist0, dist1)
+    assert (m0.index, m0.num, m0.den, m0.rotation) == (m1.index, m1.num, m1.den, m1.rotation)
 
 
 def test_generate_matches_oracle(device, tdb):
@@ -40,10 +64,10 @@ def test_generate_matches_oracle(device, tdb):
         assert (s.read(0, 70) == oc.gen_shares(SEED, 0, 70)).all()
 
 
-def test_append_write_read_roundtrip(device):
+def test_append_write_read_roundtrip(device, layout):
     rng = np.random.default_rng(1)
     recs = rng.integers(0, 2**64, (150, 400), dtype=np.uint64)
-    with ih.Database(device, ih.KIND_TEMPLATES, 300) as db:
+    with ih.Database(device, ih.KIND_TEMPLATES, 300, layout) as db:
         db.append(recs[:77])
         db.append(recs[77:])
         assert len(db) == 150
@@ -94,11 +118,11 @@ def test_template_distances_and_search(device, tdb):
         assert m2.index == 10_000 + 100 + i2 and bits_eq(m2.distance, b2)
 
 
-def test_planted_rotated_copies(device):
+def test_planted_rotated_copies(device, layout):
     """A rotated, lightly flipped copy of the query is the unique best match."""
     rng = np.random.default_rng(3)
     n = 5000
-    with ih.Database(device, ih.KIND_TEMPLATES, n) as db:
+    with ih.Database(device, ih.KIND_TEMPLATES, n, layout) as db:
         db.generate(n, 9)
         q = oc.gen_templates(1234, 0, 1)[0]
         for pos, r in ((4321, 15), (17, -15), (2500, 0)):
@@ -120,9 +144,9 @@ def test_planted_rotated_copies(device):
                 assert k - 15 == r and d[pos] < 0.01
 
 
-def test_template_edge_cases(device, golden):
+def test_template_edge_cases(device, golden, layout):
     q, db_ref = golden["query"], golden["db"]
-    with ih.Database(device, ih.KIND_TEMPLATES, db_ref.shape[0]) as db:
+    with ih.Database(device, ih.KIND_TEMPLATES, db_ref.shape[0], layout) as db:
         db.append(db_ref)
         with ih.TemplateEngine(device, q) as eng:
             num, den = eng.counts(db)
@@ -142,8 +166,8 @@ def test_template_edge_cases(device, golden):
             assert z.index == 2**64 - 1 and z.distance == np.inf
 
 
-def test_template_all_invalid_db(device):
-    with ih.Database(device, ih.KIND_TEMPLATES, 130) as db:
+def test_template_all_invalid_db(device, layout):
+    with ih.Database(device, ih.KIND_TEMPLATES, 130, layout) as db:
         db.append(np.zeros((130, 400), np.uint64))
         with ih.TemplateEngine(device, oc.gen_templates(1, 0, 1)[0]) as eng:
             m = eng.search(db)
@@ -248,12 +272,12 @@ def test_dot_u16_batch(device, na, nb):
 # ---------------------------------------------------------------- large-size properties
 
 
-def test_large_search_properties(device):
+def test_large_search_properties(device, layout):
     """2M templates (6.4 GB): planted known answer + sampled oracle checks of
     the per-template distances left on the device."""
     n = 2_000_000
     rng = np.random.default_rng(99)
-    with ih.Database(device, ih.KIND_TEMPLATES, n) as db:
+    with ih.Database(device, ih.KIND_TEMPLATES, n, layout) as db:
         db.generate(n, 2024)
         q = oc.gen_templates(555, 0, 1)[0]
         plant = 1_765_432
