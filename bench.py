@@ -79,37 +79,39 @@ def cpu_baseline(seconds):
     oc_lib = oc.load(lib) if lib else oc.load()
     query = oc.gen_templates(SEED + 1, 0, 1)[0]
 
-    def run(n):
-        db = oc.gen_templates(SEED, 0, n)
-        out = np.empty(n, np.float64)
+    n = 1_000_000  # 3.2 GB of templates: far beyond the CPU caches, streamed from DRAM each pass
+    db = oc.gen_templates(SEED, 0, n)
+    out = np.empty(n, np.float64)
+    d = np.zeros(1, np.float64)
+    i = np.zeros(1, np.uint64)
+    passes, t = 0, 0.0
+    while t < seconds and passes < 1000:
         t0 = time.perf_counter()
         oc_lib.orc_template_distances_batch(oc._p(query), oc._p(db), n, oc._p(out), threads)
-        d = np.zeros(1, np.float64)
-        i = np.zeros(1, np.uint64)
         oc_lib.orc_argmin(oc._p(out), n, oc._p(d), oc._p(i))  # resolver aggregation, src/main.rs:616-621
-        return time.perf_counter() - t0
-
-    probe = 40_000
-    t = run(probe)
-    n = int(min(2_000_000, max(probe, probe * seconds / max(t, 1e-6))))
-    t = run(n)
+        t += time.perf_counter() - t0
+        passes += 1
+    del db
     try:
         model = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
     except Exception:
         model = "unknown"
     return {
-        "value": ROT * n / t, "unit": "template comparisons/s", "cores": threads, "kind": "port",
-        "sample": f"{n} templates x 31 rotations, 1 query, distances + argmin, {t:.2f} s, "
+        "value": ROT * n * passes / t, "unit": "template comparisons/s", "cores": threads, "kind": "port",
+        "sample": f"{passes} passes over {n} templates x 31 rotations, 1 query, distances + argmin, {t:.2f} s, "
                   f"{threads} threads on {model}, gcc -O3 -march=native oracle/iris_oracle.c",
     }
 
 
-def load_traffic(n_per_launch):
+def load_traffic(n_per_launch, layout):
     """HBM bytes per launch of the search kernel from the committed PMC run
-    (profiles/*pmc*.json), scaled to this launch size; None if absent."""
-    for p in sorted((ROOT / "profiles").glob("*pmc*.json"), reverse=True):
+    (profiles/*pmc*.json, FETCH_SIZE/WRITE_SIZE corrected per
+    MI355X_MICROARCH.md §HBM), scaled to this launch size; None if absent."""
+    for p in sorted((ROOT / "profiles").glob("*pmc_template_search*.json"), reverse=True):
         try:
             j = json.loads(p.read_text())
+            if j.get("layout") != layout:
+                continue
             return j["hbm_bytes_per_template"] * n_per_launch, p.name
         except Exception:
             continue
@@ -190,7 +192,7 @@ def main():
     _, rms, _ = dev.kernel_stats("reduce")
     avg_ms = kms / max(1, launches)
     achieved = BYTES_PER_TEMPLATE * n / (avg_ms * 1e-3) / 1e9
-    traffic, traffic_src = load_traffic(n)
+    traffic, traffic_src = load_traffic(n, args.layout)
     ms_per_step = elapsed / args.steps * 1e3
     value = ROT * total / (elapsed / args.steps)
 
