@@ -126,18 +126,24 @@ def main():
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
     dist = None
+    # "nccl" is RCCL on ROCm (the exchange runs over xGMI); IRIS_DIST_BACKEND=gloo
+    # rehearses the same flow with CPU exchange tensors (e.g. 2 ranks on 1 GPU).
+    backend = os.environ.get("IRIS_DIST_BACKEND", "nccl")
+    ordinal = local
     if world > 1:
         import torch
         import torch.distributed as dist
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", rank=rank, world_size=world)
+        ordinal = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(ordinal)
+        dist.init_process_group(backend, rank=rank, world_size=world)
         import iris_dist
+    xdev = f"cuda:{ordinal}" if backend == "nccl" else "cpu"
 
     n = args.n_per_gpu
     lo = rank * n
     total = n * world
-    dev = ih.Device(local)
+    dev = ih.Device(ordinal)
     layout = ih.LAYOUT_TILES if args.layout == "tiles" else ih.LAYOUT_LANES
     db = ih.Database(dev, ih.KIND_TEMPLATES, n, layout)
     t0 = time.time()
@@ -166,7 +172,7 @@ def main():
     def step():
         m = eng.search(db, index_base=lo)
         if dist is not None:
-            m = iris_dist.allgather_merge(m, device=f"cuda:{local}")
+            m = iris_dist.allgather_merge(m, device=xdev)
         return m
 
     for _ in range(args.warmup):
@@ -183,7 +189,7 @@ def main():
     if dist is not None:
         import torch
 
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=xdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
