@@ -53,7 +53,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--layout", choices=["tiles", "lanes"], default="tiles",
-                    help="tiles = fp4-MFMA kernel (default), lanes = VALU popcount kernel")
+                    help="tiles = MFMA kernels (default), lanes = VALU kernels")
+    ap.add_argument("--workload", choices=["search", "masks", "shares"], default="search",
+                    help="search = Template masked Hamming + argmin (configs[1], default); "
+                         "masks = MasksEngine denominators; shares = DistanceEngine u16 share dot (configs[3])")
     return ap.parse_args()
 
 
@@ -145,7 +148,8 @@ def main():
     total = n * world
     dev = ih.Device(ordinal)
     layout = ih.LAYOUT_TILES if args.layout == "tiles" else ih.LAYOUT_LANES
-    db = ih.Database(dev, ih.KIND_TEMPLATES, n, layout)
+    kind = {"search": ih.KIND_TEMPLATES, "masks": ih.KIND_MASKS, "shares": ih.KIND_SHARES}[args.workload]
+    db = ih.Database(dev, kind, n, layout)
     t0 = time.time()
     db.generate(n, SEED, global_index0=lo)
     gen_s = time.time() - t0
@@ -155,9 +159,17 @@ def main():
     query = oc.gen_templates(SEED + 1, 0, 1)[0]
     plant_global = total * 3 // 4 + 12345
     plant_rot = 9
-    if lo <= plant_global < lo + n:
-        db.write(plant_global - lo, planted_record(query, plant_rot)[None, :])
-    eng = ih.TemplateEngine(dev, query)
+    out_dev = None
+    if args.workload == "search":
+        if lo <= plant_global < lo + n:
+            db.write(plant_global - lo, planted_record(query, plant_rot)[None, :])
+        eng = ih.TemplateEngine(dev, query)
+    elif args.workload == "masks":
+        eng = ih.MasksEngine(dev, query[200:])
+        out_dev = dev.alloc(n * ROT * 2)
+    else:
+        eng = ih.DistanceEngine(dev, ih.encode(ih.Template.from_array(query)))
+        out_dev = dev.alloc(n * ROT * 2)
 
     def sync_all():
         if dist is not None:
@@ -170,6 +182,9 @@ def main():
             dev.synchronize()
 
     def step():
+        if args.workload != "search":
+            eng.batch_process_device(db, out_dev)  # [n][31] u16 left in HBM
+            return None
         m = eng.search(db, index_base=lo)
         if dist is not None:
             m = iris_dist.allgather_merge(m, device=xdev)
@@ -193,18 +208,30 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    ok = m.index == plant_global and m.rotation == plant_rot
-    launches, kms, items = dev.kernel_stats("template_search")
+    kname = {"search": "template_search", "masks": "masks", "shares": "shares"}[args.workload]
+    rec_bytes = {"search": BYTES_PER_TEMPLATE, "masks": 1600, "shares": 25600}[args.workload]
+    if args.workload == "search":
+        ok = m.index == plant_global and m.rotation == plant_rot
+    else:  # spot-check 64 outputs against the oracle
+        sample = np.random.default_rng(0).choice(n, 64, replace=False)
+        full = np.empty((n, ROT), np.uint16)
+        dev.d2h(full, out_dev)
+        recs = np.stack([db.read(int(i), 1)[0] for i in sample])
+        want = (oc.masks_batch(query[200:], recs) if args.workload == "masks"
+                else oc.distance_batch(ih.encode(ih.Template.from_array(query)).values, recs))
+        ok = bool((full[sample] == want).all())
+        del full
+    launches, kms, items = dev.kernel_stats(kname)
     _, rms, _ = dev.kernel_stats("reduce")
     avg_ms = kms / max(1, launches)
-    achieved = BYTES_PER_TEMPLATE * n / (avg_ms * 1e-3) / 1e9
-    traffic, traffic_src = load_traffic(n, args.layout)
+    achieved = rec_bytes * n / (avg_ms * 1e-3) / 1e9
+    traffic, traffic_src = load_traffic(n, args.layout) if args.workload == "search" else (None, None)
     ms_per_step = elapsed / args.steps * 1e3
     value = ROT * total / (elapsed / args.steps)
 
     if rank == 0:
         cpu = None
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and args.workload == "search":
             try:
                 cpu = cpu_baseline(args.cpu_seconds)
             except Exception as ex:  # reported, never fatal
@@ -223,39 +250,50 @@ def main():
             "dtype": "u32",
             "data": "synthetic (on-device counter-based generator, uniform random pattern+mask bits; planted known answer)",
             "config": {
-                "workload": "1 query x 31 rotations x N templates, Template masked Hamming + fused min/argmin (BASELINE configs[1] at N=1)",
+                "workload": {
+                    "search": "1 query x 31 rotations x N templates, Template masked Hamming + fused min/argmin (BASELINE configs[1] at N=1)",
+                    "masks": "MasksEngine: 1 query mask x 31 rotations x N masks, [u16;31] denominators left in HBM",
+                    "shares": "DistanceEngine: 1 encoded query x 31 rotations x N u16 shares, [u16;31] left in HBM (BASELINE configs[3])",
+                }[args.workload],
                 "templates_per_gpu": n, "total_templates": total, "queries": 1, "rotations": ROT,
-                "bytes_per_template": BYTES_PER_TEMPLATE, "parallelism": f"db-shard x{world}",
+                "bytes_per_template": rec_bytes, "parallelism": f"db-shard x{world}", "layout": args.layout,
             },
             "roofline": {
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
             },
             "kernel": {
-                "name": "template_mfma_kernel<MF_SEARCH> (fp4 MFMA)" if args.layout == "tiles"
-                        else "template_kernel<MODE_SEARCH> (VALU popcount)",
+                "name": {("search", "tiles"): "template_mfma_kernel<MF_SEARCH> (fp4 MFMA)",
+                         ("search", "lanes"): "template_kernel<MODE_SEARCH> (VALU popcount)",
+                         ("masks", "tiles"): "masks_mfma_kernel (fp4 MFMA)",
+                         ("masks", "lanes"): "masks_kernel (VALU popcount)",
+                         ("shares", "tiles"): "shares_mfma_kernel (i8 MFMA)",
+                         ("shares", "lanes"): "shares_kernel (VALU v_pk_mad_u16)"}[(args.workload, args.layout)],
                 "avg_ms": avg_ms, "launches": launches,
                 "reduce_avg_ms": rms / max(1, launches),
                 "frac_of_measured_hbm": achieved / HBM_MEASURED_GBS,
                 "valu_int_frac": (VALU_OPS_PER_TEMPLATE * n / (avg_ms * 1e-3) / VALU_INT_PEAK_OPS
-                                  if args.layout == "lanes" else None),
+                                  if args.layout == "lanes" and args.workload == "search" else None),
                 "mfma_fp4_frac": (MFMA_MACS_PER_TEMPLATE * n / (avg_ms * 1e-3) / FP4_DENSE_PEAK_MACS
-                                  if args.layout == "tiles" else None),
+                                  if args.layout == "tiles" and args.workload == "search" else None),
                 "traffic_source": traffic_src,
             },
             "cpu_baseline": cpu,
-            "check": {"planted_index": plant_global, "found_index": int(m.index), "rotation": int(m.rotation),
-                      "distance": m.distance, "ok": bool(ok)},
+            "check": ({"planted_index": plant_global, "found_index": int(m.index), "rotation": int(m.rotation),
+                       "distance": m.distance, "ok": bool(ok)} if args.workload == "search"
+                      else {"sampled_outputs_vs_oracle": 64, "ok": bool(ok)}),
             "setup": {"generate_s": gen_s},
         }
         print(json.dumps(line))
+    if out_dev is not None:
+        dev.free(out_dev)
     eng.close()
     db.close()
     dev.close()
     if dist is not None:
         dist.destroy_process_group()
     if not ok:
-        print(f"planted answer not found: {m}", file=sys.stderr)
+        print(f"result check failed: {m}", file=sys.stderr)
         sys.exit(3)
 
 

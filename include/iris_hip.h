@@ -147,6 +147,10 @@ int iris_engine_destroy(iris_engine_t *engine);
  * array of n*31 uint16_t.  The engine kind must match the DB kind. */
 int iris_engine_batch_process(iris_engine_t *engine, const iris_db_t *db, uint64_t first, uint64_t n,
                               uint16_t *out);
+/* As iris_engine_batch_process, with out_device a DEVICE array of n*31
+ * uint16_t (for pipelines that keep the results on the GPU). */
+int iris_engine_batch_process_device(iris_engine_t *engine, const iris_db_t *db, uint64_t first, uint64_t n,
+                                     uint16_t *out_device);
 /* Host-slice form with exactly the reference signature: `db` is a host array
  * of n reference-layout records, `out` a host array of n*31 uint16_t. */
 int iris_engine_batch_process_host(iris_engine_t *engine, const void *db, uint64_t n, uint16_t *out);

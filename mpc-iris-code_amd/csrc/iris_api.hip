@@ -195,7 +195,7 @@ struct TempDb {
 
 int temp_db(iris_device *d, int kind, uint64_t cap, TempDb &t) {
     t.db.dev = d;
-    t.db.k = kind_info(kind, IRIS_LAYOUT_LANES);
+    t.db.k = kind_info(kind, IRIS_LAYOUT_TILES);
     t.db.cap = (cap + t.db.k.block - 1) / t.db.k.block * t.db.k.block;
     t.db.len = 0;
     const size_t bytes = std::max<uint64_t>(1, t.db.cap / t.db.k.block) * block_bytes(t.db.k);
@@ -218,36 +218,55 @@ int run_u16_engine(iris_engine *e, const iris_db *db, uint64_t first, uint64_t n
     for (uint64_t done = 0; done < n; done += ch) {
         const uint64_t m = std::min<uint64_t>(ch, n - done);
         LaunchRange r{first + done, m};
+        const bool tiles = db->k.layout == IRIS_LAYOUT_TILES;
+        uint16_t *o = (uint16_t *)d->out_a.p;
         if (e->kind == IRIS_KIND_MASKS)
-            CHK(timed(d, "masks", m, [&] { return launch_masks(d->stream, db->data, e->qtab, r, (uint16_t *)d->out_a.p); }));
+            CHK(timed(d, "masks", m, [&] {
+                return tiles ? launch_masks_mfma(d->stream, db->data, e->qfrag, r, o) : launch_masks(d->stream, db->data, e->qtab, r, o);
+            }));
         else
-            CHK(timed(d, "shares", m, [&] { return launch_shares(d->stream, db->data, e->qtab, r, (uint16_t *)d->out_a.p); }));
+            CHK(timed(d, "shares", m, [&] {
+                return tiles ? launch_shares_mfma(d->stream, db->data, e->qfrag, r, o) : launch_shares(d->stream, db->data, e->qtab, r, o);
+            }));
         HIPCHK(hipMemcpyAsync(out + done * kRot, d->out_a.p, m * kRot * 2, hipMemcpyDeviceToHost, d->stream));
         CHK(sync(d));
     }
     return 0;
 }
 
-int engine_new(iris_device *dev, int kind, const void *table, size_t bytes, iris_engine **out) {
+void engine_free(iris_engine *e) {
+    if (!e) return;
+    if (e->qtab) (void)hipFree(e->qtab);
+    if (e->qfrag) (void)hipFree(e->qfrag);
+    delete e;
+}
+
+// Uploads the LANES table and (optionally) the TILES fragments of a new engine.
+int engine_new(iris_device *dev, int kind, const void *table, size_t bytes, iris_engine **out,
+               const void *frag = nullptr, size_t frag_bytes = 0) {
     iris_engine *e = new (std::nothrow) iris_engine();
     if (!e) return fail(IRIS_E_NOMEM, "out of host memory");
     e->dev = dev;
     e->kind = kind;
     hipError_t err = hipMalloc(&e->qtab, bytes);
+    if (err == hipSuccess && frag) err = hipMalloc(&e->qfrag, frag_bytes);
     if (err != hipSuccess) {
-        delete e;
+        engine_free(e);
         return fail(IRIS_E_NOMEM, std::string("hipMalloc query table: ") + hipGetErrorString(err));
     }
     err = hipMemcpyAsync(e->qtab, table, bytes, hipMemcpyHostToDevice, dev->stream);
+    if (err == hipSuccess && frag) err = hipMemcpyAsync(e->qfrag, frag, frag_bytes, hipMemcpyHostToDevice, dev->stream);
     if (err == hipSuccess) err = hipStreamSynchronize(dev->stream);
     if (err != hipSuccess) {
-        (void)hipFree(e->qtab);
-        delete e;
+        engine_free(e);
         return fail(IRIS_E_HIP, std::string("upload query table: ") + hipGetErrorString(err));
     }
     *out = e;
     return 0;
 }
+
+constexpr size_t kMaskFragBytes = kMaskFragUint4 * 16;
+constexpr size_t kShareFragBytes = kShareFragUint4 * 16 + 32 * 8;
 
 double rust_f64_min(double a, double b) {
     if (isnan(a)) return b;
@@ -387,9 +406,8 @@ int iris_db_create(iris_device_t *d, int kind, uint64_t capacity, iris_db_t **ou
 int iris_db_create_ex(iris_device_t *d, int kind, uint64_t capacity, int layout, iris_db_t **out) {
     ARG(d && out, "NULL argument");
     CHK(check_kind(kind));
-    if (layout == IRIS_LAYOUT_DEFAULT) layout = kind == IRIS_KIND_TEMPLATES ? IRIS_LAYOUT_TILES : IRIS_LAYOUT_LANES;
-    ARG(layout == IRIS_LAYOUT_LANES || (layout == IRIS_LAYOUT_TILES && kind == IRIS_KIND_TEMPLATES),
-        "unsupported layout for this record kind");
+    if (layout == IRIS_LAYOUT_DEFAULT) layout = IRIS_LAYOUT_TILES;
+    ARG(layout == IRIS_LAYOUT_LANES || layout == IRIS_LAYOUT_TILES, "unknown layout");
     std::lock_guard<std::recursive_mutex> g(d->mu);
     CHK(set_device(d));
     iris_db *db = new (std::nothrow) iris_db();
@@ -519,7 +537,15 @@ int iris_masks_engine_new(iris_device_t *d, const uint64_t query_mask[IRIS_LIMBS
     CHK(set_device(d));
     std::vector<uint32_t> tab((size_t)kPlaneDwords * kSlotTabStride);
     build_masks_rotations(query_mask, tab.data());
-    return engine_new(d, IRIS_KIND_MASKS, tab.data(), tab.size() * 4, out);
+    std::vector<uint64_t> rot((size_t)kRot * IRIS_LIMBS);
+    const uint64_t *ptrs[kRot];
+    for (int k = 0; k < kRot; ++k) {
+        bits_rotated(query_mask, k - 15, &rot[(size_t)k * IRIS_LIMBS]);
+        ptrs[k] = &rot[(size_t)k * IRIS_LIMBS];
+    }
+    std::vector<uint32_t> frag(kMaskFragBytes / 4);
+    build_masks_frags(ptrs, kRot, frag.data());
+    return engine_new(d, IRIS_KIND_MASKS, tab.data(), tab.size() * 4, out, frag.data(), kMaskFragBytes);
 }
 
 int iris_distance_engine_new(iris_device_t *d, const uint16_t query[IRIS_BITS], iris_engine_t **out) {
@@ -528,7 +554,15 @@ int iris_distance_engine_new(iris_device_t *d, const uint16_t query[IRIS_BITS], 
     CHK(set_device(d));
     std::vector<uint32_t> tab((size_t)kShareDwords * kSlotTabStride);
     build_shares_rotations(query, tab.data());
-    return engine_new(d, IRIS_KIND_SHARES, tab.data(), tab.size() * 4, out);
+    std::vector<uint16_t> rot((size_t)kRot * IRIS_BITS);
+    const uint16_t *ptrs[kRot];
+    for (int k = 0; k < kRot; ++k) {
+        encoded_rotated(query, k - 15, &rot[(size_t)k * IRIS_BITS]);
+        ptrs[k] = &rot[(size_t)k * IRIS_BITS];
+    }
+    std::vector<uint32_t> frag(kShareFragBytes / 4);
+    build_shares_frags(ptrs, kRot, frag.data());
+    return engine_new(d, IRIS_KIND_SHARES, tab.data(), tab.size() * 4, out, frag.data(), kShareFragBytes);
 }
 
 int iris_template_engine_new(iris_device_t *d, const iris_template_t *query, iris_engine_t **out) {
@@ -539,17 +573,7 @@ int iris_template_engine_new(iris_device_t *d, const iris_template_t *query, iri
     build_template_table(query, tab.data());
     std::vector<uint32_t> frag(kTemplateFragDwords);
     build_template_frags(query, frag.data());
-    iris_engine *e = nullptr;
-    CHK(engine_new(d, IRIS_KIND_TEMPLATES, tab.data(), tab.size() * 4, &e));
-    hipError_t err = hipMalloc(&e->qfrag, frag.size() * 4);
-    if (err == hipSuccess) err = hipMemcpyAsync(e->qfrag, frag.data(), frag.size() * 4, hipMemcpyHostToDevice, d->stream);
-    if (err == hipSuccess) err = hipStreamSynchronize(d->stream);
-    if (err != hipSuccess) {
-        iris_engine_destroy(e);
-        return fail(IRIS_E_HIP, std::string("upload query fragments: ") + hipGetErrorString(err));
-    }
-    *out = e;
-    return 0;
+    return engine_new(d, IRIS_KIND_TEMPLATES, tab.data(), tab.size() * 4, out, frag.data(), frag.size() * 4);
 }
 
 int iris_engine_destroy(iris_engine_t *e) {
@@ -558,10 +582,8 @@ int iris_engine_destroy(iris_engine_t *e) {
         std::lock_guard<std::recursive_mutex> g(e->dev->mu);
         (void)hipSetDevice(e->dev->ordinal);
         (void)hipStreamSynchronize(e->dev->stream);
-        if (e->qtab) (void)hipFree(e->qtab);
-        if (e->qfrag) (void)hipFree(e->qfrag);
+        engine_free(e);
     }
-    delete e;
     return 0;
 }
 
@@ -576,6 +598,33 @@ int iris_engine_batch_process(iris_engine_t *e, const iris_db_t *db, uint64_t fi
     if (n == 0) return 0;
     ARG(out, "out is NULL");
     return run_u16_engine(e, db, first, n, out);
+}
+
+int iris_engine_batch_process_device(iris_engine_t *e, const iris_db_t *db, uint64_t first, uint64_t n,
+                                     uint16_t *out_device) {
+    ARG(e && db, "NULL argument");
+    ARG(e->kind == IRIS_KIND_MASKS || e->kind == IRIS_KIND_SHARES, "batch_process needs a masks or distance engine");
+    ARG(db->k.kind == e->kind, "engine kind does not match the database kind");
+    ARG(e->dev == db->dev, "engine and database live on different devices");
+    iris_device *d = e->dev;
+    std::lock_guard<std::recursive_mutex> g(d->mu);
+    CHK(set_device(d));
+    CHK(range_ok(db, first, n));
+    if (n == 0) return 0;
+    ARG(out_device, "out is NULL");
+    LaunchRange r{first, n};
+    const bool tiles = db->k.layout == IRIS_LAYOUT_TILES;
+    if (e->kind == IRIS_KIND_MASKS)
+        CHK(timed(d, "masks", n, [&] {
+            return tiles ? launch_masks_mfma(d->stream, db->data, e->qfrag, r, out_device)
+                         : launch_masks(d->stream, db->data, e->qtab, r, out_device);
+        }));
+    else
+        CHK(timed(d, "shares", n, [&] {
+            return tiles ? launch_shares_mfma(d->stream, db->data, e->qfrag, r, out_device)
+                         : launch_shares(d->stream, db->data, e->qtab, r, out_device);
+        }));
+    return sync(d);
 }
 
 int iris_engine_batch_process_host(iris_engine_t *e, const void *records, uint64_t n, uint16_t *out) {
@@ -720,16 +769,17 @@ int iris_dot_bool_batch(iris_device_t *d, const uint64_t *a, uint64_t na, const 
     CHK(db_write_locked(&t.db, 0, b, nb));
     std::vector<uint16_t> tmp(nb * kRot);
     std::vector<uint32_t> tab((size_t)kPlaneDwords * kSlotTabStride);
+    std::vector<uint32_t> frag(kMaskFragBytes / 4);
     for (uint64_t i0 = 0; i0 < na; i0 += kRot) {
         const int cnt = (int)std::min<uint64_t>(kRot, na - i0);
         const uint64_t *ptrs[kRot];
         for (int k = 0; k < cnt; ++k) ptrs[k] = a + (i0 + k) * IRIS_LIMBS;
         build_masks_table(ptrs, cnt, tab.data());
+        build_masks_frags(ptrs, cnt, frag.data());
         iris_engine *e = nullptr;
-        CHK(engine_new(d, IRIS_KIND_MASKS, tab.data(), tab.size() * 4, &e));
+        CHK(engine_new(d, IRIS_KIND_MASKS, tab.data(), tab.size() * 4, &e, frag.data(), kMaskFragBytes));
         int rc = run_u16_engine(e, &t.db, 0, nb, tmp.data());
-        (void)hipFree(e->qtab);
-        delete e;
+        engine_free(e);
         CHK(rc);
         for (uint64_t j = 0; j < nb; ++j)
             for (int k = 0; k < cnt; ++k) out[j * na + i0 + k] = tmp[j * kRot + k];
@@ -749,16 +799,17 @@ int iris_dot_u16_batch(iris_device_t *d, const uint16_t *a, uint64_t na, const u
     CHK(db_write_locked(&t.db, 0, b, nb));
     std::vector<uint16_t> tmp(nb * kRot);
     std::vector<uint32_t> tab((size_t)kShareDwords * kSlotTabStride);
+    std::vector<uint32_t> frag(kShareFragBytes / 4);
     for (uint64_t i0 = 0; i0 < na; i0 += kRot) {
         const int cnt = (int)std::min<uint64_t>(kRot, na - i0);
         const uint16_t *ptrs[kRot];
         for (int k = 0; k < cnt; ++k) ptrs[k] = a + (i0 + k) * IRIS_BITS;
         build_shares_table(ptrs, cnt, tab.data());
+        build_shares_frags(ptrs, cnt, frag.data());
         iris_engine *e = nullptr;
-        CHK(engine_new(d, IRIS_KIND_SHARES, tab.data(), tab.size() * 4, &e));
+        CHK(engine_new(d, IRIS_KIND_SHARES, tab.data(), tab.size() * 4, &e, frag.data(), kShareFragBytes));
         int rc = run_u16_engine(e, &t.db, 0, nb, tmp.data());
-        (void)hipFree(e->qtab);
-        delete e;
+        engine_free(e);
         CHK(rc);
         for (uint64_t j = 0; j < nb; ++j)
             for (int k = 0; k < cnt; ++k) out[j * na + i0 + k] = tmp[j * kRot + k];

@@ -1,0 +1,414 @@
+// iris_engines_mfma.hip — MasksEngine and DistanceEngine on the matrix cores.
+//
+// MasksEngine::batch_process (src/lib.rs:69-79): out[k][t] = popcount(rot_k(qm) & m_t)
+//   = sum_b qm_k[b] * m_t[b]: fp4 e2m1 MFMA, M = 32 rotation rows, N = 32 masks,
+//   K = 12800 bits, one v_mfma_scale_f32_32x32x64_f8f6f4 per 64-bit chunk.
+//
+// DistanceEngine::batch_process (src/lib.rs:42-52): out[k][t] = sum_i q_k[i] e_t[i]
+//   mod 2^16 over 12800 u16.  With bytes a = a_hi*256 + a_lo and a' = a - 128
+//   (an i8): q*e = q_lo e_lo + 256 (q_lo e_hi + q_hi e_lo)  (mod 2^16), and
+//   sum x_lo y_lo = sum x'y' + 128 sum x' + 128 sum y' + 16384 K, so two i32
+//   accumulators of v_mfma_i32_32x32x32_i8 over pre-biased byte planes
+//     S1 = sum q'_lo e'_lo,  S2 = sum q'_lo e'_hi + q'_hi e'_lo
+//   plus per-row query sums (host) and per-share byte sums (the otherwise
+//   unused 32nd A row is all ones) recombine exactly mod 2^16.
+//   |S| <= 2 * 12800 * 128^2 < 2^31.
+#include <hip/hip_runtime.h>
+
+#include "iris_internal.hpp"
+
+namespace iris {
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v8i __attribute__((ext_vector_type(8)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+typedef float v16f __attribute__((ext_vector_type(16)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kTile = 32;
+constexpr int kMasksTiles = 4;   // tiles per wave
+constexpr int kSharesTiles = 2;
+
+__device__ __forceinline__ uint4 nt_load(const uint4 *p) {
+    const u32x4 v = __builtin_nontemporal_load((const u32x4 *)p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+struct Tiles {
+    uint64_t tile0, ntiles, grid;
+};
+
+static Tiles tiles_of(LaunchRange r, int per_wave) {
+    Tiles t;
+    t.tile0 = r.first / kTile;
+    const uint64_t tile1 = (r.first + r.n + kTile - 1) / kTile;
+    t.ntiles = tile1 - t.tile0;
+    const uint64_t waves = (t.ntiles + per_wave - 1) / per_wave;
+    t.grid = (waves + kWaveSlots - 1) / kWaveSlots;
+    return t;
+}
+
+// ------------------------------------------------------------------ masks (fp4)
+
+__device__ __forceinline__ v16f mfma_fp4(const v8i &a, const v8i &b, const v16f &c) {
+    return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, c, 4, 4, 0, 127, 0, 127);
+}
+
+__device__ __forceinline__ void mask_chunk(uint32_t x, const uint4 &q, v16f &acc) {
+    const v8i b = {(int)(x & 0x11111111u), (int)(x & 0x22222222u), (int)(x & 0x44444444u),
+                   (int)((x >> 1) & 0x44444444u), 0, 0, 0, 0};
+    const v8i a = {(int)q.x, (int)q.y, (int)q.z, (int)q.w, 0, 0, 0, 0};
+    acc = mfma_fp4(a, b, acc);
+}
+
+__global__ void __launch_bounds__(256, 2)
+    masks_mfma_kernel(const uint4 *__restrict__ db, const uint4 *__restrict__ qfrag, uint64_t tile0, uint64_t ntiles,
+                      uint64_t first, uint64_t end, uint16_t *__restrict__ out) {
+    constexpr int T = kMasksTiles;
+    constexpr int kSteps = kMaskChunks / 4;  // 50 steps of 4 chunks
+    const int lane = threadIdx.x & 63;
+    const uint64_t wave = (uint64_t)blockIdx.x * kWaveSlots + (threadIdx.x >> 6);
+    const uint64_t tw = wave * T;
+    if (tw >= ntiles) return;
+    v16f acc[T];
+#pragma unroll
+    for (int t = 0; t < T; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
+
+    const uint4 *dp[T];
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        const uint64_t rel = (tw + t < ntiles) ? tw + t : ntiles - 1;
+        dp[t] = db + (tile0 + rel) * (uint64_t)kMaskTileUint4 + lane;
+    }
+    const uint4 *qp = qfrag + lane;  // chunk c: qfrag[c * 64 + lane]
+    struct Stage {
+        uint4 d[T];
+        uint4 q[4];
+    };
+    auto load = [&](Stage &st, int g) {
+        g = g < kSteps ? g : kSteps - 1;
+#pragma unroll
+        for (int t = 0; t < T; ++t) st.d[t] = nt_load(dp[t] + g * 64);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) st.q[i] = qp[(4 * g + i) * 64];
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto compute = [&](const Stage &st) {
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+            mask_chunk(st.d[t].x, st.q[0], acc[t]);
+            mask_chunk(st.d[t].y, st.q[1], acc[t]);
+            mask_chunk(st.d[t].z, st.q[2], acc[t]);
+            mask_chunk(st.d[t].w, st.q[3], acc[t]);
+        }
+    };
+    Stage sa, sb, sc;
+    load(sa, 0);
+    load(sb, 1);
+    int g = 0;
+#pragma unroll 1
+    for (; g + 3 <= kSteps; g += 3) {
+        load(sc, g + 2);
+        compute(sa);
+        load(sa, g + 3);
+        compute(sb);
+        load(sb, g + 4);
+        compute(sc);
+    }
+    // 50 = 16 * 3 + 2: two steps left, in sa and sb
+    if (g < kSteps) compute(sa);
+    if (g + 1 < kSteps) compute(sb);
+
+    const int h = lane >> 5;
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        const uint64_t tg = (tile0 + tw + t) * kTile + (lane & 31);
+        if (tw + t >= ntiles || tg < first || tg >= end) continue;
+        const uint64_t o = tg - first;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int k = (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (k < kRot) out[o * kRot + k] = (uint16_t)(uint32_t)acc[t][r];
+        }
+    }
+}
+
+int launch_masks_mfma(void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *out) {
+    if (r.n == 0) return 0;
+    const Tiles t = tiles_of(r, kMasksTiles);
+    hipLaunchKernelGGL(masks_mfma_kernel, dim3((uint32_t)t.grid), dim3(256), 0, (hipStream_t)stream,
+                       (const uint4 *)db, (const uint4 *)qfrag, t.tile0, t.ntiles, r.first, r.first + r.n, out);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// ------------------------------------------------------------------ shares (i8)
+
+__device__ __forceinline__ v16i mfma_i8(const uint4 &a, const uint4 &b, const v16i &c) {
+    const v4i av = {(int)a.x, (int)a.y, (int)a.z, (int)a.w};
+    const v4i bv = {(int)b.x, (int)b.y, (int)b.z, (int)b.w};
+    return __builtin_amdgcn_mfma_i32_32x32x32_i8(av, bv, c, 0, 0, 0);
+}
+
+__global__ void __launch_bounds__(256, 2)
+    shares_mfma_kernel(const uint4 *__restrict__ db, const uint4 *__restrict__ qfrag, const int2 *__restrict__ qsum,
+                       uint64_t tile0, uint64_t ntiles, uint64_t first, uint64_t end, uint16_t *__restrict__ out) {
+    constexpr int T = kSharesTiles;
+    constexpr int kSteps = kShareChunks / 2;  // 200 steps of 2 chunks
+    const int lane = threadIdx.x & 63;
+    const uint64_t wave = (uint64_t)blockIdx.x * kWaveSlots + (threadIdx.x >> 6);
+    const uint64_t tw = wave * T;
+    if (tw >= ntiles) return;
+    v16i s1[T], s2[T];
+#pragma unroll
+    for (int t = 0; t < T; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            s1[t][i] = 0;
+            s2[t][i] = 0;
+        }
+    const uint4 *dp[T];
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        const uint64_t rel = (tw + t < ntiles) ? tw + t : ntiles - 1;
+        dp[t] = db + (tile0 + rel) * (uint64_t)kShareTileUint4 + lane;
+    }
+    const uint4 *qp = qfrag + lane;  // chunk c: lo [(2c) * 64 + lane], hi [(2c+1) * 64 + lane]
+    struct Stage {
+        uint4 lo[T][2], hi[T][2];
+        uint4 qlo[2], qhi[2];
+    };
+    auto load = [&](Stage &st, int g) {
+        g = g < kSteps ? g : kSteps - 1;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int c = 2 * g + i;
+#pragma unroll
+            for (int t = 0; t < T; ++t) {
+                st.lo[t][i] = nt_load(dp[t] + (2 * c) * 64);
+                st.hi[t][i] = nt_load(dp[t] + (2 * c + 1) * 64);
+            }
+            st.qlo[i] = qp[(2 * c) * 64];
+            st.qhi[i] = qp[(2 * c + 1) * 64];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto compute = [&](const Stage &st) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int t = 0; t < T; ++t) {
+                s1[t] = mfma_i8(st.qlo[i], st.lo[t][i], s1[t]);
+                s2[t] = mfma_i8(st.qlo[i], st.hi[t][i], s2[t]);
+                s2[t] = mfma_i8(st.qhi[i], st.lo[t][i], s2[t]);
+            }
+    };
+    Stage sa, sb, sc;
+    load(sa, 0);
+    load(sb, 1);
+    int g = 0;
+#pragma unroll 1
+    for (; g + 3 <= kSteps; g += 3) {
+        load(sc, g + 2);
+        compute(sa);
+        load(sa, g + 3);
+        compute(sb);
+        load(sb, g + 4);
+        compute(sc);
+    }
+    // 200 = 66 * 3 + 2
+    if (g < kSteps) compute(sa);
+    if (g + 1 < kSteps) compute(sb);
+
+    // row 31 (lane t + 32, register 15) holds sum e'_lo in S1 and sum e'_hi + sum e'_lo in S2
+    const int h = lane >> 5;
+    const int src = (lane & 31) + 32;
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        const int elo = __shfl(s1[t][15], src);
+        const int ehi = __shfl(s2[t][15], src) - elo;
+        const uint64_t tg = (tile0 + tw + t) * kTile + (lane & 31);
+        if (tw + t >= ntiles || tg < first || tg >= end) continue;
+        const uint64_t o = tg - first;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int k = (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (k >= kRot) continue;
+            const int2 qs = qsum[k];  // (sum q'_lo, sum q'_hi) of row k
+            // the 16384 * K terms vanish mod 2^16 (K = 12800)
+            const uint32_t lo = (uint32_t)s1[t][r] + 128u * (uint32_t)elo + 128u * (uint32_t)qs.x;
+            const uint32_t cross = (uint32_t)s2[t][r] + 128u * (uint32_t)ehi + 128u * (uint32_t)qs.x +
+                                   128u * (uint32_t)elo + 128u * (uint32_t)qs.y;
+            out[o * kRot + k] = (uint16_t)(lo + 256u * cross);
+        }
+    }
+}
+
+int launch_shares_mfma(void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *out) {
+    if (r.n == 0) return 0;
+    const Tiles t = tiles_of(r, kSharesTiles);
+    const int2 *qsum = (const int2 *)((const uint4 *)qfrag + kShareFragUint4);
+    hipLaunchKernelGGL(shares_mfma_kernel, dim3((uint32_t)t.grid), dim3(256), 0, (hipStream_t)stream,
+                       (const uint4 *)db, (const uint4 *)qfrag, qsum, t.tile0, t.ntiles, r.first, r.first + r.n, out);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// ------------------------------------------------------------------ TILES plumbing (masks, shares)
+
+// masks: thread per (record, step g, half h): mask dwords {8g+h, 8g+2+h, 8g+4+h, 8g+6+h}
+__global__ void __launch_bounds__(256) pack_masks_tiles(const uint32_t *__restrict__ staging, uint4 *__restrict__ db,
+                                                        uint64_t t_first, uint64_t n, int inverse) {
+    const uint64_t total = n * (uint64_t)(2 * (kMaskChunks / 4));
+    for (uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; tid < total;
+         tid += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t i = tid % n, gh = tid / n;
+        const int g = (int)(gh >> 1), h = (int)(gh & 1);
+        const uint64_t t = t_first + i;
+        uint4 *dst = db + (t / kTile) * (uint64_t)kMaskTileUint4 + (uint64_t)g * 64 + (t % kTile) + 32 * h;
+        uint32_t *rec = (uint32_t *)staging + i * kPlaneDwords;
+        const int w = 8 * g + h;
+        if (!inverse) {
+            *dst = make_uint4(rec[w], rec[w + 2], rec[w + 4], rec[w + 6]);
+        } else {
+            const uint4 v = *dst;
+            rec[w] = v.x;
+            rec[w + 2] = v.y;
+            rec[w + 4] = v.z;
+            rec[w + 6] = v.w;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) generate_masks_tiles(uint4 *__restrict__ db, uint64_t t_first, uint64_t n,
+                                                            uint64_t key, uint64_t global_index0) {
+    const uint64_t total = n * (uint64_t)(2 * (kMaskChunks / 4));
+    for (uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; tid < total;
+         tid += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t i = tid % n, gh = tid / n;
+        const int g = (int)(gh >> 1), h = (int)(gh & 1);
+        const uint64_t gt = global_index0 + i, t = t_first + i;
+        uint32_t v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = (uint32_t)(gen_limb(key, gt * 400 + 200 + 4 * g + q) >> (32 * h));
+        db[(t / kTile) * (uint64_t)kMaskTileUint4 + (uint64_t)g * 64 + (t % kTile) + 32 * h] =
+            make_uint4(v[0], v[1], v[2], v[3]);
+    }
+}
+
+// shares: thread per (record, chunk c, half h): elements 32c + 16h .. +15 -> lo / hi byte planes ^ 0x80
+__device__ __forceinline__ void split_bytes(const uint32_t *src8, uint4 &lo, uint4 &hi) {
+    uint32_t l[4], hh[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t a = src8[2 * q], b = src8[2 * q + 1];  // elements 4q..4q+3
+        l[q] = ((a & 0xFFu) | ((a >> 8) & 0xFF00u) | ((b & 0xFFu) << 16) | ((b << 8) & 0xFF000000u)) ^ 0x80808080u;
+        hh[q] = (((a >> 8) & 0xFFu) | ((a >> 16) & 0xFF00u) | (((b >> 8) & 0xFFu) << 16) | (b & 0xFF000000u)) ^
+                0x80808080u;
+    }
+    lo = make_uint4(l[0], l[1], l[2], l[3]);
+    hi = make_uint4(hh[0], hh[1], hh[2], hh[3]);
+}
+
+__device__ __forceinline__ void join_bytes(const uint4 &lo_, const uint4 &hi_, uint32_t *dst8) {
+    const uint32_t lo[4] = {lo_.x ^ 0x80808080u, lo_.y ^ 0x80808080u, lo_.z ^ 0x80808080u, lo_.w ^ 0x80808080u};
+    const uint32_t hi[4] = {hi_.x ^ 0x80808080u, hi_.y ^ 0x80808080u, hi_.z ^ 0x80808080u, hi_.w ^ 0x80808080u};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        dst8[2 * q] = (lo[q] & 0xFFu) | ((hi[q] & 0xFFu) << 8) | ((lo[q] & 0xFF00u) << 8) | ((hi[q] & 0xFF00u) << 16);
+        dst8[2 * q + 1] = ((lo[q] >> 16) & 0xFFu) | ((hi[q] >> 8) & 0xFF00u) | ((lo[q] >> 8) & 0xFF0000u) |
+                          (hi[q] & 0xFF000000u);
+    }
+}
+
+__global__ void __launch_bounds__(256) pack_shares_tiles(const uint32_t *__restrict__ staging, uint4 *__restrict__ db,
+                                                         uint64_t t_first, uint64_t n, int inverse) {
+    const uint64_t total = n * (uint64_t)(2 * kShareChunks);
+    for (uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; tid < total;
+         tid += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t i = tid % n, ch = tid / n;
+        const int c = (int)(ch >> 1), h = (int)(ch & 1);
+        const uint64_t t = t_first + i;
+        uint4 *base = db + (t / kTile) * (uint64_t)kShareTileUint4 + (t % kTile) + 32 * h;
+        uint32_t *rec = (uint32_t *)staging + i * kShareDwords + (32 * c + 16 * h) / 2;
+        if (!inverse) {
+            uint4 lo, hi;
+            split_bytes(rec, lo, hi);
+            base[(2 * c) * 64] = lo;
+            base[(2 * c + 1) * 64] = hi;
+        } else {
+            join_bytes(base[(2 * c) * 64], base[(2 * c + 1) * 64], rec);
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) generate_shares_tiles(uint4 *__restrict__ db, uint64_t t_first, uint64_t n,
+                                                             uint64_t key, uint64_t global_index0) {
+    const uint64_t total = n * (uint64_t)(2 * kShareChunks);
+    for (uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; tid < total;
+         tid += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t i = tid % n, ch = tid / n;
+        const int c = (int)(ch >> 1), h = (int)(ch & 1);
+        const uint64_t gt = global_index0 + i, t = t_first + i;
+        uint32_t src[8];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {  // limbs (32c + 16h)/4 + q, 4 u16 each
+            const uint64_t v = gen_limb(key, gt * 3200 + 8 * c + 4 * h + q);
+            src[2 * q] = (uint32_t)v;
+            src[2 * q + 1] = (uint32_t)(v >> 32);
+        }
+        uint4 lo, hi;
+        split_bytes(src, lo, hi);
+        uint4 *base = db + (t / kTile) * (uint64_t)kShareTileUint4 + (t % kTile) + 32 * h;
+        base[(2 * c) * 64] = lo;
+        base[(2 * c + 1) * 64] = hi;
+    }
+}
+
+static int plumb_grid(uint64_t total) {
+    uint64_t b = (total + 255) / 256;
+    if (b > 256ull * 64) b = 256ull * 64;
+    return (int)(b ? b : 1);
+}
+
+int launch_pack_tiles_kind(void *stream, int kind, const void *staging, void *db, uint64_t t_first, uint64_t n) {
+    if (n == 0) return 0;
+    hipStream_t s = (hipStream_t)stream;
+    if (kind == IRIS_KIND_TEMPLATES) return launch_pack_tiles(stream, staging, db, t_first, n);
+    if (kind == IRIS_KIND_MASKS)
+        hipLaunchKernelGGL(pack_masks_tiles, dim3(plumb_grid(n * kMaskChunks / 2)), dim3(256), 0, s,
+                           (const uint32_t *)staging, (uint4 *)db, t_first, n, 0);
+    else
+        hipLaunchKernelGGL(pack_shares_tiles, dim3(plumb_grid(n * 2 * kShareChunks)), dim3(256), 0, s,
+                           (const uint32_t *)staging, (uint4 *)db, t_first, n, 0);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_unpack_tiles_kind(void *stream, int kind, const void *db, void *staging, uint64_t t_first, uint64_t n) {
+    if (n == 0) return 0;
+    hipStream_t s = (hipStream_t)stream;
+    if (kind == IRIS_KIND_TEMPLATES) return launch_unpack_tiles(stream, db, staging, t_first, n);
+    if (kind == IRIS_KIND_MASKS)
+        hipLaunchKernelGGL(pack_masks_tiles, dim3(plumb_grid(n * kMaskChunks / 2)), dim3(256), 0, s,
+                           (const uint32_t *)staging, (uint4 *)db, t_first, n, 1);
+    else
+        hipLaunchKernelGGL(pack_shares_tiles, dim3(plumb_grid(n * 2 * kShareChunks)), dim3(256), 0, s,
+                           (const uint32_t *)staging, (uint4 *)db, t_first, n, 1);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_generate_tiles_kind(void *stream, int kind, void *db, uint64_t t_first, uint64_t n, uint64_t seed,
+                               uint64_t global_index0) {
+    if (n == 0) return 0;
+    hipStream_t s = (hipStream_t)stream;
+    if (kind == IRIS_KIND_TEMPLATES) return launch_generate_tiles(stream, db, t_first, n, seed, global_index0);
+    if (kind == IRIS_KIND_MASKS)
+        hipLaunchKernelGGL(generate_masks_tiles, dim3(plumb_grid(n * kMaskChunks / 2)), dim3(256), 0, s, (uint4 *)db,
+                           t_first, n, gen_key(seed, 0), global_index0);
+    else
+        hipLaunchKernelGGL(generate_shares_tiles, dim3(plumb_grid(n * 2 * kShareChunks)), dim3(256), 0, s,
+                           (uint4 *)db, t_first, n, gen_key(seed, 1), global_index0);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace iris

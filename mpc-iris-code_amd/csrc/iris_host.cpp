@@ -133,3 +133,50 @@ void build_template_frags(const iris_template_t *q, uint32_t *frag) {
 }
 
 }  // namespace iris
+
+namespace iris {
+
+// fp4 A-fragments of masks_mfma_kernel: row k = vectors[k] (rotations for
+// MasksEngine, arbitrary vectors for dot_bool); value 2 / 1 / 0.5 / 0.5 by
+// fragment dword, matching the template-side 0.5 / 1 / 2 / 2 (iris_internal.hpp).
+void build_masks_frags(const uint64_t *const *vectors, int count, uint32_t *frag) {
+    static const uint32_t code[4] = {0x4u, 0x2u, 0x1u, 0x1u};
+    memset(frag, 0, sizeof(uint32_t) * 4 * kMaskFragUint4);
+    for (int k = 0; k < count && k < kRot; ++k)
+        for (int c = 0; c < kMaskChunks; ++c)
+            for (int h = 0; h < 2; ++h) {
+                const uint32_t x = dword_of(vectors[k], 2 * c + h);
+                uint32_t *f = frag + ((size_t)c * 64 + k + 32 * h) * 4;
+                for (int j = 0; j < 32; ++j)
+                    if ((x >> mask_frag_bit(j)) & 1u) f[j / 8] |= code[j / 8] << (4 * (j % 8));
+            }
+}
+
+// i8 A-fragments of shares_mfma_kernel: low / high bytes of row k's elements
+// minus 128; row 31 is all ones (per-share byte sums).  After the fragments:
+// 32 int2 row constants (sum of biased low bytes, sum of biased high bytes).
+void build_shares_frags(const uint16_t *const *vectors, int count, uint32_t *frag) {
+    memset(frag, 0, sizeof(uint32_t) * 4 * kShareFragUint4 + 32 * 8);
+    int32_t *qsum = (int32_t *)(frag + 4 * kShareFragUint4);
+    uint8_t *bytes = (uint8_t *)frag;
+    for (int c = 0; c < kShareChunks; ++c)
+        for (int h = 0; h < 2; ++h)
+            for (int k = 0; k < 32; ++k) {
+                uint8_t *lo = bytes + (((size_t)(2 * c) * 64) + k + 32 * h) * 16;
+                uint8_t *hi = bytes + (((size_t)(2 * c + 1) * 64) + k + 32 * h) * 16;
+                for (int j = 0; j < 16; ++j) {
+                    if (k == 31) {
+                        lo[j] = 1;
+                        hi[j] = 1;
+                    } else if (k < count) {
+                        const uint16_t e = vectors[k][32 * c + 16 * h + j];
+                        lo[j] = (uint8_t)((e & 0xFFu) ^ 0x80u);
+                        hi[j] = (uint8_t)((e >> 8) ^ 0x80u);
+                        qsum[2 * k] += (int8_t)lo[j];
+                        qsum[2 * k + 1] += (int8_t)hi[j];
+                    }
+                }
+            }
+}
+
+}  // namespace iris

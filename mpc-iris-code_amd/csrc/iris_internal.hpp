@@ -59,8 +59,12 @@ inline KindInfo kind_info(int kind, int layout = IRIS_LAYOUT_LANES) {
     case IRIS_KIND_TEMPLATES:
         if (layout == IRIS_LAYOUT_TILES) return {kind, layout, 32, kPlaneGroups, 2, 2 * kPlaneDwords, {kPlaneDwords, 0}, 3200};
         return {kind, IRIS_LAYOUT_LANES, 64, 2 * kPlaneGroups, 2, 2 * kPlaneDwords, {kPlaneDwords, 0}, 3200};
-    case IRIS_KIND_MASKS: return {kind, IRIS_LAYOUT_LANES, 64, kPlaneGroups, 1, kPlaneDwords, {0, 0}, 1600};
-    case IRIS_KIND_SHARES: return {kind, IRIS_LAYOUT_LANES, 64, kShareGroups, 1, kShareDwords, {0, 0}, 25600};
+    case IRIS_KIND_MASKS:
+        if (layout == IRIS_LAYOUT_TILES) return {kind, layout, 32, kPlaneGroups / 2, 1, kPlaneDwords, {0, 0}, 1600};
+        return {kind, IRIS_LAYOUT_LANES, 64, kPlaneGroups, 1, kPlaneDwords, {0, 0}, 1600};
+    case IRIS_KIND_SHARES:
+        if (layout == IRIS_LAYOUT_TILES) return {kind, layout, 32, kShareDwords / 16, 2, kShareDwords, {0, 0}, 25600};
+        return {kind, IRIS_LAYOUT_LANES, 64, kShareGroups, 1, kShareDwords, {0, 0}, 25600};
     default: return {0, 0, 0, 0, 0, 0, {0, 0}, 0};
     }
 }
@@ -101,6 +105,26 @@ IRIS_HD inline int frag_bit(int j) { return (j & 16) + 2 * (j & 7) + ((j >> 3) &
 // plane dword 2c + h (+1.0 = 0x2, -1.0 = 0xA, 0).  The den operand is derived
 // from it in-kernel (|enc|, doubled where the template side carries 0.5).
 constexpr int kFragDwords = 4;
+
+// TILES layouts of the other kinds (iris_mfma.hip):
+//  MASKS  (fp4, den only): tile of 32 masks = 3200 uint4.  uint4 [g*64 + L]
+//    (g = 0..49, L = t + 32h) = mask dwords {8g+h, 8g+2+h, 8g+4+h, 8g+6+h}, i.e.
+//    the lane's dword of chunks 4g..4g+3.  Fragment dword d of a chunk is
+//    x & (0x11111111 << d) for d < 3 and (x >> 1) & 0x44444444 for d = 3, so
+//    K index j <-> mask bit 4 (j % 8) + j / 8 with template-side value
+//    0.5 / 1 / 2 / 2 and query-side value 2 / 1 / 0.5 / 0.5.
+//  SHARES (i8): tile of 32 shares = 51200 uint4.  For chunk c (elements
+//    [32c, 32c+32)) and lane L = t + 32h: uint4 [(2c) * 64 + L] = low bytes,
+//    [(2c+1) * 64 + L] = high bytes of elements 32c + 16h + j (j = 0..15), each
+//    XOR 0x80 (the byte minus 128 as an i8), the B fragment of
+//    v_mfma_i32_32x32x32_i8 (lane l holds K = 16 (l >> 5) + j).
+constexpr int kMaskTileUint4 = (kPlaneGroups / 2) * 64;   // 3200
+constexpr int kShareTileUint4 = (kShareDwords / 16) * 2 * 64;  // 51200
+constexpr int kMaskChunks = kPlaneDwords / 2;   // 200 chunks of 64 bits
+constexpr int kShareChunks = IRIS_BITS / 32;    // 400 chunks of 32 elements
+constexpr size_t kMaskFragUint4 = (size_t)kMaskChunks * 64;
+constexpr size_t kShareFragUint4 = (size_t)kShareChunks * 64 * 2;  // + 32 int2 row constants after it
+IRIS_HD inline int mask_frag_bit(int j) { return 4 * (j & 7) + (j >> 3); }
 constexpr size_t kTemplateFragDwords = (size_t)(kPlaneDwords / 2) * 64 * kFragDwords;  // 200 chunks
 
 // Rotated-query tables (built on the host, uploaded once per engine):
@@ -158,6 +182,12 @@ uint32_t mfma_search_partials(LaunchRange r);
 int launch_pack_tiles(void *stream, const void *staging, void *db, uint64_t t_first, uint64_t n);
 int launch_unpack_tiles(void *stream, const void *db, void *staging, uint64_t t_first, uint64_t n);
 int launch_generate_tiles(void *stream, void *db, uint64_t t_first, uint64_t n, uint64_t seed, uint64_t global_index0);
+int launch_pack_tiles_kind(void *stream, int kind, const void *staging, void *db, uint64_t t_first, uint64_t n);
+int launch_unpack_tiles_kind(void *stream, int kind, const void *db, void *staging, uint64_t t_first, uint64_t n);
+int launch_generate_tiles_kind(void *stream, int kind, void *db, uint64_t t_first, uint64_t n, uint64_t seed,
+                               uint64_t global_index0);
+int launch_masks_mfma(void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *out);
+int launch_shares_mfma(void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *out);
 int launch_template_search(void *stream, const void *db, const void *qtab, LaunchRange r, double *dist_out,
                            Partial *partials, uint32_t *n_partials);
 int launch_reduce(void *stream, const Partial *partials, uint32_t n_partials, Partial *out);
@@ -173,6 +203,8 @@ void encoded_rotated(const uint16_t *in, int amount, uint16_t *out);
 void encode_template(const iris_template_t *t, uint16_t *out);
 void build_template_table(const iris_template_t *q, uint32_t *tab);                  // 400*64 dwords
 void build_template_frags(const iris_template_t *q, uint32_t *frag);                 // kTemplateFragDwords
+void build_masks_frags(const uint64_t *const *vectors, int count, uint32_t *frag);    // kMaskFragUint4 uint4
+void build_shares_frags(const uint16_t *const *vectors, int count, uint32_t *frag);   // kShareFragUint4 uint4 + 64 int
 void build_masks_table(const uint64_t *const *vectors, int count, uint32_t *tab);     // 400*32
 void build_shares_table(const uint16_t *const *vectors, int count, uint32_t *tab);    // 6400*32
 void build_masks_rotations(const uint64_t *query, uint32_t *tab);

@@ -100,6 +100,7 @@ def load_library(path=None):
             "iris_engine_destroy": ([P], ctypes.c_int),
             "iris_engine_batch_process": ([P, P, u64, u64, P], ctypes.c_int),
             "iris_engine_batch_process_host": ([P, P, u64, P], ctypes.c_int),
+            "iris_engine_batch_process_device": ([P, P, u64, u64, P], ctypes.c_int),
             "iris_template_counts": ([P, P, u64, u64, P, P], ctypes.c_int),
             "iris_template_distances": ([P, P, u64, u64, P], ctypes.c_int),
             "iris_template_search": ([P, P, u64, u64, u64, P, ctypes.POINTER(Match)], ctypes.c_int),
@@ -129,7 +130,7 @@ def exported_symbols():
         "iris_db_destroy", "iris_db_len", "iris_db_capacity", "iris_db_kind", "iris_db_append", "iris_db_write",
         "iris_db_read", "iris_db_generate", "iris_db_clear", "iris_masks_engine_new", "iris_distance_engine_new",
         "iris_template_engine_new", "iris_engine_destroy", "iris_engine_batch_process",
-        "iris_engine_batch_process_host", "iris_template_counts", "iris_template_distances", "iris_template_search",
+        "iris_engine_batch_process_host", "iris_engine_batch_process_device", "iris_template_counts", "iris_template_distances", "iris_template_search",
         "iris_dot_bool_batch", "iris_dot_u16_batch", "iris_bits_rotated", "iris_encoded_rotated", "iris_encode",
         "iris_decode_distance", "iris_match_merge",
     ]
@@ -530,6 +531,16 @@ class _Engine:
                 raise IrisError(-1, f"assertion `out.len() == db.len()` failed: {out.shape[0]} != {a.shape[0]}")
             _check(lib.iris_engine_batch_process_host(self.handle, _ptr(a), a.shape[0], _ptr(out)))
         return out
+
+
+def _batch_process_device(self, db, out_device_ptr, first=0, n=None):
+    """Results stay on the GPU: out_device_ptr is a device array of n*31 u16."""
+    n = (len(db) - first) if n is None else n
+    _check(load_library().iris_engine_batch_process_device(self.handle, db.handle, int(first), int(n),
+                                                           ctypes.c_void_p(out_device_ptr)))
+
+
+_Engine.batch_process_device = _batch_process_device
 
 
 class MasksEngine(_Engine):

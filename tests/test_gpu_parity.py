@@ -53,15 +53,29 @@ def test_layouts_agree(device):
     assert (m0.index, m0.num, m0.den, m0.rotation) == (m1.index, m1.num, m1.den, m1.rotation)
 
 
-def test_generate_matches_oracle(device, tdb):
+def test_generate_matches_oracle(device, tdb, layout):
     got = tdb.read(0, 1000)
     assert (got == oc.gen_templates(SEED, 0, 1000)).all()
-    with ih.Database(device, ih.KIND_MASKS, 200) as m:
+    with ih.Database(device, ih.KIND_MASKS, 200, layout) as m:
         m.generate(130, SEED, global_index0=500)
         assert (m.read(0, 130) == oc.gen_masks(SEED, 500, 130)).all()
-    with ih.Database(device, ih.KIND_SHARES, 100) as s:
+    with ih.Database(device, ih.KIND_SHARES, 100, layout) as s:
         s.generate(70, SEED)
         assert (s.read(0, 70) == oc.gen_shares(SEED, 0, 70)).all()
+
+
+def test_masks_shares_roundtrip(device, layout):
+    rng = np.random.default_rng(4)
+    masks = rng.integers(0, 2**64, (77, 200), dtype=np.uint64)
+    shares = rng.integers(0, 2**16, (45, 12800), dtype=np.uint16)
+    with ih.Database(device, ih.KIND_MASKS, 100, layout) as m:
+        m.append(masks)
+        assert (m.read(0, 77) == masks).all()
+        m.write(33, masks[:2])
+        assert (m.read(33, 2) == masks[:2]).all()
+    with ih.Database(device, ih.KIND_SHARES, 64, layout) as s:
+        s.append(shares)
+        assert (s.read(0, 45) == shares).all()
 
 
 def test_append_write_read_roundtrip(device, layout):
@@ -185,13 +199,13 @@ def test_template_distance_value_type(device, golden):
 # ---------------------------------------------------------------- MasksEngine / DistanceEngine
 
 
-def test_masks_engine(device, golden):
+def test_masks_engine(device, golden, layout):
     q, db_ref = golden["query"], golden["db"]
     with ih.MasksEngine(device, q[200:]) as eng:
         out = np.empty((db_ref.shape[0], ROT), np.uint16)
         eng.batch_process(out, db_ref[:, 200:])  # host slice, reference signature
         assert (out == golden["masks_out"]).all()
-        with ih.Database(device, ih.KIND_MASKS, 2000) as db:
+        with ih.Database(device, ih.KIND_MASKS, 2000, layout) as db:
             db.generate(1999, 5)
             ref = db.read(0, 1999)
             out = np.empty((1999, ROT), np.uint16)
@@ -204,19 +218,45 @@ def test_masks_engine(device, golden):
             eng.batch_process(np.empty((3, ROT), np.uint16), db_ref[:2, 200:])
 
 
-def test_distance_engine(device, golden):
+def test_distance_engine(device, golden, layout):
     enc_q = golden["enc_query"]
     with ih.DistanceEngine(device, enc_q) as eng:
         for k in range(3):
             out = np.empty((golden["shares"].shape[1], ROT), np.uint16)
             eng.batch_process(out, golden["shares"][k])
             assert (out == golden["share_out"][k]).all()
-        with ih.Database(device, ih.KIND_SHARES, 300) as db:
+        with ih.Database(device, ih.KIND_SHARES, 300, layout) as db:
             db.generate(257, 8)
             ref = db.read(0, 257)
+            assert (ref == oc.gen_shares(8, 0, 257)).all()
             out = np.empty((257, ROT), np.uint16)
             eng.batch_process(out, db)
             assert (out == oc.distance_batch(enc_q, ref)).all()
+            out2 = np.empty((100, ROT), np.uint16)
+            eng.batch_process(out2, db, first=157, n=100)
+            assert (out2 == oc.distance_batch(enc_q, ref[157:])).all()
+
+
+def test_distance_engine_arbitrary_query(device, layout):
+    """DistanceEngine::new accepts any EncodedBits, not only encode() output:
+    uniform u16 query and shares, plus the all-0xFFFF wraparound case."""
+    rng = np.random.default_rng(12)
+    q = rng.integers(0, 2**16, 12800, dtype=np.uint16)
+    shares = rng.integers(0, 2**16, (70, 12800), dtype=np.uint16)
+    shares[5] = 0xFFFF
+    with ih.DistanceEngine(device, q) as eng, ih.Database(device, ih.KIND_SHARES, 70, layout) as db:
+        db.append(shares)
+        out = np.empty((70, ROT), np.uint16)
+        eng.batch_process(out, db)
+        assert (out == oc.distance_batch(q, shares)).all()
+        ptr = device.alloc(70 * ROT * 2)
+        try:
+            eng.batch_process_device(db, ptr)
+            dev_out = np.empty((70, ROT), np.uint16)
+            device.d2h(dev_out, ptr)
+        finally:
+            device.free(ptr)
+        assert (dev_out == out).all()
 
 
 def test_resolver_decode_matches_template_distance(device, golden):
