@@ -171,6 +171,20 @@ int iris_template_distances(iris_engine_t *engine, const iris_db_t *db, uint64_t
 int iris_template_search(iris_engine_t *engine, const iris_db_t *db, uint64_t first, uint64_t n,
                          uint64_t index_base, double *dist_out_device, iris_match_t *out);
 
+/* ---------------------------------------------------------------- resolver
+ * The resolver's aggregation (src/main.rs:597-621) fused on the GPU: for each
+ * entry i, num = wrapping sum over the `parts` participants' [u16;31] shares,
+ * decode_distance(num, denoms[i]) (src/lib.rs:97-107), then the first entry
+ * with a strictly smaller distance.  out->index = index_base + i, out->num =
+ * the decoded uneq count, out->den = the denominator.  At most 8 parts.
+ * Device form: all arrays are DEVICE arrays of n*31 uint16_t.            */
+int iris_resolver_search(iris_device_t *dev, const uint16_t *const *shares_device, uint32_t parts,
+                         const uint16_t *denoms_device, uint64_t n, uint64_t index_base, double *dist_out_device,
+                         iris_match_t *out);
+/* Host form: shares[p] and denoms are host arrays (uploaded in chunks). */
+int iris_resolver_search_host(iris_device_t *dev, const uint16_t *const *shares, uint32_t parts,
+                              const uint16_t *denoms, uint64_t n, uint64_t index_base, iris_match_t *out);
+
 /* ------------------------------------------------------------ arch plugin
  * The reference's backend plugin point (src/arch/mod.rs:5):
  *   dot_bool(&[u64;200], &[u64;200]) -> u16   src/arch/generic.rs:4-9

@@ -755,6 +755,86 @@ int iris_template_distances(iris_engine_t *e, const iris_db_t *db, uint64_t firs
     return 0;
 }
 
+// ------------------------------------------------------------------ resolver
+
+static int resolver_finish(iris_device *d, uint32_t np, Partial *res) {
+    if (np) {
+        CHK(timed(d, "reduce", np, [&] { return launch_reduce(d->stream, (Partial *)d->partials.p, np, (Partial *)d->result.p); }));
+        HIPCHK(hipMemcpyAsync(res, d->result.p, sizeof(Partial), hipMemcpyDeviceToHost, d->stream));
+    }
+    return sync(d);
+}
+
+static void match_from(const Partial &r, bool any, uint64_t base, iris_match_t *out) {
+    if (!any || r.den == 0) {
+        out->distance = INFINITY;
+        out->index = UINT64_MAX;
+        out->num = 0;
+        out->den = 0;
+        out->rotation = 0;
+    } else {
+        out->distance = (double)r.num / (double)r.den;
+        out->index = base + r.idx;
+        out->num = r.num;
+        out->den = r.den;
+        out->rotation = r.rot - IRIS_MAX_ROTATION;
+    }
+    out->reserved = 0;
+}
+
+// Partial.idx values of one launch are row indices of that launch; chunked
+// host calls merge the per-chunk winners on the host in chunk order.
+int iris_resolver_search(iris_device_t *d, const uint16_t *const *shares, uint32_t parts, const uint16_t *denoms,
+                         uint64_t n, uint64_t index_base, double *dist_out_device, iris_match_t *out) {
+    ARG(d && out, "NULL argument");
+    ARG(parts >= 1 && parts <= 8, "parts must be 1..8");
+    ARG(n == 0 || (shares && denoms), "NULL argument");
+    for (uint32_t p = 0; n && p < parts; ++p) ARG(shares[p], "NULL share array");
+    std::lock_guard<std::recursive_mutex> g(d->mu);
+    CHK(set_device(d));
+    const uint32_t np = resolver_partials(n);
+    CHK(ensure(d->partials, (size_t)std::max<uint32_t>(np, 1) * sizeof(Partial)));
+    CHK(ensure(d->result, sizeof(Partial)));
+    CHK(timed(d, "resolver", n, [&] {
+        return launch_resolver(d->stream, shares, parts, denoms, n, dist_out_device, (Partial *)d->partials.p);
+    }));
+    Partial res{};
+    CHK(resolver_finish(d, n ? np : 0, &res));
+    match_from(res, n > 0, index_base, out);
+    return 0;
+}
+
+int iris_resolver_search_host(iris_device_t *d, const uint16_t *const *shares, uint32_t parts, const uint16_t *denoms,
+                              uint64_t n, uint64_t index_base, iris_match_t *out) {
+    ARG(d && out, "NULL argument");
+    ARG(parts >= 1 && parts <= 8, "parts must be 1..8");
+    ARG(n == 0 || (shares && denoms), "NULL argument");
+    std::lock_guard<std::recursive_mutex> g(d->mu);
+    CHK(set_device(d));
+    const uint64_t ch = std::min<uint64_t>(n, 1ull << 20);
+    const size_t row = (size_t)kRot * 2;
+    CHK(ensure(d->staging, std::max<uint64_t>(ch, 1) * row * (parts + 1)));
+    iris_match_t best;
+    match_from(Partial{}, false, 0, &best);
+    for (uint64_t done = 0; done < n; done += ch) {
+        const uint64_t m = std::min<uint64_t>(ch, n - done);
+        const uint16_t *dev_sh[8];
+        for (uint32_t p = 0; p < parts; ++p) {
+            uint16_t *dst = (uint16_t *)((char *)d->staging.p + (size_t)p * ch * row);
+            HIPCHK(hipMemcpyAsync(dst, shares[p] + done * kRot, m * row, hipMemcpyHostToDevice, d->stream));
+            dev_sh[p] = dst;
+        }
+        uint16_t *dden = (uint16_t *)((char *)d->staging.p + (size_t)parts * ch * row);
+        HIPCHK(hipMemcpyAsync(dden, denoms + done * kRot, m * row, hipMemcpyHostToDevice, d->stream));
+        iris_match_t cm;
+        CHK(iris_resolver_search(d, dev_sh, parts, dden, m, index_base + done, nullptr, &cm));
+        iris_match_t pair[2] = {best, cm};
+        CHK(iris_match_merge(pair, 2, &best));
+    }
+    *out = best;
+    return 0;
+}
+
 // ------------------------------------------------------------------ arch plugin
 
 int iris_dot_bool_batch(iris_device_t *d, const uint64_t *a, uint64_t na, const uint64_t *b, uint64_t nb,

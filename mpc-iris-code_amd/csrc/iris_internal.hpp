@@ -187,6 +187,9 @@ int launch_unpack_tiles_kind(void *stream, int kind, const void *db, void *stagi
 int launch_generate_tiles_kind(void *stream, int kind, void *db, uint64_t t_first, uint64_t n, uint64_t seed,
                                uint64_t global_index0);
 int launch_masks_mfma(void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *out);
+uint32_t resolver_partials(uint64_t n);
+int launch_resolver(void *stream, const uint16_t *const *shares, uint32_t parts, const uint16_t *denoms, uint64_t n,
+                    double *dist_out, Partial *partials);
 int launch_shares_mfma(void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *out);
 int launch_template_search(void *stream, const void *db, const void *qtab, LaunchRange r, double *dist_out,
                            Partial *partials, uint32_t *n_partials);

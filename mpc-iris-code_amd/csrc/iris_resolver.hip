@@ -1,0 +1,131 @@
+// iris_resolver.hip — the resolver's combine + decode + argmin, fused on the GPU.
+//
+// Reference: src/main.rs:597-621.  For every entry i the resolver sums the
+// participants' [u16;31] shares with wrapping adds (:603-607), decodes with
+// decode_distance (src/lib.rs:97-107: uneq = (den - num) / 2 in u16, value
+// uneq as f64 / den as f64, fold(INF, f64::min)), then keeps the first entry
+// with a strictly smaller distance (:616-621).
+//
+// Exactness: uneq <= 32767 and den <= 65535, so fractions compare exactly by
+// u32 cross-multiplication; distinct fractions are distinct f64 values, so the
+// exact order is the reference's f64 order.  den = 0 gives NaN or +inf in the
+// reference, which never wins a f64::min or a strict <; here it is "no
+// candidate".  The winner's f64 is computed once with IEEE division.
+#include <hip/hip_runtime.h>
+
+#include "iris_internal.hpp"
+
+namespace iris {
+
+constexpr int kMaxParts = 8;
+constexpr int kWaveRows = 64;
+
+struct ResolverArgs {
+    const uint16_t *shares[kMaxParts];
+    uint32_t parts;
+};
+
+__device__ __forceinline__ bool res_better(const Partial &a, const Partial &b) {
+    if (a.den == 0) return false;
+    if (b.den == 0) return true;
+    const uint32_t l = a.num * b.den, r = b.num * a.den;  // <= 32767 * 65535 < 2^32
+    if (l != r) return l < r;
+    return a.idx < b.idx;
+}
+
+__device__ __forceinline__ Partial res_shfl(const Partial &c, int off) {
+    Partial o;
+    o.num = __shfl_xor(c.num, off);
+    o.den = __shfl_xor(c.den, off);
+    o.rot = __shfl_xor(c.rot, off);
+    o.pad = 0;
+    const uint32_t lo = __shfl_xor((uint32_t)c.idx, off), hi = __shfl_xor((uint32_t)(c.idx >> 32), off);
+    o.idx = ((uint64_t)hi << 32) | lo;
+    return o;
+}
+
+// Stage one wave's 64 rows of a [n][31] u16 array into LDS with dword loads
+// when the wave's byte range is 4-aligned (always, for n multiple of 2 rows).
+__device__ __forceinline__ void stage_rows(const uint16_t *__restrict__ src, uint64_t row0, uint64_t rows,
+                                           uint16_t *lds, int lane) {
+    const uint64_t e0 = row0 * kRot, ne = rows * kRot;
+    if ((e0 & 1) == 0) {
+        const uint32_t *s32 = (const uint32_t *)(src + e0);
+        const uint32_t ndw = (uint32_t)(ne / 2);
+        for (uint32_t i = lane; i < ndw; i += 64) ((uint32_t *)lds)[i] = s32[i];
+        if ((ne & 1) && lane == 0) lds[ne - 1] = src[e0 + ne - 1];
+    } else {
+        for (uint32_t i = lane; i < ne; i += 64) lds[i] = src[e0 + i];
+    }
+}
+
+__global__ void __launch_bounds__(256) resolver_kernel(ResolverArgs a, const uint16_t *__restrict__ denoms,
+                                                       uint64_t n, double *__restrict__ dist_out,
+                                                       Partial *__restrict__ partials) {
+    __shared__ uint16_t sh_num[kWaveSlots][kWaveRows * kRot + 2];
+    __shared__ uint16_t sh_den[kWaveSlots][kWaveRows * kRot + 2];
+    __shared__ Partial sh_best[kWaveSlots];
+    const int lane = threadIdx.x & 63, ws = threadIdx.x >> 6;
+    const uint64_t row0 = ((uint64_t)blockIdx.x * kWaveSlots + ws) * kWaveRows;
+    const uint64_t rows = row0 < n ? ((n - row0) < kWaveRows ? n - row0 : kWaveRows) : 0;
+    Partial c;
+    c.num = 0;
+    c.den = 0;
+    c.rot = 0;
+    c.pad = 0;
+    c.idx = row0 + lane;
+    // wrapping sum of the shares, in LDS (src/main.rs:603-607)
+    stage_rows(denoms, row0, rows, sh_den[ws], lane);
+    stage_rows(a.shares[0], row0, rows, sh_num[ws], lane);
+    __syncthreads();
+    for (uint32_t p = 1; p < a.parts; ++p) {
+        const uint64_t e0 = row0 * kRot, ne = rows * kRot;
+        for (uint32_t i = lane; i < ne; i += 64) sh_num[ws][i] = (uint16_t)(sh_num[ws][i] + a.shares[p][e0 + i]);
+    }
+    __syncthreads();
+    if ((uint64_t)lane < rows) {
+        const uint16_t *nr = sh_num[ws] + lane * kRot, *dr = sh_den[ws] + lane * kRot;
+#pragma unroll
+        for (int k = 0; k < kRot; ++k) {
+            const uint32_t d = dr[k];
+            const uint32_t u = (uint16_t)(d - nr[k]) >> 1;  // src/lib.rs:104
+            if (d != 0 && (c.den == 0 || u * c.den < c.num * d)) {
+                c.num = u;
+                c.den = d;
+                c.rot = k;
+            }
+        }
+        if (dist_out) dist_out[row0 + lane] = c.den ? (double)c.num / (double)c.den : __builtin_inf();
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const Partial o = res_shfl(c, off);
+        if (res_better(o, c)) c = o;
+    }
+    if (lane == 0) sh_best[ws] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        Partial b = sh_best[0];
+        for (int w = 1; w < kWaveSlots; ++w)
+            if (res_better(sh_best[w], b)) b = sh_best[w];
+        partials[blockIdx.x] = b;
+    }
+}
+
+uint32_t resolver_partials(uint64_t n) {
+    return (uint32_t)((n + kWaveRows * kWaveSlots - 1) / (kWaveRows * kWaveSlots));
+}
+
+int launch_resolver(void *stream, const uint16_t *const *shares, uint32_t parts, const uint16_t *denoms, uint64_t n,
+                    double *dist_out, Partial *partials) {
+    if (n == 0) return 0;
+    if (parts == 0 || parts > (uint32_t)kMaxParts) return -1;
+    ResolverArgs a{};
+    for (uint32_t p = 0; p < parts; ++p) a.shares[p] = shares[p];
+    a.parts = parts;
+    hipLaunchKernelGGL(resolver_kernel, dim3(resolver_partials(n)), dim3(256), 0, (hipStream_t)stream, a, denoms, n,
+                       dist_out, partials);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace iris

@@ -104,6 +104,10 @@ def load_library(path=None):
             "iris_template_counts": ([P, P, u64, u64, P, P], ctypes.c_int),
             "iris_template_distances": ([P, P, u64, u64, P], ctypes.c_int),
             "iris_template_search": ([P, P, u64, u64, u64, P, ctypes.POINTER(Match)], ctypes.c_int),
+            "iris_resolver_search": ([P, ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint32, P, u64, u64, P,
+                                      ctypes.POINTER(Match)], ctypes.c_int),
+            "iris_resolver_search_host": ([P, ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint32, P, u64, u64,
+                                           ctypes.POINTER(Match)], ctypes.c_int),
             "iris_dot_bool_batch": ([P, P, u64, P, u64, P], ctypes.c_int),
             "iris_dot_u16_batch": ([P, P, u64, P, u64, P], ctypes.c_int),
             "iris_bits_rotated": ([P, i32, P], ctypes.c_int),
@@ -131,7 +135,7 @@ def exported_symbols():
         "iris_db_read", "iris_db_generate", "iris_db_clear", "iris_masks_engine_new", "iris_distance_engine_new",
         "iris_template_engine_new", "iris_engine_destroy", "iris_engine_batch_process",
         "iris_engine_batch_process_host", "iris_engine_batch_process_device", "iris_template_counts", "iris_template_distances", "iris_template_search",
-        "iris_dot_bool_batch", "iris_dot_u16_batch", "iris_bits_rotated", "iris_encoded_rotated", "iris_encode",
+        "iris_resolver_search", "iris_resolver_search_host", "iris_dot_bool_batch", "iris_dot_u16_batch", "iris_bits_rotated", "iris_encoded_rotated", "iris_encode",
         "iris_decode_distance", "iris_match_merge",
     ]
 
@@ -630,6 +634,37 @@ def denominators(query, entry, device=None):
     return out[0]
 
 
+# ====================================================================== resolver
+
+
+def resolver_search(shares, denominators, index_base=0, device=None):
+    """The resolver's aggregation (src/main.rs:597-621) on the GPU: wrapping sum
+    of the participants' [n,31] u16 shares, decode_distance with the [n,31]
+    denominators, min over rotations, strict-< lowest-index argmin -> Match."""
+    dev = device or default_device()
+    arrs = [_c(s, np.uint16) for s in shares]
+    den = _c(denominators, np.uint16)
+    n = den.shape[0]
+    for a in arrs:
+        if a.shape != (n, ROTATIONS):
+            raise IrisError(-1, "shares and denominators must all be [n, 31] uint16")
+    ptrs = (ctypes.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
+    m = Match()
+    _check(load_library().iris_resolver_search_host(dev.handle, ptrs, len(arrs), _ptr(den), n, int(index_base),
+                                                    ctypes.byref(m)))
+    return m
+
+
+def resolver_search_device(device, share_ptrs, denoms_ptr, n, index_base=0, dist_out_device=None):
+    """Device-resident form: share_ptrs / denoms_ptr are device arrays of n*31 u16."""
+    ptrs = (ctypes.c_void_p * len(share_ptrs))(*share_ptrs)
+    m = Match()
+    _check(load_library().iris_resolver_search(device.handle, ptrs, len(share_ptrs), ctypes.c_void_p(denoms_ptr), int(n),
+                                               int(index_base), ctypes.c_void_p(dist_out_device or 0),
+                                               ctypes.byref(m)))
+    return m
+
+
 # ====================================================================== arch plugin
 
 
@@ -666,7 +701,7 @@ def f64_bits(x):
 
 
 __all__ = [
-    "Bits", "EncodedBits", "Template", "encode", "decode_distance", "distances", "denominators", "MasksEngine",
+    "Bits", "EncodedBits", "Template", "encode", "decode_distance", "resolver_search", "resolver_search_device", "distances", "denominators", "MasksEngine",
     "DistanceEngine", "TemplateEngine", "Device", "Database", "Match", "merge_matches", "dot_bool", "dot_u16",
     "dot_bool_batch", "dot_u16_batch", "IrisError", "load_library", "KIND_MASKS", "KIND_SHARES", "KIND_TEMPLATES",
     "LAYOUT_DEFAULT", "LAYOUT_LANES", "LAYOUT_TILES",

@@ -342,3 +342,61 @@ def test_large_search_properties(device, layout):
                 recs = np.stack([db.read(int(i), 1)[0] for i in ii])
                 assert bits_eq(dist[ii], oc.template_distances(q, recs))
             assert sample.shape == (1, 400)
+
+
+# ---------------------------------------------------------------- resolver (src/main.rs:597-621)
+
+
+def test_resolver_fused_matches_oracle(device, golden):
+    share_out, masks_out = golden["share_out"], golden["masks_out"][: golden["share_out"].shape[1]]
+    want = oc.resolver_combine(share_out, masks_out)
+    best, idx = oc.argmin(want)
+    m = ih.resolver_search(list(share_out), masks_out, device=device)
+    assert m.index == idx and bits_eq(m.distance, best)
+    # random garbage shares (den = 0 rows, uneq > den, ties): decode semantics
+    rng = np.random.default_rng(21)
+    n = 5000
+    parts = [rng.integers(0, 2**16, (n, ROT), dtype=np.uint16) for _ in range(3)]
+    den = rng.integers(0, 40, (n, ROT), dtype=np.uint16)
+    den[rng.random((n, ROT)) < 0.3] = 0
+    den[17] = 0
+    want = oc.resolver_combine(np.stack(parts), den)
+    best, idx = oc.argmin(want)
+    m = ih.resolver_search(parts, den, index_base=100, device=device)
+    assert m.index == 100 + idx and bits_eq(m.distance, best)
+    z = ih.resolver_search([np.zeros((3, ROT), np.uint16)], np.zeros((3, ROT), np.uint16), device=device)
+    assert z.index == 2**64 - 1 and z.distance == np.inf
+
+
+def test_mpc_end_to_end(device, layout):
+    """The reference's MPC flow on synthetic data: the resolver holds the masks,
+    3 participants hold additive shares of encode(template); DistanceEngine on
+    each share DB + MasksEngine + fused resolver == plaintext Template search."""
+    n = 3000
+    rng = np.random.default_rng(5)
+    templates = oc.gen_templates(91, 0, n)
+    q = templates[1234].copy()
+    q[:200] ^= np.uint64(0x3)
+    enc = np.stack([oc.encode(t) for t in templates])
+    s0 = rng.integers(0, 2**16, enc.shape, dtype=np.uint16)
+    s1 = rng.integers(0, 2**16, enc.shape, dtype=np.uint16)
+    s2 = (enc - s0 - s1).astype(np.uint16)  # EncodedBits::share (src/encoded_bits.rs:23-38)
+    enc_q = ih.encode(ih.Template.from_array(q))
+    outs = []
+    for share in (s0, s1, s2):
+        with ih.Database(device, ih.KIND_SHARES, n, layout) as db, ih.DistanceEngine(device, enc_q) as eng:
+            db.append(share)
+            out = np.empty((n, ROT), np.uint16)
+            eng.batch_process(out, db)
+            outs.append(out)
+    with ih.Database(device, ih.KIND_MASKS, n, layout) as mdb, ih.MasksEngine(device, q[200:]) as me:
+        mdb.append(templates[:, 200:])
+        den = np.empty((n, ROT), np.uint16)
+        me.batch_process(den, mdb)
+    m = ih.resolver_search(outs, den, device=device)
+    with ih.Database(device, ih.KIND_TEMPLATES, n, layout) as tdb, ih.TemplateEngine(device, q) as te:
+        tdb.append(templates)
+        ref = te.search(tdb)
+    best, idx = oc.argmin(oc.template_distances(q, templates))
+    assert m.index == ref.index == idx == 1234
+    assert bits_eq(m.distance, best) and bits_eq(ref.distance, best)
