@@ -54,9 +54,11 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--layout", choices=["tiles", "lanes"], default="tiles",
                     help="tiles = MFMA kernels (default), lanes = VALU kernels")
-    ap.add_argument("--workload", choices=["search", "masks", "shares"], default="search",
+    ap.add_argument("--queries", type=int, default=1024, help="queries per batch (workload batch)")
+    ap.add_argument("--workload", choices=["search", "masks", "shares", "batch"], default="search",
                     help="search = Template masked Hamming + argmin (configs[1], default); "
-                         "masks = MasksEngine denominators; shares = DistanceEngine u16 share dot (configs[3])")
+                         "masks = MasksEngine denominators; shares = DistanceEngine u16 share dot (configs[3]); "
+                         "batch = --queries queries x 31 rotations x N templates in one pass (configs[2])")
     return ap.parse_args()
 
 
@@ -148,7 +150,8 @@ def main():
     total = n * world
     dev = ih.Device(ordinal)
     layout = ih.LAYOUT_TILES if args.layout == "tiles" else ih.LAYOUT_LANES
-    kind = {"search": ih.KIND_TEMPLATES, "masks": ih.KIND_MASKS, "shares": ih.KIND_SHARES}[args.workload]
+    kind = {"search": ih.KIND_TEMPLATES, "batch": ih.KIND_TEMPLATES, "masks": ih.KIND_MASKS,
+            "shares": ih.KIND_SHARES}[args.workload]
     db = ih.Database(dev, kind, n, layout)
     t0 = time.time()
     db.generate(n, SEED, global_index0=lo)
@@ -160,10 +163,16 @@ def main():
     plant_global = total * 3 // 4 + 12345
     plant_rot = 9
     out_dev = None
-    if args.workload == "search":
+    nq = args.queries if args.workload == "batch" else 1
+    if args.workload in ("search", "batch"):
         if lo <= plant_global < lo + n:
             db.write(plant_global - lo, planted_record(query, plant_rot)[None, :])
+    if args.workload == "search":
         eng = ih.TemplateEngine(dev, query)
+    elif args.workload == "batch":
+        batch_q = oc.gen_templates(SEED + 2, 0, nq)
+        batch_q[nq // 2] = query  # its best match is the planted record
+        eng = ih.TemplateBatchEngine(dev, batch_q)
     elif args.workload == "masks":
         eng = ih.MasksEngine(dev, query[200:])
         out_dev = dev.alloc(n * ROT * 2)
@@ -182,6 +191,11 @@ def main():
             dev.synchronize()
 
     def step():
+        if args.workload == "batch":
+            ms = eng.search(db, index_base=lo)
+            if dist is not None:
+                ms = [iris_dist.allgather_merge(x, device=xdev) for x in ms]
+            return ms
         if args.workload != "search":
             eng.batch_process_device(db, out_dev)  # [n][31] u16 left in HBM
             return None
@@ -208,10 +222,15 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    kname = {"search": "template_search", "masks": "masks", "shares": "shares"}[args.workload]
-    rec_bytes = {"search": BYTES_PER_TEMPLATE, "masks": 1600, "shares": 25600}[args.workload]
+    kname = {"search": "template_search", "batch": "template_batch", "masks": "masks", "shares": "shares"}[args.workload]
+    rec_bytes = {"search": BYTES_PER_TEMPLATE, "batch": BYTES_PER_TEMPLATE, "masks": 1600,
+                 "shares": 25600}[args.workload]
     if args.workload == "search":
         ok = m.index == plant_global and m.rotation == plant_rot
+    elif args.workload == "batch":
+        mq = m[nq // 2]
+        ok = mq.index == plant_global and mq.rotation == plant_rot
+        m = mq
     else:  # spot-check 64 outputs against the oracle
         sample = np.random.default_rng(0).choice(n, 64, replace=False)
         full = np.empty((n, ROT), np.uint16)
@@ -227,7 +246,7 @@ def main():
     achieved = rec_bytes * n / (avg_ms * 1e-3) / 1e9
     traffic, traffic_src = load_traffic(n, args.layout) if args.workload == "search" else (None, None)
     ms_per_step = elapsed / args.steps * 1e3
-    value = ROT * total / (elapsed / args.steps)
+    value = ROT * total * nq / (elapsed / args.steps)
 
     if rank == 0:
         cpu = None
@@ -254,33 +273,40 @@ def main():
                     "search": "1 query x 31 rotations x N templates, Template masked Hamming + fused min/argmin (BASELINE configs[1] at N=1)",
                     "masks": "MasksEngine: 1 query mask x 31 rotations x N masks, [u16;31] denominators left in HBM",
                     "shares": "DistanceEngine: 1 encoded query x 31 rotations x N u16 shares, [u16;31] left in HBM (BASELINE configs[3])",
+                    "batch": f"{nq} queries x 31 rotations x N templates in one pass, per-query min/argmin (BASELINE configs[2])",
                 }[args.workload],
-                "templates_per_gpu": n, "total_templates": total, "queries": 1, "rotations": ROT,
+                "templates_per_gpu": n, "total_templates": total, "queries": nq, "rotations": ROT,
                 "bytes_per_template": rec_bytes, "parallelism": f"db-shard x{world}", "layout": args.layout,
             },
-            "roofline": {
+            "roofline": ({
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-            },
+            } if args.workload != "batch" else {
+                # compute-bound: fp4 MFMA FLOPs (2 per MAC) of the den + encode products
+                "bound": "mfma", "achieved": 2 * MFMA_MACS_PER_TEMPLATE * n * nq / (avg_ms * 1e-3) / 1e12,
+                "peak": 2 * FP4_DENSE_PEAK_MACS / 1e12, "unit": "TFLOP/s",
+                "frac": MFMA_MACS_PER_TEMPLATE * n * nq / (avg_ms * 1e-3) / FP4_DENSE_PEAK_MACS, "traffic": None,
+            }),
             "kernel": {
                 "name": {("search", "tiles"): "template_mfma_kernel<MF_SEARCH> (fp4 MFMA)",
                          ("search", "lanes"): "template_kernel<MODE_SEARCH> (VALU popcount)",
                          ("masks", "tiles"): "masks_mfma_kernel (fp4 MFMA)",
                          ("masks", "lanes"): "masks_kernel (VALU popcount)",
                          ("shares", "tiles"): "shares_mfma_kernel (i8 MFMA)",
-                         ("shares", "lanes"): "shares_kernel (VALU v_pk_mad_u16)"}[(args.workload, args.layout)],
+                         ("shares", "lanes"): "shares_kernel (VALU v_pk_mad_u16)",
+                         ("batch", "tiles"): "batch_kernel (fp4 MFMA, LDS-tiled GEMM)"}[(args.workload, args.layout)],
                 "avg_ms": avg_ms, "launches": launches,
                 "reduce_avg_ms": rms / max(1, launches),
                 "frac_of_measured_hbm": achieved / HBM_MEASURED_GBS,
                 "valu_int_frac": (VALU_OPS_PER_TEMPLATE * n / (avg_ms * 1e-3) / VALU_INT_PEAK_OPS
                                   if args.layout == "lanes" and args.workload == "search" else None),
-                "mfma_fp4_frac": (MFMA_MACS_PER_TEMPLATE * n / (avg_ms * 1e-3) / FP4_DENSE_PEAK_MACS
-                                  if args.layout == "tiles" and args.workload == "search" else None),
+                "mfma_fp4_frac": (MFMA_MACS_PER_TEMPLATE * n * nq / (avg_ms * 1e-3) / FP4_DENSE_PEAK_MACS
+                                  if args.layout == "tiles" and args.workload in ("search", "batch") else None),
                 "traffic_source": traffic_src,
             },
             "cpu_baseline": cpu,
             "check": ({"planted_index": plant_global, "found_index": int(m.index), "rotation": int(m.rotation),
-                       "distance": m.distance, "ok": bool(ok)} if args.workload == "search"
+                       "distance": m.distance, "ok": bool(ok)} if args.workload in ("search", "batch")
                       else {"sampled_outputs_vs_oracle": 64, "ok": bool(ok)}),
             "setup": {"generate_s": gen_s},
         }

@@ -171,6 +171,14 @@ int iris_template_distances(iris_engine_t *engine, const iris_db_t *db, uint64_t
 int iris_template_search(iris_engine_t *engine, const iris_db_t *db, uint64_t first, uint64_t n,
                          uint64_t index_base, double *dist_out_device, iris_match_t *out);
 
+/* Batched queries (BASELINE configs[2]): nq query Templates searched against
+ * one TILES template database in one pass; out[q] is query q's best match
+ * (same rules as iris_template_search).  DB layout must be TILES. */
+int iris_template_batch_engine_new(iris_device_t *dev, const iris_template_t *queries, uint32_t nq,
+                                   iris_engine_t **out);
+int iris_template_batch_search(iris_engine_t *engine, const iris_db_t *db, uint64_t first, uint64_t n,
+                               uint64_t index_base, iris_match_t *out);
+
 /* ---------------------------------------------------------------- resolver
  * The resolver's aggregation (src/main.rs:597-621) fused on the GPU: for each
  * entry i, num = wrapping sum over the `parts` participants' [u16;31] shares,

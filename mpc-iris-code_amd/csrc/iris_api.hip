@@ -87,6 +87,7 @@ struct iris_engine {
     int kind = 0;             // IRIS_KIND_* of the DB it runs against
     void *qtab = nullptr;     // SGPR rotated-query table (LANES kernels)
     void *qfrag = nullptr;    // fp4 query fragments (TILES kernel, templates only)
+    uint32_t nq = 0;          // > 0: batched template engine (qfrag = nq padded query tiles)
 };
 
 namespace {
@@ -650,7 +651,7 @@ int iris_engine_batch_process_host(iris_engine_t *e, const void *records, uint64
 
 static int template_args(iris_engine_t *e, const iris_db_t *db) {
     ARG(e && db, "NULL argument");
-    ARG(e->kind == IRIS_KIND_TEMPLATES, "not a template engine");
+    ARG(e->kind == IRIS_KIND_TEMPLATES && e->nq == 0, "not a single-query template engine");
     ARG(db->k.kind == IRIS_KIND_TEMPLATES, "database does not hold templates");
     ARG(e->dev == db->dev, "engine and database live on different devices");
     return 0;
@@ -751,6 +752,70 @@ int iris_template_distances(iris_engine_t *e, const iris_db_t *db, uint64_t firs
         CHK(search_locked(e, db, first + done, m, 0, (double *)d->out_a.p, &ignored));
         HIPCHK(hipMemcpyAsync(out + done, d->out_a.p, m * sizeof(double), hipMemcpyDeviceToHost, d->stream));
         CHK(sync(d));
+    }
+    return 0;
+}
+
+// ------------------------------------------------------------------ batched queries
+
+int iris_template_batch_engine_new(iris_device_t *d, const iris_template_t *queries, uint32_t nq, iris_engine_t **out) {
+    ARG(d && out && (nq == 0 || queries), "NULL argument");
+    ARG(nq > 0, "a batch needs at least one query");
+    std::lock_guard<std::recursive_mutex> g(d->mu);
+    CHK(set_device(d));
+    const uint32_t nqp = (nq + 3) / 4 * 4;  // padded to the kernel's query groups (zero tiles: no candidate)
+    const size_t tile_dw = (size_t)4 * kPlaneGroups * 64;
+    std::vector<uint32_t> tiles((size_t)nqp * tile_dw, 0u);
+    for (uint32_t i = 0; i < nq; ++i) build_query_tile(queries + i, tiles.data() + i * tile_dw);
+    uint32_t dummy = 0;
+    iris_engine *e = nullptr;
+    CHK(engine_new(d, IRIS_KIND_TEMPLATES, &dummy, sizeof(dummy), &e, tiles.data(), tiles.size() * 4));
+    e->nq = nq;
+    *out = e;
+    return 0;
+}
+
+int iris_template_batch_search(iris_engine_t *e, const iris_db_t *db, uint64_t first, uint64_t n, uint64_t index_base,
+                               iris_match_t *out) {
+    ARG(e && db && out, "NULL argument");
+    ARG(e->kind == IRIS_KIND_TEMPLATES && e->nq > 0, "not a batched template engine");
+    ARG(db->k.kind == IRIS_KIND_TEMPLATES && db->k.layout == IRIS_LAYOUT_TILES,
+        "batched search needs a template database in the TILES layout");
+    ARG(e->dev == db->dev, "engine and database live on different devices");
+    iris_device *d = e->dev;
+    std::lock_guard<std::recursive_mutex> g(d->mu);
+    CHK(set_device(d));
+    CHK(range_ok(db, first, n));
+    LaunchRange r{first, n};
+    const BatchGeometry geo = batch_geometry(r, e->nq);
+    const uint32_t nqp = geo.nqg * 4;
+    std::vector<Partial> res(nqp);
+    if (n > 0) {
+        CHK(ensure(d->partials, (size_t)nqp * geo.G * sizeof(Partial)));
+        CHK(ensure(d->result, (size_t)nqp * sizeof(Partial)));
+        CHK(timed(d, "template_batch", n * e->nq, [&] {
+            return launch_batch(d->stream, db->data, e->qfrag, r, geo, (Partial *)d->partials.p, (Partial *)d->result.p);
+        }));
+        HIPCHK(hipMemcpyAsync(res.data(), d->result.p, nqp * sizeof(Partial), hipMemcpyDeviceToHost, d->stream));
+    }
+    CHK(sync(d));
+    for (uint32_t q = 0; q < e->nq; ++q) {
+        const Partial &p = res[q];
+        iris_match_t &m = out[q];
+        if (n == 0 || p.den == 0) {
+            m.distance = INFINITY;
+            m.index = UINT64_MAX;
+            m.num = 0;
+            m.den = 0;
+            m.rotation = 0;
+        } else {
+            m.distance = (double)p.num / (double)p.den;
+            m.index = index_base + first + p.idx;
+            m.num = p.num;
+            m.den = p.den;
+            m.rotation = p.rot - IRIS_MAX_ROTATION;
+        }
+        m.reserved = 0;
     }
     return 0;
 }

@@ -180,3 +180,28 @@ void build_shares_frags(const uint16_t *const *vectors, int count, uint32_t *fra
 }
 
 }  // namespace iris
+
+namespace iris {
+
+// The 31 rotated copies of a query packed as records 0..30 of a TILES tile
+// (record 31 zero): the A operand of the batched kernel (iris_batch.hip).
+void build_query_tile(const iris_template_t *q, uint32_t *tile) {
+    memset(tile, 0, sizeof(uint32_t) * 4 * kPlaneGroups * 64);
+    for (int k = 0; k < kRot; ++k) {
+        uint64_t m[IRIS_LIMBS], p[IRIS_LIMBS];
+        bits_rotated(q->mask, k - 15, m);
+        bits_rotated(q->pattern, k - 15, p);
+        for (int g = 0; g < kPlaneGroups; ++g)
+            for (int h = 0; h < 2; ++h) {
+                const uint32_t em0 = dword_of(m, 4 * g + h), ep0 = dword_of(p, 4 * g + h);
+                const uint32_t em1 = dword_of(m, 4 * g + 2 + h), ep1 = dword_of(p, 4 * g + 2 + h);
+                uint32_t *v = tile + ((size_t)g * 64 + k + 32 * h) * 4;
+                v[0] = xpack(em0 & 0xFFFFu, ep0 & 0xFFFFu);
+                v[1] = xpack(em0 >> 16, ep0 >> 16);
+                v[2] = xpack(em1 & 0xFFFFu, ep1 & 0xFFFFu);
+                v[3] = xpack(em1 >> 16, ep1 >> 16);
+            }
+    }
+}
+
+}  // namespace iris

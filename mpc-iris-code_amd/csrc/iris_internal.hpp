@@ -188,6 +188,13 @@ int launch_generate_tiles_kind(void *stream, int kind, void *db, uint64_t t_firs
                                uint64_t global_index0);
 int launch_masks_mfma(void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *out);
 uint32_t resolver_partials(uint64_t n);
+struct BatchGeometry {
+    uint64_t tile0, ntiles;
+    uint32_t nqg, G;  // query groups of 4, workgroups per query group
+};
+BatchGeometry batch_geometry(LaunchRange r, uint32_t nq);
+int launch_batch(void *stream, const void *db, const void *qtiles, LaunchRange r, const BatchGeometry &g,
+                 Partial *partials, Partial *out);
 int launch_resolver(void *stream, const uint16_t *const *shares, uint32_t parts, const uint16_t *denoms, uint64_t n,
                     double *dist_out, Partial *partials);
 int launch_shares_mfma(void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *out);
@@ -207,6 +214,7 @@ void encode_template(const iris_template_t *t, uint16_t *out);
 void build_template_table(const iris_template_t *q, uint32_t *tab);                  // 400*64 dwords
 void build_template_frags(const iris_template_t *q, uint32_t *frag);                 // kTemplateFragDwords
 void build_masks_frags(const uint64_t *const *vectors, int count, uint32_t *frag);    // kMaskFragUint4 uint4
+void build_query_tile(const iris_template_t *q, uint32_t *tile);                      // 6400 uint4 (TILES tile)
 void build_shares_frags(const uint16_t *const *vectors, int count, uint32_t *frag);   // kShareFragUint4 uint4 + 64 int
 void build_masks_table(const uint64_t *const *vectors, int count, uint32_t *tab);     // 400*32
 void build_shares_table(const uint16_t *const *vectors, int count, uint32_t *tab);    // 6400*32

@@ -104,6 +104,8 @@ def load_library(path=None):
             "iris_template_counts": ([P, P, u64, u64, P, P], ctypes.c_int),
             "iris_template_distances": ([P, P, u64, u64, P], ctypes.c_int),
             "iris_template_search": ([P, P, u64, u64, u64, P, ctypes.POINTER(Match)], ctypes.c_int),
+            "iris_template_batch_engine_new": ([P, P, ctypes.c_uint32, PP], ctypes.c_int),
+            "iris_template_batch_search": ([P, P, u64, u64, u64, ctypes.POINTER(Match)], ctypes.c_int),
             "iris_resolver_search": ([P, ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint32, P, u64, u64, P,
                                       ctypes.POINTER(Match)], ctypes.c_int),
             "iris_resolver_search_host": ([P, ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint32, P, u64, u64,
@@ -135,7 +137,8 @@ def exported_symbols():
         "iris_db_read", "iris_db_generate", "iris_db_clear", "iris_masks_engine_new", "iris_distance_engine_new",
         "iris_template_engine_new", "iris_engine_destroy", "iris_engine_batch_process",
         "iris_engine_batch_process_host", "iris_engine_batch_process_device", "iris_template_counts", "iris_template_distances", "iris_template_search",
-        "iris_resolver_search", "iris_resolver_search_host", "iris_dot_bool_batch", "iris_dot_u16_batch", "iris_bits_rotated", "iris_encoded_rotated", "iris_encode",
+        "iris_template_batch_engine_new", "iris_template_batch_search", "iris_resolver_search",
+        "iris_resolver_search_host", "iris_dot_bool_batch", "iris_dot_u16_batch", "iris_bits_rotated", "iris_encoded_rotated", "iris_encode",
         "iris_decode_distance", "iris_match_merge",
     ]
 
@@ -616,6 +619,27 @@ class TemplateEngine(_Engine):
         return m
 
 
+class TemplateBatchEngine(_Engine):
+    """Many query Templates against one template DB in one pass (configs[2])."""
+
+    kind = KIND_TEMPLATES
+
+    def __init__(self, device, queries):
+        self.device = device
+        q = _records(KIND_TEMPLATES, queries)
+        self.nq = q.shape[0]
+        h = ctypes.c_void_p()
+        _check(load_library().iris_template_batch_engine_new(device.handle, _ptr(q), self.nq, ctypes.byref(h)))
+        self.handle = h
+
+    def search(self, db, first=0, n=None, index_base=0):
+        n = (len(db) - first) if n is None else n
+        out = (Match * self.nq)()
+        _check(load_library().iris_template_batch_search(self.handle, db.handle, int(first), int(n), int(index_base),
+                                                         out))
+        return list(out)
+
+
 def distances(query, entry, device=None):
     """distances(&EncodedBits, &EncodedBits) -> [u16; 31] (src/lib.rs:82-87)."""
     dev = device or default_device()
@@ -702,7 +726,7 @@ def f64_bits(x):
 
 __all__ = [
     "Bits", "EncodedBits", "Template", "encode", "decode_distance", "resolver_search", "resolver_search_device", "distances", "denominators", "MasksEngine",
-    "DistanceEngine", "TemplateEngine", "Device", "Database", "Match", "merge_matches", "dot_bool", "dot_u16",
+    "DistanceEngine", "TemplateEngine", "TemplateBatchEngine", "Device", "Database", "Match", "merge_matches", "dot_bool", "dot_u16",
     "dot_bool_batch", "dot_u16_batch", "IrisError", "load_library", "KIND_MASKS", "KIND_SHARES", "KIND_TEMPLATES",
     "LAYOUT_DEFAULT", "LAYOUT_LANES", "LAYOUT_TILES",
     "ROTATIONS", "BITS", "LIMBS", "COLS", "ROWS",

@@ -400,3 +400,33 @@ def test_mpc_end_to_end(device, layout):
     best, idx = oc.argmin(oc.template_distances(q, templates))
     assert m.index == ref.index == idx == 1234
     assert bits_eq(m.distance, best) and bits_eq(ref.distance, best)
+
+
+# ---------------------------------------------------------------- batched queries (configs[2])
+
+
+def test_batch_search_matches_single(device):
+    """9 queries (a padded query group) against 5000 templates (a partial
+    N-group): every query's best equals the single-query search and the oracle."""
+    n, nq = 5000, 9
+    db_ref = oc.gen_templates(61, 0, n)
+    queries = oc.gen_templates(62, 0, nq)
+    queries[3] = db_ref[4321]          # exact member -> distance 0
+    queries[7, :200] = db_ref[17, :200] ^ np.uint64(0x5)
+    queries[7, 200:] = db_ref[17, 200:]
+    queries[5, 200:] = 0               # empty query mask -> no candidate
+    with ih.Database(device, ih.KIND_TEMPLATES, n) as db:
+        db.append(db_ref)
+        with ih.TemplateBatchEngine(device, queries) as be:
+            got = be.search(db)
+            sub = be.search(db, first=1000, n=3333, index_base=7)
+        for q in range(nq):
+            want_d, want_i = oc.argmin(oc.template_distances(queries[q], db_ref))
+            assert got[q].index == want_i and bits_eq(got[q].distance, want_d), q
+            with ih.TemplateEngine(device, queries[q]) as eng:
+                one = eng.search(db)
+            assert (one.index, one.num, one.den, one.rotation) == (got[q].index, got[q].num, got[q].den, got[q].rotation)
+            sd, si = oc.argmin(oc.template_distances(queries[q], db_ref[1000:4333]))
+            assert sub[q].index == (7 + 1000 + si if si != 2**64 - 1 else si) and bits_eq(sub[q].distance, sd), q
+    assert got[3].index == 4321 and got[3].distance == 0.0
+    assert got[5].index == 2**64 - 1
