@@ -1,0 +1,62 @@
+// iris_device.hpp — device helpers shared by the MFMA kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "iris_internal.hpp"
+
+namespace iris {
+
+// Workgroups of one launch that fit on the current device at `per_cu` per CU
+// (persistent grids); cached per device ordinal.
+static inline uint64_t resident_blocks(int per_cu) {
+    static int cus[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+    if (cus[dev] == 0) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+        cus[dev] = n;
+    }
+    return (uint64_t)cus[dev] * per_cu;
+}
+
+typedef unsigned int u32x4_nt __attribute__((ext_vector_type(4)));
+
+// Writes one 32-record tile's [32][31] u16 output rows.  In the 32x32 MFMA C
+// layout lane l holds rows k = (r & 3) + 8 (r >> 2) + 4 (l >> 5), r = 0..15, of
+// record (l & 31); `val(r)` returns that value.  A tile fully inside
+// [first, end) whose output offset is 16-B aligned is staged through the
+// wave's 2 KB LDS buffer and written with 124 16-byte stores (1984 B); other
+// tiles fall back to per-element stores of their valid records.
+template <class F>
+__device__ __forceinline__ void store_tile_rows(uint16_t *__restrict__ out, uint16_t *lds, uint64_t tile_t0,
+                                                uint64_t first, uint64_t end, bool tile_valid, int lane, F val) {
+    const int h = lane >> 5;
+    const bool full = tile_valid && tile_t0 >= first && tile_t0 + 32 <= end && ((tile_t0 - first) & 7) == 0 &&
+                      (((uintptr_t)out & 15) == 0);
+    if (full) {  // wave-uniform
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int k = (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (k < kRot) lds[(lane & 31) * kRot + k] = val(r);
+        }
+        uint4 *dst = (uint4 *)(out + (tile_t0 - first) * kRot);
+        const uint4 *src = (const uint4 *)lds;
+        // streamed out with nontemporal stores: the rows are not re-read by this launch
+        for (int i = lane; i < 32 * kRot * 2 / 16; i += 64) {
+            const uint4 v = src[i];
+            const u32x4_nt w = {v.x, v.y, v.z, v.w};
+            __builtin_nontemporal_store(w, (u32x4_nt *)&dst[i]);
+        }
+    } else {
+        const uint64_t tg = tile_t0 + (lane & 31);
+        if (!tile_valid || tg < first || tg >= end) return;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int k = (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (k < kRot) out[(tg - first) * kRot + k] = val(r);
+        }
+    }
+}
+
+}  // namespace iris

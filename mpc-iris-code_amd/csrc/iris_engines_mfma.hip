@@ -15,7 +15,7 @@
 //   |S| <= 2 * 12800 * 128^2 < 2^31.
 #include <hip/hip_runtime.h>
 
-#include "iris_internal.hpp"
+#include "iris_device.hpp"
 
 namespace iris {
 
@@ -26,7 +26,7 @@ typedef float v16f __attribute__((ext_vector_type(16)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kTile = 32;
-constexpr int kMasksTiles = 4;   // tiles per wave
+constexpr int kMasksTiles = 4;  // tiles per wave
 constexpr int kSharesTiles = 2;
 
 __device__ __forceinline__ uint4 nt_load(const uint4 *p) {
@@ -54,91 +54,105 @@ __device__ __forceinline__ v16f mfma_fp4(const v8i &a, const v8i &b, const v16f 
     return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, c, 4, 4, 0, 127, 0, 127);
 }
 
-__device__ __forceinline__ void mask_chunk(uint32_t x, const uint4 &q, v16f &acc) {
+// x: one dword of a mask tile (8 masks' nibbles); w: the compact query word of
+// the same chunk (see kMaskFragUint4)
+__device__ __forceinline__ v8i mask_a(uint32_t w) {
+    return v8i{(int)(w & 0x44444444u), (int)(w & 0x22222222u), (int)(w & 0x11111111u), (int)((w >> 3) & 0x11111111u),
+               0, 0, 0, 0};
+}
+
+__device__ __forceinline__ void mask_chunk(uint32_t x, const v8i &a, v16f &acc) {
     const v8i b = {(int)(x & 0x11111111u), (int)(x & 0x22222222u), (int)(x & 0x44444444u),
                    (int)((x >> 1) & 0x44444444u), 0, 0, 0, 0};
-    const v8i a = {(int)q.x, (int)q.y, (int)q.z, (int)q.w, 0, 0, 0, 0};
     acc = mfma_fp4(a, b, acc);
 }
 
+// Persistent: each wave walks the tile groups wave, wave + nwaves, ... as one
+// flat stream of (group, step) K-steps, so the loads of the next group are in
+// flight while the current group's rows are written out (a wave that exits
+// after its stores leaves its slot idle until they are acknowledged).  The
+// compact query (51 KB) is staged in LDS once per workgroup.
 __global__ void __launch_bounds__(256, 2)
     masks_mfma_kernel(const uint4 *__restrict__ db, const uint4 *__restrict__ qfrag, uint64_t tile0, uint64_t ntiles,
                       uint64_t first, uint64_t end, uint16_t *__restrict__ out) {
     constexpr int T = kMasksTiles;
-    constexpr int kSteps = kMaskChunks / 4;  // 50 steps of 4 chunks
-    const int lane = threadIdx.x & 63;
-    const uint64_t wave = (uint64_t)blockIdx.x * kWaveSlots + (threadIdx.x >> 6);
-    const uint64_t tw = wave * T;
-    if (tw >= ntiles) return;
-    v16f acc[T];
-#pragma unroll
-    for (int t = 0; t < T; ++t)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
+    constexpr uint32_t kSteps = kMaskChunks / 4;  // 50 steps of 4 chunks
+    __shared__ uint4 sq[kMaskFragUint4];
+    __shared__ __attribute__((aligned(16))) uint16_t sh_out[kWaveSlots][1024];
+    for (int i = threadIdx.x; i < (int)kMaskFragUint4; i += blockDim.x) sq[i] = qfrag[i];
+    __syncthreads();
 
-    const uint4 *dp[T];
+    const int lane = threadIdx.x & 63;
+    const uint64_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaveSlots + (threadIdx.x >> 6));
+    const uint64_t nwaves = (uint64_t)gridDim.x * kWaveSlots;
+    const uint64_t ngroups = (ntiles + T - 1) / T;
+    if (wave >= ngroups) return;
+    const uint32_t total = (uint32_t)((ngroups - wave + nwaves - 1) / nwaves) * kSteps;
+    uint16_t *lds = sh_out[threadIdx.x >> 6];
+
+    v16f acc[T];
+    auto zero = [&] {
 #pragma unroll
-    for (int t = 0; t < T; ++t) {
-        const uint64_t rel = (tw + t < ntiles) ? tw + t : ntiles - 1;
-        dp[t] = db + (tile0 + rel) * (uint64_t)kMaskTileUint4 + lane;
-    }
-    const uint4 *qp = qfrag + lane;  // chunk c: qfrag[c * 64 + lane]
+        for (int t = 0; t < T; ++t)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
+    };
+    zero();
     struct Stage {
         uint4 d[T];
-        uint4 q[4];
+        uint4 w;
     };
-    auto load = [&](Stage &st, int g) {
-        g = g < kSteps ? g : kSteps - 1;
-#pragma unroll
-        for (int t = 0; t < T; ++t) st.d[t] = nt_load(dp[t] + g * 64);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) st.q[i] = qp[(4 * g + i) * 64];
-        __builtin_amdgcn_sched_barrier(0);
-    };
-    auto compute = [&](const Stage &st) {
+    auto load = [&](Stage &st, uint32_t s) {
+        s = s < total ? s : total - 1;
+        const uint32_t j = s / kSteps, g = s - j * kSteps;
+        const uint64_t tw = (wave + (uint64_t)j * nwaves) * T;
 #pragma unroll
         for (int t = 0; t < T; ++t) {
-            mask_chunk(st.d[t].x, st.q[0], acc[t]);
-            mask_chunk(st.d[t].y, st.q[1], acc[t]);
-            mask_chunk(st.d[t].z, st.q[2], acc[t]);
-            mask_chunk(st.d[t].w, st.q[3], acc[t]);
+            const uint64_t rel = (tw + t < ntiles) ? tw + t : ntiles - 1;
+            st.d[t] = nt_load(db + (tile0 + rel) * (uint64_t)kMaskTileUint4 + g * 64 + lane);
+        }
+        st.w = sq[g * 64 + lane];
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto compute = [&](const Stage &st, uint32_t s) {
+        if (s >= total) return;
+        const v8i a0 = mask_a(st.w.x), a1 = mask_a(st.w.y), a2 = mask_a(st.w.z), a3 = mask_a(st.w.w);
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+            mask_chunk(st.d[t].x, a0, acc[t]);
+            mask_chunk(st.d[t].y, a1, acc[t]);
+            mask_chunk(st.d[t].z, a2, acc[t]);
+            mask_chunk(st.d[t].w, a3, acc[t]);
+        }
+        const uint32_t j = s / kSteps;
+        if (s - j * kSteps == kSteps - 1) {  // group j done: write its rows
+            const uint64_t tw = (wave + (uint64_t)j * nwaves) * T;
+#pragma unroll
+            for (int t = 0; t < T; ++t)
+                store_tile_rows(out, lds, (tile0 + tw + t) * kTile, first, end, tw + t < ntiles, lane,
+                                [&](int r) { return (uint16_t)(uint32_t)acc[t][r]; });
+            zero();
         }
     };
     Stage sa, sb, sc;
     load(sa, 0);
     load(sb, 1);
-    int g = 0;
 #pragma unroll 1
-    for (; g + 3 <= kSteps; g += 3) {
-        load(sc, g + 2);
-        compute(sa);
-        load(sa, g + 3);
-        compute(sb);
-        load(sb, g + 4);
-        compute(sc);
-    }
-    // 50 = 16 * 3 + 2: two steps left, in sa and sb
-    if (g < kSteps) compute(sa);
-    if (g + 1 < kSteps) compute(sb);
-
-    const int h = lane >> 5;
-#pragma unroll
-    for (int t = 0; t < T; ++t) {
-        const uint64_t tg = (tile0 + tw + t) * kTile + (lane & 31);
-        if (tw + t >= ntiles || tg < first || tg >= end) continue;
-        const uint64_t o = tg - first;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const int k = (r & 3) + 8 * (r >> 2) + 4 * h;
-            if (k < kRot) out[o * kRot + k] = (uint16_t)(uint32_t)acc[t][r];
-        }
+    for (uint32_t s = 0; s < total; s += 3) {
+        load(sc, s + 2);
+        compute(sa, s);
+        load(sa, s + 3);
+        compute(sb, s + 1);
+        load(sb, s + 4);
+        compute(sc, s + 2);
     }
 }
 
 int launch_masks_mfma(void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *out) {
     if (r.n == 0) return 0;
     const Tiles t = tiles_of(r, kMasksTiles);
-    hipLaunchKernelGGL(masks_mfma_kernel, dim3((uint32_t)t.grid), dim3(256), 0, (hipStream_t)stream,
+    const uint64_t grid = std::min<uint64_t>(t.grid, resident_blocks(2));
+    hipLaunchKernelGGL(masks_mfma_kernel, dim3((uint32_t)grid), dim3(256), 0, (hipStream_t)stream,
                        (const uint4 *)db, (const uint4 *)qfrag, t.tile0, t.ntiles, r.first, r.first + r.n, out);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
@@ -224,24 +238,21 @@ __global__ void __launch_bounds__(256, 2)
     // row 31 (lane t + 32, register 15) holds sum e'_lo in S1 and sum e'_hi + sum e'_lo in S2
     const int h = lane >> 5;
     const int src = (lane & 31) + 32;
+    __shared__ __attribute__((aligned(16))) uint16_t sh_out[kWaveSlots][1024];
+    uint16_t *lds = sh_out[threadIdx.x >> 6];
 #pragma unroll
     for (int t = 0; t < T; ++t) {
         const int elo = __shfl(s1[t][15], src);
         const int ehi = __shfl(s2[t][15], src) - elo;
-        const uint64_t tg = (tile0 + tw + t) * kTile + (lane & 31);
-        if (tw + t >= ntiles || tg < first || tg >= end) continue;
-        const uint64_t o = tg - first;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
+        store_tile_rows(out, lds, (tile0 + tw + t) * kTile, first, end, tw + t < ntiles, lane, [&](int r) {
             const int k = (r & 3) + 8 * (r >> 2) + 4 * h;
-            if (k >= kRot) continue;
-            const int2 qs = qsum[k];  // (sum q'_lo, sum q'_hi) of row k
+            const int2 qs = qsum[k < kRot ? k : 0];  // (sum q'_lo, sum q'_hi) of row k
             // the 16384 * K terms vanish mod 2^16 (K = 12800)
             const uint32_t lo = (uint32_t)s1[t][r] + 128u * (uint32_t)elo + 128u * (uint32_t)qs.x;
             const uint32_t cross = (uint32_t)s2[t][r] + 128u * (uint32_t)ehi + 128u * (uint32_t)qs.x +
                                    128u * (uint32_t)elo + 128u * (uint32_t)qs.y;
-            out[o * kRot + k] = (uint16_t)(lo + 256u * cross);
-        }
+            return (uint16_t)(lo + 256u * cross);
+        });
     }
 }
 

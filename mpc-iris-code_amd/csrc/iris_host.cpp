@@ -140,15 +140,18 @@ namespace iris {
 // MasksEngine, arbitrary vectors for dot_bool); value 2 / 1 / 0.5 / 0.5 by
 // fragment dword, matching the template-side 0.5 / 1 / 2 / 2 (iris_internal.hpp).
 void build_masks_frags(const uint64_t *const *vectors, int count, uint32_t *frag) {
-    static const uint32_t code[4] = {0x4u, 0x2u, 0x1u, 0x1u};
+    // element j of dword j / 8 has fp4 code {4, 2, 1, 1}[j / 8] (2.0, 1.0, 0.5, 0.5 against the
+    // B codes 0.5, 1.0, 2.0, 2.0 of mask_chunk); the kernel selects code bits 2, 1, 0 in place
+    // and shifts bit 3 down to bit 0
+    static const int bitpos[4] = {2, 1, 0, 3};
     memset(frag, 0, sizeof(uint32_t) * 4 * kMaskFragUint4);
     for (int k = 0; k < count && k < kRot; ++k)
         for (int c = 0; c < kMaskChunks; ++c)
             for (int h = 0; h < 2; ++h) {
                 const uint32_t x = dword_of(vectors[k], 2 * c + h);
-                uint32_t *f = frag + ((size_t)c * 64 + k + 32 * h) * 4;
+                uint32_t *f = frag + ((size_t)(c / 4) * 64 + k + 32 * h) * 4 + (c % 4);
                 for (int j = 0; j < 32; ++j)
-                    if ((x >> mask_frag_bit(j)) & 1u) f[j / 8] |= code[j / 8] << (4 * (j % 8));
+                    if ((x >> mask_frag_bit(j)) & 1u) *f |= 1u << (4 * (j % 8) + bitpos[j / 8]);
             }
 }
 

@@ -122,7 +122,9 @@ constexpr int kMaskTileUint4 = (kPlaneGroups / 2) * 64;   // 3200
 constexpr int kShareTileUint4 = (kShareDwords / 16) * 2 * 64;  // 51200
 constexpr int kMaskChunks = kPlaneDwords / 2;   // 200 chunks of 64 bits
 constexpr int kShareChunks = IRIS_BITS / 32;    // 400 chunks of 32 elements
-constexpr size_t kMaskFragUint4 = (size_t)kMaskChunks * 64;
+// masks A-fragments, one bit per fp4 element: uint4 [step g = 50][lane 64], one
+// dword per chunk 4g + i; element j of a lane's 32 is bit 4 (j & 7) + {2, 1, 0, 3}[j >> 3]
+constexpr size_t kMaskFragUint4 = (size_t)(kMaskChunks / 4) * 64;
 constexpr size_t kShareFragUint4 = (size_t)kShareChunks * 64 * 2;  // + 32 int2 row constants after it
 IRIS_HD inline int mask_frag_bit(int j) { return 4 * (j & 7) + (j >> 3); }
 constexpr size_t kTemplateFragDwords = (size_t)(kPlaneDwords / 2) * 64 * kFragDwords;  // 200 chunks
@@ -213,7 +215,7 @@ void encoded_rotated(const uint16_t *in, int amount, uint16_t *out);
 void encode_template(const iris_template_t *t, uint16_t *out);
 void build_template_table(const iris_template_t *q, uint32_t *tab);                  // 400*64 dwords
 void build_template_frags(const iris_template_t *q, uint32_t *frag);                 // kTemplateFragDwords
-void build_masks_frags(const uint64_t *const *vectors, int count, uint32_t *frag);    // kMaskFragUint4 uint4
+void build_masks_frags(const uint64_t *const *vectors, int count, uint32_t *frag);    // kMaskFragUint4 uint4 (compact)
 void build_query_tile(const iris_template_t *q, uint32_t *tile);                      // 6400 uint4 (TILES tile)
 void build_shares_frags(const uint16_t *const *vectors, int count, uint32_t *frag);   // kShareFragUint4 uint4 + 64 int
 void build_masks_table(const uint64_t *const *vectors, int count, uint32_t *tab);     // 400*32

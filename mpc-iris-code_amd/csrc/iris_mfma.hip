@@ -22,7 +22,7 @@
 // shift-and per dword pair — fast VOP2 ops, hidden under the MFMAs.
 #include <hip/hip_runtime.h>
 
-#include "iris_internal.hpp"
+#include "iris_device.hpp"
 
 namespace iris {
 
@@ -184,19 +184,19 @@ __global__ void __launch_bounds__(256, 2)
         const uint64_t tg = (tile0 + tw + t) * kTileRecs + (lane & 31);  // global template index
         const bool valid = active && (tw + t < ntiles) && tg >= first && tg < end;
         const uint64_t o = tg - first;
-        if (MODE == MF_COUNTS) {
-            if (valid) {
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int k = (r & 3) + 8 * (r >> 2) + 4 * h;
-                    if (k < kRot) {
-                        const uint32_t dd = (uint32_t)den[t][r];
-                        const int sv = (int)s[t][r];
-                        if (num_out) num_out[o * kRot + k] = (uint16_t)(((int)dd - sv) >> 1);
-                        if (den_out) den_out[o * kRot + k] = (uint16_t)dd;
-                    }
-                }
-            }
+        if constexpr (MODE == MF_COUNTS) {
+            __shared__ __attribute__((aligned(16))) uint16_t sh_out[kWaveSlots][1024];
+            uint16_t *lds = sh_out[wslot];
+            const uint64_t t0 = (tile0 + tw + t) * kTileRecs;
+            const bool tv = active && (tw + t < ntiles);
+            if (num_out)
+                store_tile_rows(num_out, lds, t0, first, end, tv, lane,
+                                [&](int r) { return (uint16_t)(((int)den[t][r] - (int)s[t][r]) >> 1); });
+            if (den_out)
+                store_tile_rows(den_out, lds, t0, first, end, tv, lane,
+                                [&](int r) { return (uint16_t)(uint32_t)den[t][r]; });
+            (void)valid;
+            (void)o;
         } else {
             uint32_t bn = 0, bd = 0;
             int br = 0;

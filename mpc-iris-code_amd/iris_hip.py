@@ -20,13 +20,15 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 import pathlib
 import threading
 
 import numpy as np
 
 HERE = pathlib.Path(__file__).resolve().parent
-LIB_PATH = HERE / "libiris_hip.so"
+# IRIS_HIP_LIB points at an alternative in-tree build (kernel experiments under tools/)
+LIB_PATH = pathlib.Path(os.environ.get("IRIS_HIP_LIB", HERE / "libiris_hip.so"))
 
 COLS, ROWS, BITS, LIMBS, ROTATIONS = 200, 64, 12800, 200, 31
 KIND_MASKS, KIND_SHARES, KIND_TEMPLATES = 1, 2, 3
