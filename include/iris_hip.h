@@ -50,6 +50,8 @@ extern "C" {
 #define IRIS_E_NOMEM (-3)     /* device or host allocation failed          */
 #define IRIS_E_NODEV (-4)     /* no usable gfx950 device                    */
 #define IRIS_E_RANGE (-5)     /* index range outside the database          */
+#define IRIS_E_IO (-6)        /* file open / read / write failed            */
+#define IRIS_E_FORMAT (-7)    /* malformed JSON template file               */
 
 /* Database record kinds */
 #define IRIS_KIND_MASKS 1     /* records are Bits (the resolver's masks file, src/main.rs:455-469) */
@@ -129,6 +131,33 @@ int iris_db_read(const iris_db_t *db, uint64_t first, uint64_t n, void *records)
  * src/encoded_bits.rs:81-87, src/template.rs:67-74). */
 int iris_db_generate(iris_db_t *db, uint64_t n, uint64_t seed, uint64_t global_index0);
 int iris_db_clear(iris_db_t *db);
+
+/* ---------------------------------------------------------------- on-disk formats
+ * Record files hold the raw little-endian bytes of a record slice
+ * (bytemuck::bytes_of): `prepare` writes them and `participant` / `resolver`
+ * mmap them (src/main.rs:299-309,341,353-357,386-400,455-469):
+ *   IRIS_KIND_MASKS      *.masks    Bits        1600 B
+ *   IRIS_KIND_SHARES     *.share-i  EncodedBits 25600 B
+ *   IRIS_KIND_TEMPLATES  raw Template (pattern then mask) 3200 B
+ * iris_db_load_file appends records [first, first+count) of the file
+ * (count = UINT64_MAX: to the end), streamed through pinned buffers with the
+ * file reads overlapping the H2D copies and the layout transpose; *loaded
+ * (may be NULL) receives the number appended.  A file whose size is not a
+ * multiple of the record size is rejected (IRIS_E_ARG), as the reference's
+ * try_cast_slice does ("Share file … invalid.", src/main.rs:390-393,459-462). */
+int iris_db_load_file(iris_db_t *db, const char *path, uint64_t first, uint64_t count, uint64_t *loaded);
+/* Writes records [first, first+n) of db to `path` (created / truncated) in
+ * the same raw format. */
+int iris_db_save_file(const iris_db_t *db, const char *path, uint64_t first, uint64_t n);
+/* JSON template files: a top-level array of {"pattern": hex, "mask": hex}
+ * objects, each Bits the hex of its 1600 LE bytes (serde form of Template,
+ * src/template.rs:11-29, src/bits.rs:74-93; read like the streaming
+ * iter_json_array, src/json_stream.rs:53-60).  Read: up to cap templates go
+ * to out (out may be NULL to count); *n is the number in the file;
+ * IRIS_E_RANGE if it exceeds cap, IRIS_E_FORMAT with the byte offset on
+ * malformed input.  Write: compact JSON, lowercase hex (hex::serialize). */
+int iris_templates_read_json(const char *path, iris_template_t *out, uint64_t cap, uint64_t *n);
+int iris_templates_write_json(const char *path, const iris_template_t *templates, uint64_t n);
 
 /* ---------------------------------------------------------------- engines
  * MasksEngine::new(&Bits)            src/lib.rs:60-67

@@ -20,151 +20,11 @@
 
 using namespace iris;
 
-// ------------------------------------------------------------------ errors
+#include "iris_handles.hpp"
 
-static thread_local std::string g_err;
-
-static int fail(int code, const std::string &msg) {
-    g_err = msg;
-    return code;
-}
-
-#define HIPCHK(x)                                                                                   \
-    do {                                                                                            \
-        hipError_t e_ = (x);                                                                        \
-        if (e_ != hipSuccess) return fail(IRIS_E_HIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
-    } while (0)
-
-#define CHK(x)                   \
-    do {                         \
-        int rc_ = (x);           \
-        if (rc_ != 0) return rc_; \
-    } while (0)
-
-#define ARG(cond, msg)                                    \
-    do {                                                  \
-        if (!(cond)) return fail(IRIS_E_ARG, (msg));      \
-    } while (0)
-
-// ------------------------------------------------------------------ handles
-
-struct KStat {
-    uint64_t launches = 0, items = 0;
-    double ms = 0;
-};
-
-struct Pending {
-    std::string name;
-    hipEvent_t a, b;
-    uint64_t items;
-};
-
-struct DevBuf {
-    void *p = nullptr;
-    size_t cap = 0;
-};
-
-struct iris_device {
-    int ordinal = 0;
-    hipStream_t stream = nullptr;
-    std::recursive_mutex mu;
-    bool profiling = false;
-    std::map<std::string, KStat> stats;
-    std::vector<Pending> pending;
-    std::vector<hipEvent_t> event_pool;
-    DevBuf partials, result, staging, out_a, out_b;
-};
-
-struct iris_db {
-    iris_device *dev = nullptr;
-    KindInfo k{};
-    uint64_t len = 0, cap = 0;
-    void *data = nullptr;
-};
-
-struct iris_engine {
-    iris_device *dev = nullptr;
-    int kind = 0;             // IRIS_KIND_* of the DB it runs against
-    void *qtab = nullptr;     // SGPR rotated-query table (LANES kernels)
-    void *qfrag = nullptr;    // fp4 query fragments (TILES kernel, templates only)
-    uint32_t nq = 0;          // > 0: batched template engine (qfrag = nq padded query tiles)
-};
+using namespace iris_api;
 
 namespace {
-
-int set_device(iris_device *d) {
-    HIPCHK(hipSetDevice(d->ordinal));
-    return 0;
-}
-
-int ensure(DevBuf &b, size_t bytes) {
-    if (bytes <= b.cap) return 0;
-    if (b.p) HIPCHK(hipFree(b.p));
-    b.p = nullptr;
-    b.cap = 0;
-    size_t want = std::max(bytes, (size_t)4096);
-    hipError_t e = hipMalloc(&b.p, want);
-    if (e != hipSuccess) return fail(IRIS_E_NOMEM, std::string("hipMalloc workspace: ") + hipGetErrorString(e));
-    b.cap = want;
-    return 0;
-}
-
-hipEvent_t take_event(iris_device *d) {
-    if (!d->event_pool.empty()) {
-        hipEvent_t e = d->event_pool.back();
-        d->event_pool.pop_back();
-        return e;
-    }
-    hipEvent_t e = nullptr;
-    if (hipEventCreate(&e) != hipSuccess) return nullptr;
-    return e;
-}
-
-// Runs `launch` on the device stream, bracketed by HIP events when profiling.
-template <class F>
-int timed(iris_device *d, const char *name, uint64_t items, F &&launch) {
-    hipEvent_t a = nullptr, b = nullptr;
-    if (d->profiling) {
-        a = take_event(d);
-        b = take_event(d);
-        if (a && b) HIPCHK(hipEventRecord(a, d->stream));
-    }
-    int rc = launch();
-    if (rc != 0) return fail(IRIS_E_HIP, std::string("kernel launch failed: ") + name + ": " +
-                                             hipGetErrorString(hipGetLastError()));
-    if (d->profiling && a && b) {
-        HIPCHK(hipEventRecord(b, d->stream));
-        d->pending.push_back(Pending{name, a, b, items});
-    }
-    return 0;
-}
-
-// Waits for the stream, then folds recorded kernel times into the stats.
-int sync(iris_device *d) {
-    HIPCHK(hipStreamSynchronize(d->stream));
-    for (auto &p : d->pending) {
-        float ms = 0;
-        HIPCHK(hipEventElapsedTime(&ms, p.a, p.b));
-        KStat &s = d->stats[p.name];
-        s.launches += 1;
-        s.ms += ms;
-        s.items += p.items;
-        d->event_pool.push_back(p.a);
-        d->event_pool.push_back(p.b);
-    }
-    d->pending.clear();
-    return 0;
-}
-
-constexpr size_t kStagingBytes = 256ull << 20;  // H2D/D2H staging per chunk
-
-uint64_t chunk_records(const KindInfo &k) { return std::max<uint64_t>(64, kStagingBytes / k.rec_bytes / 64 * 64); }
-
-int check_kind(int kind) {
-    if (kind != IRIS_KIND_MASKS && kind != IRIS_KIND_SHARES && kind != IRIS_KIND_TEMPLATES)
-        return fail(IRIS_E_ARG, "unknown record kind");
-    return 0;
-}
 
 int db_write_locked(iris_db *db, uint64_t index, const void *records, uint64_t n) {
     iris_device *d = db->dev;

@@ -96,6 +96,10 @@ def load_library(path=None):
             "iris_db_read": ([P, u64, u64, P], ctypes.c_int),
             "iris_db_generate": ([P, u64, u64, u64], ctypes.c_int),
             "iris_db_clear": ([P], ctypes.c_int),
+            "iris_db_load_file": ([P, ctypes.c_char_p, u64, u64, ctypes.POINTER(u64)], ctypes.c_int),
+            "iris_db_save_file": ([P, ctypes.c_char_p, u64, u64], ctypes.c_int),
+            "iris_templates_read_json": ([ctypes.c_char_p, P, u64, ctypes.POINTER(u64)], ctypes.c_int),
+            "iris_templates_write_json": ([ctypes.c_char_p, P, u64], ctypes.c_int),
             "iris_masks_engine_new": ([P, P, PP], ctypes.c_int),
             "iris_distance_engine_new": ([P, P, PP], ctypes.c_int),
             "iris_template_engine_new": ([P, P, PP], ctypes.c_int),
@@ -141,8 +145,27 @@ def exported_symbols():
         "iris_engine_batch_process_host", "iris_engine_batch_process_device", "iris_template_counts", "iris_template_distances", "iris_template_search",
         "iris_template_batch_engine_new", "iris_template_batch_search", "iris_resolver_search",
         "iris_resolver_search_host", "iris_dot_bool_batch", "iris_dot_u16_batch", "iris_bits_rotated", "iris_encoded_rotated", "iris_encode",
-        "iris_decode_distance", "iris_match_merge",
+        "iris_decode_distance", "iris_match_merge", "iris_db_load_file", "iris_db_save_file",
+        "iris_templates_read_json", "iris_templates_write_json",
     ]
+
+
+def read_templates_json(path):
+    """JSON array of {"pattern": hex, "mask": hex} (src/bits.rs:74-93) -> uint64 [n, 400]
+    (pattern limbs then mask limbs, the Template byte layout)."""
+    lib = load_library()
+    n = ctypes.c_uint64(0)
+    _check(lib.iris_templates_read_json(os.fsencode(path), None, 0, ctypes.byref(n)))
+    out = np.zeros((n.value, 2 * LIMBS), np.uint64)
+    if n.value:
+        _check(lib.iris_templates_read_json(os.fsencode(path), _ptr(out), n.value, ctypes.byref(n)))
+    return out
+
+
+def write_templates_json(path, templates):
+    """Inverse of read_templates_json (compact JSON, lowercase hex)."""
+    a = np.ascontiguousarray(np.asarray(templates, np.uint64).reshape(-1, 2 * LIMBS))
+    _check(load_library().iris_templates_write_json(os.fsencode(path), _ptr(a), a.shape[0]))
 
 
 def _check(rc):
@@ -496,6 +519,21 @@ class Database:
 
     def clear(self):
         _check(load_library().iris_db_clear(self.handle))
+
+    def load_file(self, path, first=0, count=None):
+        """Appends records [first, first+count) of a raw record file (.masks / .share-i /
+        raw templates; src/main.rs:386-400,455-469).  Returns the number appended."""
+        got = ctypes.c_uint64(0)
+        cnt = (1 << 64) - 1 if count is None else int(count)
+        _check(load_library().iris_db_load_file(self.handle, os.fsencode(path), int(first), cnt,
+                                                ctypes.byref(got)))
+        return got.value
+
+    def save_file(self, path, first=0, n=None):
+        """Writes records [first, first+n) to a raw record file."""
+        if n is None:
+            n = len(self) - int(first)
+        _check(load_library().iris_db_save_file(self.handle, os.fsencode(path), int(first), int(n)))
 
 
 # ====================================================================== engines
