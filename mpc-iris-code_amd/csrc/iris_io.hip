@@ -1,5 +1,6 @@
 // iris_io.hip — the reference's on-disk record formats <-> device databases,
-// and its JSON template format.
+// its JSON template format, and the C ABI of share
+// preparation (row 4; kernel in iris_prepare.hip).
 //
 // Record files are the raw little-endian bytes of bytemuck::bytes_of over a
 // slice of records, exactly what `prepare` writes and `participant` /
@@ -351,3 +352,61 @@ int iris_templates_write_json(const char *path, const iris_template_t *t, uint64
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------------ share preparation
+
+extern "C" int iris_prepare_shares(const iris_db_t *templates, uint64_t first, uint64_t n, uint64_t index_base,
+                                   const uint8_t key[32], uint64_t nonce, uint32_t parties,
+                                   iris_db_t *const *shares, iris_db_t *masks) {
+    ARG(templates && key && shares, "NULL argument");
+    ARG(parties >= 1 && parties <= 64, "parties must be 1..64 (EncodedBits::share asserts n > 0)");
+    ARG(templates->k.kind == IRIS_KIND_TEMPLATES, "iris_prepare_shares needs a template database");
+    iris_device *d = templates->dev;
+    for (uint32_t j = 0; j < parties; ++j) {
+        ARG(shares[j] && shares[j]->k.kind == IRIS_KIND_SHARES, "shares[j] must be a share database");
+        ARG(shares[j]->dev == d, "all databases must live on one device");
+        for (uint32_t i = 0; i < j; ++i) ARG(shares[i] != shares[j], "share databases must be distinct");
+        if (n > shares[j]->cap - shares[j]->len) return fail(IRIS_E_RANGE, "share database capacity exceeded");
+    }
+    if (masks) {
+        ARG(masks->k.kind == IRIS_KIND_MASKS && masks->dev == d, "masks must be a masks database on the same device");
+        if (n > masks->cap - masks->len) return fail(IRIS_E_RANGE, "masks database capacity exceeded");
+    }
+    std::lock_guard<std::recursive_mutex> g(d->mu);
+    CHK(set_device(d));
+    if (first > templates->len || n > templates->len - first)
+        return fail(IRIS_E_RANGE, "record range outside the database");
+    if (n == 0) return 0;
+    // staging: templates (3200 B) | masks (1600 B) | parties shares (25600 B each) per record
+    const size_t tb = kind_info(IRIS_KIND_TEMPLATES, IRIS_LAYOUT_TILES).rec_bytes;
+    const size_t mb = kind_info(IRIS_KIND_MASKS, IRIS_LAYOUT_TILES).rec_bytes;
+    const size_t sb = kind_info(IRIS_KIND_SHARES, IRIS_LAYOUT_TILES).rec_bytes;
+    const size_t per = tb + mb + (size_t)parties * sb;
+    const uint64_t ch = std::max<uint64_t>(64, (kStagingBytes / per) / 64 * 64);
+    const uint64_t m0 = std::min<uint64_t>(ch, n);
+    CHK(ensure(d->staging, m0 * per));
+    char *st_t = (char *)d->staging.p, *st_m = st_t + m0 * tb, *st_s = st_m + m0 * mb;
+    std::vector<uint64_t> base(parties);
+    for (uint32_t j = 0; j < parties; ++j) base[j] = shares[j]->len;
+    const uint64_t mbase = masks ? masks->len : 0;
+    for (uint64_t off = 0; off < n; off += ch) {
+        const uint64_t m = std::min<uint64_t>(ch, n - off);
+        CHK(timed(d, "unpack", m,
+                  [&] { return launch_unpack(d->stream, templates->k, templates->data, st_t, first + off, m); }));
+        CHK(timed(d, "prepare", m, [&] {
+            return launch_prepare_shares(d->stream, st_t, m, index_base + first + off, key, nonce, parties, st_s);
+        }));
+        for (uint32_t j = 0; j < parties; ++j)
+            CHK(timed(d, "pack", m, [&] {
+                return launch_pack(d->stream, shares[j]->k, st_s + (size_t)j * m * sb, shares[j]->data, base[j] + off, m);
+            }));
+        if (masks) {
+            HIPCHK(hipMemcpy2DAsync(st_m, mb, st_t + mb, tb, mb, m, hipMemcpyDeviceToDevice, d->stream));
+            CHK(timed(d, "pack", m, [&] { return launch_pack(d->stream, masks->k, st_m, masks->data, mbase + off, m); }));
+        }
+        CHK(sync(d));
+    }
+    for (uint32_t j = 0; j < parties; ++j) shares[j]->len = base[j] + n;
+    if (masks) masks->len = mbase + n;
+    return 0;
+}

@@ -1,0 +1,126 @@
+// iris_prepare.hip — secret-share preparation on the device (SURVEY.md §8(f)
+// row 4): the reference's `prepare` (src/main.rs:333-361) turns every
+// Template into a `.masks` record (its mask) and `count` additive shares of
+// encode(template) (EncodedBits::share, src/encoded_bits.rs:23-38): count-1
+// uniformly random EncodedBits and a last share = encode - sum(rest), mod 2^16.
+//
+// Randomness: ChaCha20 (D. J. Bernstein's original: 64-bit nonce, 64-bit
+// block counter) keyed by the caller's 256-bit key, in counter mode, so every
+// (template, share, 64-byte block) is an independent thread of work:
+//   block counter = (g * (parties-1) + j) * 400 + b   (g = global template index)
+//   share j, elements 32b .. 32b+31 = the block's 32 little-endian u16.
+// The reference draws from rand's thread_rng (a ChaCha-based CSPRNG seeded
+// from the OS); its stream is unseeded and not reproducible, so parity here is
+// against the oracle's restatement of this derivation (oracle/iris_oracle.c,
+// pinned by the RFC 8439 ChaCha20 vectors) plus the share-sum identity.
+//
+// One thread per (template, block b): element block b of encode(t) needs
+// pattern and mask dword b only (element i = bit i, LE limbs), so the thread
+// computes parties-1 keystream blocks, writes them as 64-byte rows of shares
+// 0..parties-2, and the last share's row as encode minus their sum.
+#include <hip/hip_runtime.h>
+
+#include "iris_internal.hpp"
+
+namespace iris {
+
+struct ChachaKey {
+    uint32_t k[8];
+};
+
+__device__ __forceinline__ uint32_t rotl(uint32_t x, int r) { return __builtin_rotateleft32(x, r); }
+
+#define CC_QR(a, b, c, d)   \
+    a += b;                 \
+    d = rotl(d ^ a, 16);    \
+    c += d;                 \
+    b = rotl(b ^ c, 12);    \
+    a += b;                 \
+    d = rotl(d ^ a, 8);     \
+    c += d;                 \
+    b = rotl(b ^ c, 7);
+
+__device__ __forceinline__ void chacha20_block(const ChachaKey &key, uint64_t nonce, uint64_t counter,
+                                               uint32_t out[16]) {
+    const uint32_t in[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u, key.k[0], key.k[1],
+                             key.k[2],    key.k[3],    key.k[4],    key.k[5],    key.k[6], key.k[7],
+                             (uint32_t)counter, (uint32_t)(counter >> 32), (uint32_t)nonce,
+                             (uint32_t)(nonce >> 32)};
+    uint32_t x[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) x[i] = in[i];
+#pragma unroll 2
+    for (int r = 0; r < 10; ++r) {
+        CC_QR(x[0], x[4], x[8], x[12]);
+        CC_QR(x[1], x[5], x[9], x[13]);
+        CC_QR(x[2], x[6], x[10], x[14]);
+        CC_QR(x[3], x[7], x[11], x[15]);
+        CC_QR(x[0], x[5], x[10], x[15]);
+        CC_QR(x[1], x[6], x[11], x[12]);
+        CC_QR(x[2], x[7], x[8], x[13]);
+        CC_QR(x[3], x[4], x[9], x[14]);
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) out[i] = x[i] + in[i];
+}
+
+constexpr int kBlocks = IRIS_BITS / 32;  // 400 keystream blocks per share
+
+// templates: m reference-layout records (pattern dwords 0..399, mask 400..799)
+// shares: [parties][m][12800] u16
+__global__ void __launch_bounds__(256) prepare_shares_kernel(const uint32_t *__restrict__ templates, uint64_t m,
+                                                             uint64_t g0, ChachaKey key, uint64_t nonce,
+                                                             uint32_t parties, uint16_t *__restrict__ shares) {
+    const uint64_t total = m * kBlocks;
+    for (uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; tid < total;
+         tid += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t i = tid / kBlocks;
+        const int b = (int)(tid - i * kBlocks);
+        const uint32_t pw = templates[i * (2 * kPlaneDwords) + b];
+        const uint32_t mw = templates[i * (2 * kPlaneDwords) + kPlaneDwords + b];
+        // last[e] accumulates encode - sum, two u16 lanes per dword (independent mod 2^16 halves)
+        uint32_t last[16];
+#pragma unroll
+        for (int w = 0; w < 16; ++w) {
+            const uint32_t m0 = (mw >> (2 * w)) & 1u, m1 = (mw >> (2 * w + 1)) & 1u;
+            const uint32_t p0 = (pw >> (2 * w)) & 1u, p1 = (pw >> (2 * w + 1)) & 1u;
+            const uint32_t e0 = (m0 - 2u * (p0 & m0)) & 0xFFFFu, e1 = (m1 - 2u * (p1 & m1)) & 0xFFFFu;
+            last[w] = e0 | (e1 << 16);
+        }
+        const uint64_t g = g0 + i;
+        for (uint32_t j = 0; j + 1 < parties; ++j) {
+            uint32_t r[16];
+            chacha20_block(key, nonce, (g * (parties - 1) + j) * kBlocks + (uint64_t)b, r);
+            uint4 *dst = (uint4 *)(shares + ((uint64_t)j * m + i) * IRIS_BITS + 32 * b);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) dst[q] = make_uint4(r[4 * q], r[4 * q + 1], r[4 * q + 2], r[4 * q + 3]);
+#pragma unroll
+            for (int w = 0; w < 16; ++w) {
+                const uint32_t lo = (last[w] - r[w]) & 0xFFFFu;
+                const uint32_t hi = ((last[w] >> 16) - (r[w] >> 16)) & 0xFFFFu;
+                last[w] = lo | (hi << 16);
+            }
+        }
+        uint4 *dst = (uint4 *)(shares + ((uint64_t)(parties - 1) * m + i) * IRIS_BITS + 32 * b);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            dst[q] = make_uint4(last[4 * q], last[4 * q + 1], last[4 * q + 2], last[4 * q + 3]);
+    }
+}
+
+int launch_prepare_shares(void *stream, const void *templates, uint64_t m, uint64_t g0, const uint8_t key[32],
+                          uint64_t nonce, uint32_t parties, void *shares) {
+    if (m == 0) return 0;
+    ChachaKey k;
+    for (int i = 0; i < 8; ++i)
+        k.k[i] = (uint32_t)key[4 * i] | ((uint32_t)key[4 * i + 1] << 8) | ((uint32_t)key[4 * i + 2] << 16) |
+                 ((uint32_t)key[4 * i + 3] << 24);
+    const uint64_t total = m * kBlocks;
+    uint64_t grid = (total + 255) / 256;
+    if (grid > 256ull * 64) grid = 256ull * 64;
+    hipLaunchKernelGGL(prepare_shares_kernel, dim3((uint32_t)grid), dim3(256), 0, (hipStream_t)stream,
+                       (const uint32_t *)templates, m, g0, k, nonce, parties, (uint16_t *)shares);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace iris

@@ -100,6 +100,7 @@ def load_library(path=None):
             "iris_db_save_file": ([P, ctypes.c_char_p, u64, u64], ctypes.c_int),
             "iris_templates_read_json": ([ctypes.c_char_p, P, u64, ctypes.POINTER(u64)], ctypes.c_int),
             "iris_templates_write_json": ([ctypes.c_char_p, P, u64], ctypes.c_int),
+            "iris_prepare_shares": ([P, u64, u64, u64, P, u64, ctypes.c_uint32, P, P], ctypes.c_int),
             "iris_masks_engine_new": ([P, P, PP], ctypes.c_int),
             "iris_distance_engine_new": ([P, P, PP], ctypes.c_int),
             "iris_template_engine_new": ([P, P, PP], ctypes.c_int),
@@ -146,7 +147,7 @@ def exported_symbols():
         "iris_template_batch_engine_new", "iris_template_batch_search", "iris_resolver_search",
         "iris_resolver_search_host", "iris_dot_bool_batch", "iris_dot_u16_batch", "iris_bits_rotated", "iris_encoded_rotated", "iris_encode",
         "iris_decode_distance", "iris_match_merge", "iris_db_load_file", "iris_db_save_file",
-        "iris_templates_read_json", "iris_templates_write_json",
+        "iris_templates_read_json", "iris_templates_write_json", "iris_prepare_shares",
     ]
 
 
@@ -166,6 +167,25 @@ def write_templates_json(path, templates):
     """Inverse of read_templates_json (compact JSON, lowercase hex)."""
     a = np.ascontiguousarray(np.asarray(templates, np.uint64).reshape(-1, 2 * LIMBS))
     _check(load_library().iris_templates_write_json(os.fsencode(path), _ptr(a), a.shape[0]))
+
+
+def prepare_shares(templates, shares, masks=None, key=None, nonce=0, first=0, n=None, index_base=0):
+    """`prepare` on the device (src/main.rs:333-361): appends EncodedBits::share(len(shares))
+    of encode(templates[first:first+n]) to the share Databases and, optionally, the masks to
+    a masks Database.  key: 32 bytes (default: os.urandom, a CSPRNG).  Returns the key."""
+    if key is None:
+        key = os.urandom(32)
+    key = bytes(key)
+    if len(key) != 32:
+        raise ValueError("key must be 32 bytes")
+    if n is None:
+        n = len(templates) - int(first)
+    kbuf = (ctypes.c_uint8 * 32).from_buffer_copy(key)
+    arr = (ctypes.c_void_p * len(shares))(*[s.handle for s in shares])
+    _check(load_library().iris_prepare_shares(templates.handle, int(first), int(n), int(index_base), kbuf,
+                                              int(nonce), len(shares), arr,
+                                              masks.handle if masks is not None else None))
+    return key
 
 
 def _check(rc):

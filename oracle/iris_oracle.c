@@ -375,3 +375,72 @@ void orc_gen_masks(uint64_t seed, uint64_t t0, uint64_t n, uint64_t *out) {
 void orc_gen_shares(uint64_t seed, uint64_t t0, uint64_t n, uint16_t *out) {
     for (uint64_t i = 0; i < n; ++i) orc_gen_share(seed, t0 + i, out + i * ORC_BITS);
 }
+
+/* ------------------------------------------------------------ share preparation */
+
+static uint32_t orc_rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+
+#define ORC_QR(a, b, c, d)                  \
+    do {                                    \
+        a += b; d ^= a; d = orc_rotl32(d, 16); \
+        c += d; b ^= c; b = orc_rotl32(b, 12); \
+        a += b; d ^= a; d = orc_rotl32(d, 8);  \
+        c += d; b ^= c; b = orc_rotl32(b, 7);  \
+    } while (0)
+
+void orc_chacha20_block(const uint8_t key[32], uint64_t nonce, uint64_t counter, uint8_t out[64]) {
+    uint32_t in[16], x[16];
+    in[0] = 0x61707865u; /* "expand 32-byte k" */
+    in[1] = 0x3320646eu;
+    in[2] = 0x79622d32u;
+    in[3] = 0x6b206574u;
+    for (int i = 0; i < 8; ++i)
+        in[4 + i] = (uint32_t)key[4 * i] | ((uint32_t)key[4 * i + 1] << 8) | ((uint32_t)key[4 * i + 2] << 16) |
+                    ((uint32_t)key[4 * i + 3] << 24);
+    in[12] = (uint32_t)counter;
+    in[13] = (uint32_t)(counter >> 32);
+    in[14] = (uint32_t)nonce;
+    in[15] = (uint32_t)(nonce >> 32);
+    memcpy(x, in, sizeof x);
+    for (int r = 0; r < 10; ++r) {
+        ORC_QR(x[0], x[4], x[8], x[12]);
+        ORC_QR(x[1], x[5], x[9], x[13]);
+        ORC_QR(x[2], x[6], x[10], x[14]);
+        ORC_QR(x[3], x[7], x[11], x[15]);
+        ORC_QR(x[0], x[5], x[10], x[15]);
+        ORC_QR(x[1], x[6], x[11], x[12]);
+        ORC_QR(x[2], x[7], x[8], x[13]);
+        ORC_QR(x[3], x[4], x[9], x[14]);
+    }
+    for (int i = 0; i < 16; ++i) {
+        const uint32_t v = x[i] + in[i];
+        out[4 * i] = (uint8_t)v;
+        out[4 * i + 1] = (uint8_t)(v >> 8);
+        out[4 * i + 2] = (uint8_t)(v >> 16);
+        out[4 * i + 3] = (uint8_t)(v >> 24);
+    }
+}
+
+void orc_prepare_shares(const orc_template *t, uint64_t n, uint64_t index_base, const uint8_t key[32],
+                        uint64_t nonce, uint32_t parties, uint16_t *shares, uint64_t *masks) {
+    uint16_t enc[ORC_BITS];
+    uint8_t blk[64];
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint64_t g = index_base + i;
+        orc_encode(&t[i], enc);
+        uint16_t *last = shares + ((uint64_t)(parties - 1) * n + i) * ORC_BITS;
+        memcpy(last, enc, sizeof enc);
+        for (uint32_t j = 0; j + 1 < parties; ++j) {
+            uint16_t *sh = shares + ((uint64_t)j * n + i) * ORC_BITS;
+            for (int b = 0; b < ORC_BITS / 32; ++b) {
+                orc_chacha20_block(key, nonce, (g * (parties - 1) + j) * (ORC_BITS / 32) + (uint64_t)b, blk);
+                for (int e = 0; e < 32; ++e) {
+                    const uint16_t v = (uint16_t)(blk[2 * e] | (blk[2 * e + 1] << 8));
+                    sh[32 * b + e] = v;
+                    last[32 * b + e] = (uint16_t)(last[32 * b + e] - v);
+                }
+            }
+        }
+        if (masks) memcpy(masks + i * ORC_LIMBS, t[i].mask, sizeof t[i].mask);
+    }
+}

@@ -55,6 +55,8 @@ def load(path=None):
     lib.orc_gen_templates.argtypes = [u64, u64, u64, P]
     lib.orc_gen_masks.argtypes = [u64, u64, u64, P]
     lib.orc_gen_shares.argtypes = [u64, u64, u64, P]
+    lib.orc_chacha20_block.argtypes = [P, u64, u64, P]
+    lib.orc_prepare_shares.argtypes = [P, u64, u64, P, u64, ctypes.c_uint32, P, P]
     if path is None:
         _lib = lib
     return lib
@@ -181,3 +183,25 @@ def gen_shares(seed, t0, n):
     out = np.empty((n, BITS), np.uint16)
     load().orc_gen_shares(seed, t0, n, _p(out))
     return out
+
+
+def chacha20_block(key, nonce, counter):
+    """64 keystream bytes (DJB ChaCha20: 64-bit nonce, 64-bit block counter)."""
+    k = np.frombuffer(bytes(key), np.uint8).copy()
+    assert k.size == 32
+    out = np.zeros(64, np.uint8)
+    load().orc_chacha20_block(_p(k), int(nonce), int(counter), _p(out))
+    return out.tobytes()
+
+
+def prepare_shares(templates, key, nonce=0, parties=3, index_base=0):
+    """EncodedBits::share of encode(t) with the ChaCha20 stream of orc_prepare_shares:
+    returns (shares [parties][n][12800] u16, masks [n][200] u64)."""
+    t = np.ascontiguousarray(np.asarray(templates, np.uint64).reshape(-1, 400))
+    n = t.shape[0]
+    k = np.frombuffer(bytes(key), np.uint8).copy()
+    assert k.size == 32
+    shares = np.zeros((parties, n, 12800), np.uint16)
+    masks = np.zeros((n, 200), np.uint64)
+    load().orc_prepare_shares(_p(t), n, int(index_base), _p(k), int(nonce), int(parties), _p(shares), _p(masks))
+    return shares, masks

@@ -186,3 +186,54 @@ def gen_shares(seed, t0, n):
     j = np.arange(BITS // 4, dtype=np.uint64)[None, :]
     limbs = np.ascontiguousarray(gen_limbs(seed, 1, t * np.uint64(3200) + j))
     return limbs.view("<u2").reshape(n, BITS)
+
+
+# ---------------------------------------------------------------- share preparation (§8(f) row 4)
+
+def _rotl32(x, r):
+    return ((x << np.uint32(r)) | (x >> np.uint32(32 - r))).astype(np.uint32)
+
+
+def chacha20_blocks(key, nonce, counters):
+    """Vectorised ChaCha20 blocks (DJB: 64-bit nonce, 64-bit counter) -> uint8 [len(counters), 64]."""
+    k = np.frombuffer(bytes(key), "<u4")
+    c = np.asarray(counters, np.uint64)
+    n = c.size
+    st = np.empty((16, n), np.uint32)
+    st[0:4] = np.array([0x61707865, 0x3320646E, 0x79622D32, 0x6B206574], np.uint32)[:, None]
+    st[4:12] = k[:, None]
+    st[12] = (c & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+    st[13] = (c >> np.uint64(32)).astype(np.uint32)
+    st[14] = np.uint32(nonce & 0xFFFFFFFF)
+    st[15] = np.uint32(nonce >> 32)
+    x = st.copy()
+
+    def qr(a, b, cc, d):
+        x[a] += x[b]; x[d] = _rotl32(x[d] ^ x[a], 16)
+        x[cc] += x[d]; x[b] = _rotl32(x[b] ^ x[cc], 12)
+        x[a] += x[b]; x[d] = _rotl32(x[d] ^ x[a], 8)
+        x[cc] += x[d]; x[b] = _rotl32(x[b] ^ x[cc], 7)
+
+    for _ in range(10):
+        qr(0, 4, 8, 12); qr(1, 5, 9, 13); qr(2, 6, 10, 14); qr(3, 7, 11, 15)
+        qr(0, 5, 10, 15); qr(1, 6, 11, 12); qr(2, 7, 8, 13); qr(3, 4, 9, 14)
+    out = (x + st).astype("<u4").T.copy()
+    return out.view(np.uint8).reshape(n, 64)
+
+
+def prepare_shares(templates, key, nonce=0, parties=3, index_base=0):
+    """EncodedBits::share (src/encoded_bits.rs:23-38) with the counter-mode ChaCha20
+    derivation of oracle/iris_oracle.h: shares [parties][n][12800], masks [n][200]."""
+    t = np.asarray(templates, np.uint64).reshape(-1, 400)
+    n = t.shape[0]
+    shares = np.zeros((parties, n, 12800), np.uint16)
+    for i in range(n):
+        g = index_base + i
+        last = encode(t[i, :200], t[i, 200:]).astype(np.uint16)
+        for j in range(parties - 1):
+            ctr = (g * (parties - 1) + j) * 400 + np.arange(400, dtype=np.uint64)
+            sh = chacha20_blocks(key, nonce, ctr).view("<u2").reshape(12800)
+            shares[j, i] = sh
+            last = (last - sh).astype(np.uint16)
+        shares[parties - 1, i] = last
+    return shares, t[:, 200:].copy()
