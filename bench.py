@@ -55,10 +55,14 @@ def parse():
     ap.add_argument("--layout", choices=["tiles", "lanes"], default="tiles",
                     help="tiles = MFMA kernels (default), lanes = VALU kernels")
     ap.add_argument("--queries", type=int, default=1024, help="queries per batch (workload batch)")
-    ap.add_argument("--workload", choices=["search", "masks", "shares", "batch"], default="search",
+    ap.add_argument("--workload", choices=["search", "masks", "shares", "batch", "resolver", "prepare"],
+                    default="search",
                     help="search = Template masked Hamming + argmin (configs[1], default); "
                          "masks = MasksEngine denominators; shares = DistanceEngine u16 share dot (configs[3]); "
-                         "batch = --queries queries x 31 rotations x N templates in one pass (configs[2])")
+                         "batch = --queries queries x 31 rotations x N templates in one pass (configs[2]); "
+                         "resolver = fused share sum + decode + argmin over --parties [n][31] outputs; "
+                         "prepare = GPU share preparation of n templates into --parties share DBs + masks")
+    ap.add_argument("--parties", type=int, default=3, help="parties (workloads resolver, prepare)")
     return ap.parse_args()
 
 
@@ -123,6 +127,92 @@ def load_traffic(n_per_launch, layout):
     return None, None
 
 
+def run_aux(args, dev):
+    """Single-GPU lines for the §8(f) workloads beside the hot path: the fused
+    resolver (share sum + decode + argmin) and GPU share preparation."""
+    from oracle import oracle_c as oc  # result check only
+
+    P = args.parties
+    rng = np.random.default_rng(SEED)
+    ptrs = []
+    if args.workload == "resolver":
+        n = args.n_per_gpu
+        shares = rng.integers(0, 65536, (P, n, ROT), dtype=np.uint16)
+        denoms = rng.integers(0, 12801, (n, ROT), dtype=np.uint16)
+        for j in range(P + 1):
+            ptrs.append(dev.alloc(n * ROT * 2))
+            dev.h2d(ptrs[j], shares[j] if j < P else denoms)
+
+        def step():
+            return ih.resolver_search_device(dev, ptrs[:P], ptrs[P], n)
+
+        kname, unit = "resolver", "records/s"
+        rec_bytes = (P + 1) * ROT * 2  # P share rows + the denominator row, read once
+        workload = f"resolver: {P} participants' [u16;31] outputs + denominators -> min/argmin (src/main.rs:597-621)"
+    else:
+        n = min(args.n_per_gpu, 1_000_000)  # 3 share DBs of 1M = 77 GB
+        tdb = ih.Database(dev, ih.KIND_TEMPLATES, n)
+        tdb.generate(n, SEED)
+        sdbs = [ih.Database(dev, ih.KIND_SHARES, n) for _ in range(P)]
+        mdb = ih.Database(dev, ih.KIND_MASKS, n)
+        key = bytes(range(32))
+
+        def step():
+            for db in sdbs + [mdb]:
+                db.truncate(0)
+            ih.prepare_shares(tdb, sdbs, mdb, key=key)
+
+        kname, unit = "prepare", "templates/s"
+        rec_bytes = 3200 + P * 25600  # template in, P shares out (the prepare kernel)
+        workload = f"prepare: EncodedBits::share({P}) of encode(t) + masks, ChaCha20 counter mode (src/main.rs:333-361)"
+    for _ in range(args.warmup):
+        m = step()
+    dev.reset_stats()
+    dev.set_profiling(True)
+    dev.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        m = step()
+    dev.synchronize()
+    elapsed = time.perf_counter() - t0
+    dev.set_profiling(False)
+    launches, kms, items = dev.kernel_stats(kname)
+    achieved = rec_bytes * items / (kms * 1e-3) / 1e9
+    if args.workload == "resolver":
+        best, idx = oc.argmin(oc.resolver_combine(shares, denoms))
+        ok = m.index == idx and np.float64(m.distance).view(np.uint64) == np.float64(best).view(np.uint64)
+        check = {"oracle_index": int(idx), "found_index": int(m.index), "ok": bool(ok)}
+    else:
+        sample = [0, n // 3, n - 1]
+        ok = True
+        for i in sample:
+            want, wm = oc.prepare_shares(tdb.read(i, 1), key, parties=P, index_base=i)
+            ok &= all((sdbs[j].read(i, 1)[0] == want[j, 0]).all() for j in range(P))
+            ok &= bool((mdb.read(i, 1)[0] == wm[0]).all())
+        check = {"sampled_templates_vs_oracle": len(sample), "ok": bool(ok)}
+    line = {
+        "metric": {"resolver": "resolver records/s (share sum + decode + argmin)",
+                   "prepare": "templates prepared/s (shares + masks)"}[args.workload],
+        "value": n * args.steps / elapsed, "unit": unit, "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u16",
+        "data": "synthetic (uniform random u16 / on-device generated templates)",
+        "config": {"workload": workload, "records_per_gpu": n, "parties": P},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None},
+        "kernel": {"name": kname, "avg_ms": kms / max(1, launches), "launches": launches,
+                   "bytes_per_record": rec_bytes},
+        "cpu_baseline": None,
+        "check": check,
+    }
+    print(json.dumps(line))
+    for p in ptrs:
+        dev.free(p)
+    if not ok:
+        print("result check failed", file=sys.stderr)
+        sys.exit(3)
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -149,6 +239,10 @@ def main():
     lo = rank * n
     total = n * world
     dev = ih.Device(ordinal)
+    if args.workload in ("resolver", "prepare"):
+        if world > 1:
+            raise SystemExit("workloads resolver / prepare are single-GPU lines (run without torchrun)")
+        return run_aux(args, dev)
     layout = ih.LAYOUT_TILES if args.layout == "tiles" else ih.LAYOUT_LANES
     kind = {"search": ih.KIND_TEMPLATES, "batch": ih.KIND_TEMPLATES, "masks": ih.KIND_MASKS,
             "shares": ih.KIND_SHARES}[args.workload]

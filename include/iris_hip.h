@@ -106,6 +106,7 @@ int iris_device_reset_stats(iris_device_t *dev);
 int iris_device_alloc(iris_device_t *dev, size_t bytes, void **ptr);
 int iris_device_free(iris_device_t *dev, void *ptr);
 int iris_memcpy_d2h(iris_device_t *dev, void *host, const void *device, size_t bytes);
+int iris_memcpy_h2d(iris_device_t *dev, void *device, const void *host, size_t bytes);
 
 /* -------------------------------------------------------------- databases
  * Device-resident database of `kind` records.  Replaces the mmap'd share /
@@ -131,6 +132,8 @@ int iris_db_read(const iris_db_t *db, uint64_t first, uint64_t n, void *records)
  * src/encoded_bits.rs:81-87, src/template.rs:67-74). */
 int iris_db_generate(iris_db_t *db, uint64_t n, uint64_t seed, uint64_t global_index0);
 int iris_db_clear(iris_db_t *db);
+/* Drops the records [len, current length) (no device work; later appends overwrite them). */
+int iris_db_truncate(iris_db_t *db, uint64_t len);
 
 /* ---------------------------------------------------------------- on-disk formats
  * Record files hold the raw little-endian bytes of a record slice

@@ -258,6 +258,14 @@ int iris_memcpy_d2h(iris_device_t *d, void *host, const void *device, size_t byt
     return sync(d);
 }
 
+int iris_memcpy_h2d(iris_device_t *d, void *device, const void *host, size_t bytes) {
+    ARG(d && (bytes == 0 || (host && device)), "NULL argument");
+    std::lock_guard<std::recursive_mutex> g(d->mu);
+    CHK(set_device(d));
+    HIPCHK(hipMemcpyAsync(device, host, bytes, hipMemcpyHostToDevice, d->stream));
+    return sync(d);
+}
+
 // ------------------------------------------------------------------ databases
 
 int iris_db_create(iris_device_t *d, int kind, uint64_t capacity, iris_db_t **out) {
@@ -376,6 +384,14 @@ int iris_db_generate(iris_db_t *db, uint64_t n, uint64_t seed, uint64_t global_i
     CHK(timed(d, "generate", n, [&] { return launch_generate(d->stream, db->k, db->data, db->len, n, seed, global_index0); }));
     CHK(sync(d));
     db->len += n;
+    return 0;
+}
+
+int iris_db_truncate(iris_db_t *db, uint64_t len) {
+    ARG(db, "database is NULL");
+    std::lock_guard<std::recursive_mutex> g(db->dev->mu);
+    if (len > db->len) return fail(IRIS_E_RANGE, "iris_db_truncate: len beyond the current length");
+    db->len = len;
     return 0;
 }
 

@@ -96,6 +96,8 @@ def load_library(path=None):
             "iris_db_read": ([P, u64, u64, P], ctypes.c_int),
             "iris_db_generate": ([P, u64, u64, u64], ctypes.c_int),
             "iris_db_clear": ([P], ctypes.c_int),
+            "iris_db_truncate": ([P, u64], ctypes.c_int),
+            "iris_memcpy_h2d": ([P, P, P, ctypes.c_size_t], ctypes.c_int),
             "iris_db_load_file": ([P, ctypes.c_char_p, u64, u64, ctypes.POINTER(u64)], ctypes.c_int),
             "iris_db_save_file": ([P, ctypes.c_char_p, u64, u64], ctypes.c_int),
             "iris_templates_read_json": ([ctypes.c_char_p, P, u64, ctypes.POINTER(u64)], ctypes.c_int),
@@ -148,6 +150,7 @@ def exported_symbols():
         "iris_resolver_search_host", "iris_dot_bool_batch", "iris_dot_u16_batch", "iris_bits_rotated", "iris_encoded_rotated", "iris_encode",
         "iris_decode_distance", "iris_match_merge", "iris_db_load_file", "iris_db_save_file",
         "iris_templates_read_json", "iris_templates_write_json", "iris_prepare_shares",
+        "iris_db_truncate", "iris_memcpy_h2d",
     ]
 
 
@@ -438,6 +441,10 @@ class Device:
         _check(load_library().iris_memcpy_d2h(self.handle, _ptr(host_array), ctypes.c_void_p(device_ptr),
                                                host_array.nbytes))
 
+    def h2d(self, device_ptr, host_array):
+        a = np.ascontiguousarray(host_array)
+        _check(load_library().iris_memcpy_h2d(self.handle, ctypes.c_void_p(device_ptr), _ptr(a), a.nbytes))
+
 
 _default = None
 
@@ -539,6 +546,9 @@ class Database:
 
     def clear(self):
         _check(load_library().iris_db_clear(self.handle))
+
+    def truncate(self, n):
+        _check(load_library().iris_db_truncate(self.handle, int(n)))
 
     def load_file(self, path, first=0, count=None):
         """Appends records [first, first+count) of a raw record file (.masks / .share-i /
