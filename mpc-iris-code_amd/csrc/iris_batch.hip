@@ -58,21 +58,66 @@ __device__ __forceinline__ Partial b_shfl(const Partial &c, int off) {
     return o;
 }
 
+// s_waitcnt with only the vector-memory count bounded (expcnt, lgkmcnt at max)
+#define VMCNT(n) __builtin_amdgcn_s_waitcnt(0x0F70 | ((n) & 15) | (((n) >> 4) << 14))
+
+constexpr int kRows = 2 * (BQ + BT);  // 1-KB rows per stage: 4 queries + 8 tiles, 2 chunk pairs each
+constexpr int kRing = 4;              // LDS stages: 3 in flight + the one being read
+constexpr int kRowsPerWave = kRows / 8;
+
+// Staging is LDS-DMA (global_load_lds_dwordx4, lane-linear 1-KB rows) into a
+// 4-stage ring: each K-step waits for its own rows with a counted vmcnt (the
+// next two steps stay in flight across the raw s_barrier), then issues the
+// step three ahead into the slot everyone finished reading a step ago.
+// Each workgroup walks its N-groups as one flat stream of K-steps, so the
+// pipeline never drains between N-groups.
 __global__ void __launch_bounds__(512, 1)
     batch_kernel(const uint4 *__restrict__ db, const uint4 *__restrict__ qtiles, uint64_t tile0, uint64_t ntiles,
                  uint64_t first, uint64_t end, uint32_t nqg, uint32_t G, Partial *__restrict__ partials) {
-    __shared__ uint2 sA[2][BQ][KSTEP][64];
-    __shared__ uint2 sB[2][BT][KSTEP][64];
-    __shared__ Partial sP[8];
+    __shared__ uint4 ring[kRing][kRows][64];  // all LDS in one object (no vmcnt(0) before ds_reads)
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint32_t qg = blockIdx.x % nqg, gi = blockIdx.x / nqg;
     const int wq = w & 3, wsub = (w >> 2) * WT;
     const uint64_t ngroups = (ntiles + BT - 1) / BT;
+    const uint32_t my_groups = gi < ngroups ? (uint32_t)((ngroups - gi + G - 1) / G) : 0;
+    const uint32_t total = my_groups * NSTEPS;
 
-    // loader roles: A: query (tid >> 7), chunk pair (tid >> 6) & 1, lane; B: tile (tid >> 6), lane, both pairs
-    const uint4 *qsrc = qtiles + (uint64_t)(qg * BQ + (tid >> 7)) * kTileU4 + ((tid >> 6) & 1) * 64 + lane;
-    const int lb_t = tid >> 6;
+    // this wave's DMA rows: r = w, w + 8, w + 16 (rows 0..7 queries, 8..23 template tiles)
+    const uint4 *src_q[kRowsPerWave];
+    int row_t[kRowsPerWave];
+#pragma unroll
+    for (int i = 0; i < kRowsPerWave; ++i) {
+        const int r = w + 8 * i;
+        row_t[i] = r < 2 * BQ ? -1 : (r - 2 * BQ) >> 1;
+        const int gp = r & 1;
+        src_q[i] = r < 2 * BQ ? qtiles + (uint64_t)(qg * BQ + (r >> 1)) * kTileU4 + gp * 64 + lane
+                              : db + gp * 64 + lane;
+    }
+    auto issue = [&](uint32_t s) {
+        const uint32_t j = s / NSTEPS, k = s - j * NSTEPS;
+        const uint64_t ng = gi + (uint64_t)j * G;
+#pragma unroll
+        for (int i = 0; i < kRowsPerWave; ++i) {
+            const int r = w + 8 * i;
+            const uint4 *src;
+            if (row_t[i] < 0) {
+                src = src_q[i] + (2 * k) * 64;
+            } else {
+                const uint64_t trel = ng * BT + row_t[i];
+                src = src_q[i] + (tile0 + (trel < ntiles ? trel : ntiles - 1)) * (uint64_t)kTileU4 + (2 * k) * 64;
+            }
+            // LDS-DMA in inline asm: hipcc's waitcnt pass would otherwise wait vmcnt(0)
+            // before every ds_read of the ring; the counted VMCNT waits below own these
+            const uint32_t dst = __builtin_amdgcn_readfirstlane(
+                (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void *)&ring[s % kRing][r][0]);
+            uint32_t keep;
+            asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                         : "=&s"(keep)
+                         : "v"(src), "s"(dst)
+                         : "memory");
+        }
+    };
 
     Partial best;
     best.num = 0;
@@ -80,62 +125,59 @@ __global__ void __launch_bounds__(512, 1)
     best.rot = 0;
     best.pad = 0;
     best.idx = ~0ull;
-
-    for (uint64_t ng = gi; ng < ngroups; ng += G) {
-        const uint64_t trel = ng * BT + lb_t;
-        const uint4 *bsrc = db + (tile0 + (trel < ntiles ? trel : ntiles - 1)) * (uint64_t)kTileU4 + lane;
-        v16f den[WT], s[WT];
+    v16f den[WT], sacc[WT];
+    auto zero = [&] {
 #pragma unroll
         for (int t = 0; t < WT; ++t)
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
                 den[t][i] = 0.f;
-                s[t][i] = 0.f;
+                sacc[t][i] = 0.f;
             }
-        uint4 ra, rb0, rb1;
-        auto gload = [&](int step) {  // chunk pairs 2*step, 2*step+1
-            ra = qsrc[(2 * step) * 64];
-            rb0 = bsrc[(2 * step) * 64];
-            rb1 = bsrc[(2 * step + 1) * 64];
-        };
-        auto lstore = [&](int buf) {
-            const int qa = tid >> 7, gp = (tid >> 6) & 1;
-            sA[buf][qa][2 * gp][lane] = make_uint2(ra.x, ra.y);
-            sA[buf][qa][2 * gp + 1][lane] = make_uint2(ra.z, ra.w);
-            sB[buf][lb_t][0][lane] = make_uint2(rb0.x, rb0.y);
-            sB[buf][lb_t][1][lane] = make_uint2(rb0.z, rb0.w);
-            sB[buf][lb_t][2][lane] = make_uint2(rb1.x, rb1.y);
-            sB[buf][lb_t][3][lane] = make_uint2(rb1.z, rb1.w);
-        };
-        gload(0);
-        lstore(0);
-        __syncthreads();
+    };
+    zero();
+    for (uint32_t s = 0; s < 3 && s < total; ++s) issue(s);
+
 #pragma unroll 1
-        for (int st = 0; st < NSTEPS; ++st) {
-            const int buf = st & 1;
-            if (st + 1 < NSTEPS) gload(st + 1);
+    for (uint32_t s = 0; s < total; ++s) {
+        // wait for this step's rows (this wave's), then for everyone's
+        if (s + 2 < total) {
+            VMCNT(2 * kRowsPerWave);
+        } else if (s + 1 < total) {
+            VMCNT(kRowsPerWave);
+        } else {
+            VMCNT(0);
+        }
+        __builtin_amdgcn_s_barrier();
+        if (s + 3 < total) issue(s + 3);
+        const uint4(*st)[64] = ring[s % kRing];
 #pragma unroll
-            for (int c = 0; c < KSTEP; ++c) {
-                const uint2 a = sA[buf][wq][c][lane];
-                const v8i aden = {(int)(a.x & 0x22222222u), (int)((a.x & 0x11111111u) << 2), (int)(a.y & 0x22222222u),
-                                  (int)((a.y & 0x11111111u) << 2), 0, 0, 0, 0};
-                const v8i aenc = {(int)(a.x & 0xAAAAAAAAu), (int)((a.x << 1) & 0xAAAAAAAAu), (int)(a.y & 0xAAAAAAAAu),
-                                  (int)((a.y << 1) & 0xAAAAAAAAu), 0, 0, 0, 0};
+        for (int gp = 0; gp < 2; ++gp) {
+            const uint4 a4 = st[2 * wq + gp][lane];
+#pragma unroll
+            for (int h2 = 0; h2 < 2; ++h2) {
+                const uint32_t ax = h2 ? a4.z : a4.x, ay = h2 ? a4.w : a4.y;
+                const v8i aden = {(int)(ax & 0x22222222u), (int)((ax & 0x11111111u) << 2), (int)(ay & 0x22222222u),
+                                  (int)((ay & 0x11111111u) << 2), 0, 0, 0, 0};
+                const v8i aenc = {(int)(ax & 0xAAAAAAAAu), (int)((ax << 1) & 0xAAAAAAAAu), (int)(ay & 0xAAAAAAAAu),
+                                  (int)((ay << 1) & 0xAAAAAAAAu), 0, 0, 0, 0};
 #pragma unroll
                 for (int t = 0; t < WT; ++t) {
-                    const uint2 b = sB[buf][wsub + t][c][lane];
-                    const v8i bden = {(int)(b.x & 0x22222222u), (int)(b.x & 0x11111111u), (int)(b.y & 0x22222222u),
-                                      (int)(b.y & 0x11111111u), 0, 0, 0, 0};
-                    const v8i benc = {(int)(b.x & 0xAAAAAAAAu), (int)((b.x << 1) & 0xAAAAAAAAu),
-                                      (int)(b.y & 0xAAAAAAAAu), (int)((b.y << 1) & 0xAAAAAAAAu), 0, 0, 0, 0};
+                    const uint4 b4 = st[2 * BQ + 2 * (wsub + t) + gp][lane];
+                    const uint32_t bx = h2 ? b4.z : b4.x, by = h2 ? b4.w : b4.y;
+                    const v8i bden = {(int)(bx & 0x22222222u), (int)(bx & 0x11111111u), (int)(by & 0x22222222u),
+                                      (int)(by & 0x11111111u), 0, 0, 0, 0};
+                    const v8i benc = {(int)(bx & 0xAAAAAAAAu), (int)((bx << 1) & 0xAAAAAAAAu),
+                                      (int)(by & 0xAAAAAAAAu), (int)((by << 1) & 0xAAAAAAAAu), 0, 0, 0, 0};
                     den[t] = mfma4(aden, bden, den[t]);
-                    s[t] = mfma4(aenc, benc, s[t]);
+                    sacc[t] = mfma4(aenc, benc, sacc[t]);
                 }
             }
-            if (st + 1 < NSTEPS) lstore(buf ^ 1);
-            __syncthreads();
         }
-        // per template: min over the 16 rows of this lane, then the partner half
+        const uint32_t j = s / NSTEPS;
+        if (s - j * NSTEPS != NSTEPS - 1) continue;
+        // N-group done: per template, min over the 16 rows of this lane, then the partner half
+        const uint64_t ng = gi + (uint64_t)j * G;
         const int h = lane >> 5;
 #pragma unroll
         for (int t = 0; t < WT; ++t) {
@@ -145,7 +187,7 @@ __global__ void __launch_bounds__(512, 1)
             for (int r = 0; r < 16; ++r) {
                 const int k = (r & 3) + 8 * (r >> 2) + 4 * h;
                 const uint32_t dd = (uint32_t)den[t][r];
-                const uint32_t nn = (uint32_t)(((int)dd - (int)s[t][r]) >> 1);
+                const uint32_t nn = (uint32_t)(((int)dd - (int)sacc[t][r]) >> 1);
                 if (k < kRot && dd != 0 && (bd == 0 || nn * bd < bn * dd)) {
                     bn = nn;
                     bd = dd;
@@ -170,12 +212,17 @@ __global__ void __launch_bounds__(512, 1)
             c.idx = tg - first;
             if (b_better(c, best)) best = c;
         }
+        zero();
     }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
         const Partial o = b_shfl(best, off);
         if (b_better(o, best)) best = o;
     }
+    // the ring is idle (every DMA was waited for): reuse it for the cross-wave reduction
+    VMCNT(0);
+    __syncthreads();
+    Partial *sP = (Partial *)&ring[0][0][0];
     if (lane == 0) sP[w] = best;
     __syncthreads();
     if (tid < BQ) {
