@@ -30,7 +30,12 @@ typedef float v16f __attribute__((ext_vector_type(16)));
 
 constexpr int BQ = 4;                     // queries per workgroup
 constexpr int BT = 8;                     // template tiles per N-group
-constexpr int WT = 4;                     // tiles per wave
+#ifndef IRIS_BATCH_WQ
+#define IRIS_BATCH_WQ 2
+#endif
+constexpr int WQ = IRIS_BATCH_WQ;         // queries per wave
+constexpr int WT = 4 / WQ;                // tiles per wave (WQ x WT = 4 accumulator pairs)
+constexpr int kQW = BQ / WQ;              // waves per tile set
 constexpr int KSTEP = 4;                  // chunks per K-step
 constexpr int NSTEPS = kPlaneDwords / 2 / KSTEP;  // 50
 constexpr int kTileU4 = kPlaneGroups * 64;        // 6400 uint4 per tile
@@ -78,7 +83,7 @@ __global__ void __launch_bounds__(512, 1)
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint32_t qg = blockIdx.x % nqg, gi = blockIdx.x / nqg;
-    const int wq = w & 3, wsub = (w >> 2) * WT;
+    const int wq0 = (w % kQW) * WQ, wsub = (w / kQW) * WT;
     const uint64_t ngroups = (ntiles + BT - 1) / BT;
     const uint32_t my_groups = gi < ngroups ? (uint32_t)((ngroups - gi + G - 1) / G) : 0;
     const uint32_t total = my_groups * NSTEPS;
@@ -119,21 +124,26 @@ __global__ void __launch_bounds__(512, 1)
         }
     };
 
-    Partial best;
-    best.num = 0;
-    best.den = 0;
-    best.rot = 0;
-    best.pad = 0;
-    best.idx = ~0ull;
-    v16f den[WT], sacc[WT];
+    Partial best[WQ];
+#pragma unroll
+    for (int qi = 0; qi < WQ; ++qi) {
+        best[qi].num = 0;
+        best[qi].den = 0;
+        best[qi].rot = 0;
+        best[qi].pad = 0;
+        best[qi].idx = ~0ull;
+    }
+    v16f den[WQ][WT], sacc[WQ][WT];
     auto zero = [&] {
 #pragma unroll
-        for (int t = 0; t < WT; ++t)
+        for (int qi = 0; qi < WQ; ++qi)
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                den[t][i] = 0.f;
-                sacc[t][i] = 0.f;
-            }
+            for (int t = 0; t < WT; ++t)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    den[qi][t][i] = 0.f;
+                    sacc[qi][t][i] = 0.f;
+                }
     };
     zero();
     for (uint32_t s = 0; s < 3 && s < total; ++s) issue(s);
@@ -153,24 +163,34 @@ __global__ void __launch_bounds__(512, 1)
         const uint4(*st)[64] = ring[s % kRing];
 #pragma unroll
         for (int gp = 0; gp < 2; ++gp) {
-            const uint4 a4 = st[2 * wq + gp][lane];
+            uint4 a4[WQ], b4[WT];
+#pragma unroll
+            for (int qi = 0; qi < WQ; ++qi) a4[qi] = st[2 * (wq0 + qi) + gp][lane];
+#pragma unroll
+            for (int t = 0; t < WT; ++t) b4[t] = st[2 * BQ + 2 * (wsub + t) + gp][lane];
 #pragma unroll
             for (int h2 = 0; h2 < 2; ++h2) {
-                const uint32_t ax = h2 ? a4.z : a4.x, ay = h2 ? a4.w : a4.y;
-                const v8i aden = {(int)(ax & 0x22222222u), (int)((ax & 0x11111111u) << 2), (int)(ay & 0x22222222u),
-                                  (int)((ay & 0x11111111u) << 2), 0, 0, 0, 0};
-                const v8i aenc = {(int)(ax & 0xAAAAAAAAu), (int)((ax << 1) & 0xAAAAAAAAu), (int)(ay & 0xAAAAAAAAu),
-                                  (int)((ay << 1) & 0xAAAAAAAAu), 0, 0, 0, 0};
+                v8i aden[WQ], aenc[WQ];
+#pragma unroll
+                for (int qi = 0; qi < WQ; ++qi) {
+                    const uint32_t ax = h2 ? a4[qi].z : a4[qi].x, ay = h2 ? a4[qi].w : a4[qi].y;
+                    aden[qi] = v8i{(int)(ax & 0x22222222u), (int)((ax & 0x11111111u) << 2), (int)(ay & 0x22222222u),
+                                   (int)((ay & 0x11111111u) << 2), 0, 0, 0, 0};
+                    aenc[qi] = v8i{(int)(ax & 0xAAAAAAAAu), (int)((ax << 1) & 0xAAAAAAAAu), (int)(ay & 0xAAAAAAAAu),
+                                   (int)((ay << 1) & 0xAAAAAAAAu), 0, 0, 0, 0};
+                }
 #pragma unroll
                 for (int t = 0; t < WT; ++t) {
-                    const uint4 b4 = st[2 * BQ + 2 * (wsub + t) + gp][lane];
-                    const uint32_t bx = h2 ? b4.z : b4.x, by = h2 ? b4.w : b4.y;
+                    const uint32_t bx = h2 ? b4[t].z : b4[t].x, by = h2 ? b4[t].w : b4[t].y;
                     const v8i bden = {(int)(bx & 0x22222222u), (int)(bx & 0x11111111u), (int)(by & 0x22222222u),
                                       (int)(by & 0x11111111u), 0, 0, 0, 0};
                     const v8i benc = {(int)(bx & 0xAAAAAAAAu), (int)((bx << 1) & 0xAAAAAAAAu),
                                       (int)(by & 0xAAAAAAAAu), (int)((by << 1) & 0xAAAAAAAAu), 0, 0, 0, 0};
-                    den[t] = mfma4(aden, bden, den[t]);
-                    sacc[t] = mfma4(aenc, benc, sacc[t]);
+#pragma unroll
+                    for (int qi = 0; qi < WQ; ++qi) {
+                        den[qi][t] = mfma4(aden[qi], bden, den[qi][t]);
+                        sacc[qi][t] = mfma4(aenc[qi], benc, sacc[qi][t]);
+                    }
                 }
             }
         }
@@ -180,54 +200,62 @@ __global__ void __launch_bounds__(512, 1)
         const uint64_t ng = gi + (uint64_t)j * G;
         const int h = lane >> 5;
 #pragma unroll
-        for (int t = 0; t < WT; ++t) {
-            uint32_t bn = 0, bd = 0;
-            int br = 0;
+        for (int qi = 0; qi < WQ; ++qi)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int k = (r & 3) + 8 * (r >> 2) + 4 * h;
-                const uint32_t dd = (uint32_t)den[t][r];
-                const uint32_t nn = (uint32_t)(((int)dd - (int)sacc[t][r]) >> 1);
-                if (k < kRot && dd != 0 && (bd == 0 || nn * bd < bn * dd)) {
-                    bn = nn;
-                    bd = dd;
-                    br = k;
+            for (int t = 0; t < WT; ++t) {
+                uint32_t bn = 0, bd = 0;
+                int br = 0;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int k = (r & 3) + 8 * (r >> 2) + 4 * h;
+                    const uint32_t dd = (uint32_t)den[qi][t][r];
+                    const uint32_t nn = (uint32_t)(((int)dd - (int)sacc[qi][t][r]) >> 1);
+                    if (k < kRot && dd != 0 && (bd == 0 || nn * bd < bn * dd)) {
+                        bn = nn;
+                        bd = dd;
+                        br = k;
+                    }
                 }
+                const uint32_t pn = __shfl_xor(bn, 32), pd = __shfl_xor(bd, 32);
+                const int pr = __shfl_xor(br, 32);
+                if (pd != 0 && (bd == 0 || pn * bd < bn * pd || (pn * bd == bn * pd && pr < br))) {
+                    bn = pn;
+                    bd = pd;
+                    br = pr;
+                }
+                const uint64_t trel2 = ng * BT + wsub + t;
+                const uint64_t tg = (tile0 + trel2) * 32 + (lane & 31);
+                const bool valid = trel2 < ntiles && tg >= first && tg < end;
+                Partial c;
+                c.num = bn;
+                c.den = valid ? bd : 0;
+                c.rot = br;
+                c.pad = 0;
+                c.idx = tg - first;
+                if (b_better(c, best[qi])) best[qi] = c;
             }
-            const uint32_t pn = __shfl_xor(bn, 32), pd = __shfl_xor(bd, 32);
-            const int pr = __shfl_xor(br, 32);
-            if (pd != 0 && (bd == 0 || pn * bd < bn * pd || (pn * bd == bn * pd && pr < br))) {
-                bn = pn;
-                bd = pd;
-                br = pr;
-            }
-            const uint64_t trel2 = ng * BT + wsub + t;
-            const uint64_t tg = (tile0 + trel2) * 32 + (lane & 31);
-            const bool valid = trel2 < ntiles && tg >= first && tg < end;
-            Partial c;
-            c.num = bn;
-            c.den = valid ? bd : 0;
-            c.rot = br;
-            c.pad = 0;
-            c.idx = tg - first;
-            if (b_better(c, best)) best = c;
-        }
         zero();
     }
 #pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        const Partial o = b_shfl(best, off);
-        if (b_better(o, best)) best = o;
-    }
+    for (int qi = 0; qi < WQ; ++qi)
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            const Partial o = b_shfl(best[qi], off);
+            if (b_better(o, best[qi])) best[qi] = o;
+        }
     // the ring is idle (every DMA was waited for): reuse it for the cross-wave reduction
     VMCNT(0);
     __syncthreads();
-    Partial *sP = (Partial *)&ring[0][0][0];
-    if (lane == 0) sP[w] = best;
+    Partial *sP = (Partial *)&ring[0][0][0];  // [wave][WQ]
+    if (lane == 0)
+#pragma unroll
+        for (int qi = 0; qi < WQ; ++qi) sP[w * WQ + qi] = best[qi];
     __syncthreads();
-    if (tid < BQ) {
-        Partial b = sP[tid];
-        if (b_better(sP[tid + 4], b)) b = sP[tid + 4];
+    if (tid < BQ) {  // query tid: waves with wq0 <= tid < wq0 + WQ, one per tile set
+        const int qi = tid % WQ, wl = tid / WQ;
+        Partial b = sP[wl * WQ + qi];
+        for (int ts = 1; ts < 8 / kQW; ++ts)
+            if (b_better(sP[(ts * kQW + wl) * WQ + qi], b)) b = sP[(ts * kQW + wl) * WQ + qi];
         partials[(uint64_t)(qg * BQ + tid) * G + gi] = b;
     }
 }
