@@ -1,0 +1,71 @@
+// Micro-benchmark (diagnostic only): the read-stream ceiling of HBM on this
+// MI355X, to put the search kernel's 6.7-6.8 TB/s in context.  Streams a
+// 32 GB buffer (the 10M-template database size) with 16-B loads; variants:
+// nontemporal vs plain loads, loads in flight per lane, waves per CU.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// each wave streams contiguous 1-KB rows: row r of wave w at (w + r * nwaves) * 1 KB
+template <int DEPTH, bool NT>
+__global__ void __launch_bounds__(256) stream_kernel(const uint4 *__restrict__ src, uint64_t rows, uint32_t *out) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t wave = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint64_t nwaves = (uint64_t)gridDim.x * 4;
+    uint32_t acc = 0;
+    for (uint64_t r = wave; r < rows; r += nwaves * DEPTH) {
+        u32x4 v[DEPTH];
+#pragma unroll
+        for (int d = 0; d < DEPTH; ++d) {
+            const uint64_t rr = r + d * nwaves;
+            const u32x4 *p = (const u32x4 *)(src + (rr < rows ? rr : r) * 64 + lane);
+            v[d] = NT ? __builtin_nontemporal_load(p) : *p;
+        }
+#pragma unroll
+        for (int d = 0; d < DEPTH; ++d) acc ^= v[d].x ^ v[d].y ^ v[d].z ^ v[d].w;
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
+template <int DEPTH, bool NT>
+void run(const uint4 *buf, uint64_t bytes, int blocks_per_cu, uint32_t *out) {
+    const uint64_t rows = bytes / 1024;
+    const int grid = 256 * blocks_per_cu;
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    for (int i = 0; i < 2; ++i) hipLaunchKernelGGL((stream_kernel<DEPTH, NT>), grid, 256, 0, 0, buf, rows, out);
+    const int reps = 10;
+    hipEventRecord(e0);
+    for (int i = 0; i < reps; ++i) hipLaunchKernelGGL((stream_kernel<DEPTH, NT>), grid, 256, 0, 0, buf, rows, out);
+    hipEventRecord(e1);
+    hipEventSynchronize(e1);
+    float ms = 0;
+    hipEventElapsedTime(&ms, e0, e1);
+    ms /= reps;
+    printf("read stream  depth=%2d %-5s waves/CU=%2d  %8.3f ms  %7.0f GB/s\n", DEPTH, NT ? "nt" : "plain",
+           4 * blocks_per_cu, ms, bytes / (ms * 1e-3) / 1e9);
+}
+
+int main() {
+    const uint64_t bytes = 32000000000ull;
+    uint4 *buf;
+    uint32_t *out;
+    if (hipMalloc(&buf, bytes) != hipSuccess || hipMalloc(&out, 64) != hipSuccess) {
+        printf("alloc failed\n");
+        return 1;
+    }
+    hipMemset(buf, 0x5A, bytes);
+    hipDeviceSynchronize();
+    for (int bpc : {2, 4, 8}) {
+        run<2, true>(buf, bytes, bpc, out);
+        run<4, true>(buf, bytes, bpc, out);
+        run<8, true>(buf, bytes, bpc, out);
+        run<4, false>(buf, bytes, bpc, out);
+    }
+    hipFree(buf);
+    hipFree(out);
+    return 0;
+}
