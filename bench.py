@@ -112,16 +112,18 @@ def cpu_baseline(seconds):
     }
 
 
-def load_traffic(n_per_launch, layout):
-    """HBM bytes per launch of the search kernel from the committed PMC run
-    (profiles/*pmc*.json, FETCH_SIZE/WRITE_SIZE corrected per
-    MI355X_MICROARCH.md §HBM), scaled to this launch size; None if absent."""
-    for p in sorted((ROOT / "profiles").glob("*pmc_template_search*.json"), reverse=True):
+def load_traffic(workload, n_per_launch, layout):
+    """HBM bytes per launch of the workload's kernel from the committed PMC run
+    (profiles/*_pmc_<workload>[_lanes].json, FETCH_SIZE/WRITE_SIZE in separate passes,
+    corrected per MI355X_MICROARCH.md §HBM by tools/pmc_summarize.py), scaled to this
+    launch size; (None, None) if absent."""
+    suffix = "" if layout == "tiles" else "_lanes"
+    for p in sorted((ROOT / "profiles").glob(f"*_pmc_{workload}{suffix}.json"), reverse=True):
         try:
             j = json.loads(p.read_text())
             if j.get("layout") != layout:
                 continue
-            return j["hbm_bytes_per_template"] * n_per_launch, p.name
+            return j["hbm_bytes_per_record"] * n_per_launch, p.name
         except Exception:
             continue
     return None, None
@@ -199,7 +201,8 @@ def run_aux(args, dev):
         "data": "synthetic (uniform random u16 / on-device generated templates)",
         "config": {"workload": workload, "records_per_gpu": n, "parties": P},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None},
+                     "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": load_traffic(args.workload, n, "tiles")[0] if args.workload == "resolver" else None},
         "kernel": {"name": kname, "avg_ms": kms / max(1, launches), "launches": launches,
                    "bytes_per_record": rec_bytes},
         "cpu_baseline": None,
@@ -338,7 +341,7 @@ def main():
     _, rms, _ = dev.kernel_stats("reduce")
     avg_ms = kms / max(1, launches)
     achieved = rec_bytes * n / (avg_ms * 1e-3) / 1e9
-    traffic, traffic_src = load_traffic(n, args.layout) if args.workload == "search" else (None, None)
+    traffic, traffic_src = load_traffic(args.workload, n, args.layout) if args.workload != "batch" else (None, None)
     ms_per_step = elapsed / args.steps * 1e3
     value = ROT * total * nq / (elapsed / args.steps)
 

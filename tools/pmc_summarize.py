@@ -1,0 +1,66 @@
+"""Summarise tools/pmc_traffic.sh output into profiles/r01_pmc_<workload>.json:
+average FETCH_SIZE / WRITE_SIZE per launch of the workload's dominant kernel, corrected per
+MI355X_MICROARCH.md §HBM (FETCH_SIZE reports 1/2 of wide coalesced streaming reads:
+read bytes = FETCH_SIZE kB * 1024 * 2; write bytes = WRITE_SIZE kB * 1024)."""
+import csv
+import json
+import pathlib
+import sys
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+PMC = ROOT / "gpurun_out" / "pmc"
+KERNELS = {"search": ("template_mfma_kernel<1>", 10_000_000, 3200),
+           "masks": ("masks_mfma_kernel", 10_000_000, 1600 + 62),
+           "shares": ("shares_mfma_kernel", 10_000_000, 25600 + 62),
+           "resolver": ("resolver_kernel", 10_000_000, 4 * 62)}
+
+
+def counter(dirname, name, kernel):
+    vals = []
+    for f in (PMC / dirname).rglob("*counter_collection.csv"):
+        for row in csv.DictReader(open(f)):
+            if row.get("Counter_Name") == name and kernel in row.get("Kernel_Name", ""):
+                vals.append(float(row["Counter_Value"]))
+    # per-dispatch values may be split per XCD/agent rows: sum by dispatch when present
+    return vals
+
+
+def per_launch(dirname, name, kernel):
+    by = {}
+    for f in (PMC / dirname).rglob("*counter_collection.csv"):
+        for row in csv.DictReader(open(f)):
+            if row.get("Counter_Name") == name and kernel in row.get("Kernel_Name", ""):
+                by.setdefault(row.get("Dispatch_Id", len(by)), 0.0)
+                by[row.get("Dispatch_Id", len(by))] += float(row["Counter_Value"])
+    if not by:
+        return None
+    return sum(by.values()) / len(by)
+
+
+def main(round_tag="r01"):
+    for w, (kernel, n, alg) in KERNELS.items():
+        for suffix, lay in (("", "tiles"), ("_lanes", "lanes")):
+            fdir, wdir = f"{w}_FETCH_SIZE{suffix}", f"{w}_WRITE_SIZE{suffix}"
+            if not (PMC / fdir).exists():
+                continue
+            k = kernel if lay == "tiles" else "template_kernel<1>"
+            fetch = per_launch(fdir, "FETCH_SIZE", k)
+            write = per_launch(wdir, "WRITE_SIZE", k)
+            if fetch is None or write is None:
+                print("missing", w, lay)
+                continue
+            rd, wr = fetch * 1024 * 2, write * 1024
+            j = {"round": int(round_tag[1:]), "workload": w, "layout": lay, "kernel": k,
+                 "command": f"rocprofv3 --pmc FETCH_SIZE|WRITE_SIZE (separate passes) -- python3 bench.py --workload {w} --steps 3 --warmup 1",
+                 "n_records_per_launch": n, "FETCH_SIZE_kB_raw": fetch, "WRITE_SIZE_kB_raw": write,
+                 "correction": "read bytes = FETCH_SIZE*1024*2, write bytes = WRITE_SIZE*1024 (MI355X_MICROARCH.md §HBM)",
+                 "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
+                 "hbm_bytes_per_launch": rd + wr, "hbm_bytes_per_record": (rd + wr) / n,
+                 "algorithmic_bytes_per_record": alg}
+            name = f"{round_tag}_pmc_{w}{suffix}.json"
+            (ROOT / "profiles" / name).write_text(json.dumps(j, indent=1) + "\n")
+            print(name, round((rd + wr) / n, 1), "B/record vs", alg)
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:])
