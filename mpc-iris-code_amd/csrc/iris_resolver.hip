@@ -44,43 +44,67 @@ __device__ __forceinline__ Partial res_shfl(const Partial &c, int off) {
     return o;
 }
 
-// Stage one wave's 64 rows of a [n][31] u16 array into LDS with dword loads
-// when the wave's byte range is 4-aligned (always, for n multiple of 2 rows).
-__device__ __forceinline__ void stage_rows(const uint16_t *__restrict__ src, uint64_t row0, uint64_t rows,
-                                           uint16_t *lds, int lane) {
-    const uint64_t e0 = row0 * kRot, ne = rows * kRot;
-    if ((e0 & 1) == 0) {
-        const uint32_t *s32 = (const uint32_t *)(src + e0);
-        const uint32_t ndw = (uint32_t)(ne / 2);
-        for (uint32_t i = lane; i < ndw; i += 64) ((uint32_t *)lds)[i] = s32[i];
-        if ((ne & 1) && lane == 0) lds[ne - 1] = src[e0 + ne - 1];
-    } else {
-        for (uint32_t i = lane; i < ne; i += 64) lds[i] = src[e0 + i];
-    }
+typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
+
+// One wave's 64 rows of a [n][31] u16 array as 16-B words: 64 rows = 3968 B =
+// 248 words, 16-B aligned when the array is (row0 is a multiple of 64).  Word
+// i of the wave's block -> lane i % 64, slot i / 64 (4 slots).  Words past the
+// end of the array are read element-wise (zero beyond it).
+__device__ __forceinline__ u16x8 load_word(const uint16_t *__restrict__ src, uint64_t e0, uint64_t ne, uint32_t i,
+                                           bool aligned) {
+    const uint64_t e = (uint64_t)i * 8;
+    if (aligned && e + 8 <= ne) return *(const u16x8 *)(src + e0 + e);
+    u16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+        if (e + j < ne) v[j] = src[e0 + e + j];
+    return v;
 }
+
+constexpr int kWords = kWaveRows * kRot * 2 / 16;  // 248
+constexpr int kSlots = (kWords + 63) / 64;         // 4
 
 __global__ void __launch_bounds__(256) resolver_kernel(ResolverArgs a, const uint16_t *__restrict__ denoms,
                                                        uint64_t n, double *__restrict__ dist_out,
                                                        Partial *__restrict__ partials) {
-    __shared__ uint16_t sh_num[kWaveSlots][kWaveRows * kRot + 2];
-    __shared__ uint16_t sh_den[kWaveSlots][kWaveRows * kRot + 2];
+    __shared__ __attribute__((aligned(16))) uint16_t sh_num[kWaveSlots][kWaveRows * kRot + 8];
+    __shared__ __attribute__((aligned(16))) uint16_t sh_den[kWaveSlots][kWaveRows * kRot + 8];
     __shared__ Partial sh_best[kWaveSlots];
     const int lane = threadIdx.x & 63, ws = threadIdx.x >> 6;
     const uint64_t row0 = ((uint64_t)blockIdx.x * kWaveSlots + ws) * kWaveRows;
     const uint64_t rows = row0 < n ? ((n - row0) < kWaveRows ? n - row0 : kWaveRows) : 0;
+    const uint64_t e0 = row0 * kRot, ne = rows * kRot;
+    bool aligned = ((uintptr_t)denoms & 15) == 0;
+    for (uint32_t p = 0; p < a.parts; ++p) aligned &= ((uintptr_t)a.shares[p] & 15) == 0;
     Partial c;
     c.num = 0;
     c.den = 0;
     c.rot = 0;
     c.pad = 0;
     c.idx = row0 + lane;
-    // wrapping sum of the shares, in LDS (src/main.rs:603-607)
-    stage_rows(denoms, row0, rows, sh_den[ws], lane);
-    stage_rows(a.shares[0], row0, rows, sh_num[ws], lane);
-    __syncthreads();
-    for (uint32_t p = 1; p < a.parts; ++p) {
-        const uint64_t e0 = row0 * kRot, ne = rows * kRot;
-        for (uint32_t i = lane; i < ne; i += 64) sh_num[ws][i] = (uint16_t)(sh_num[ws][i] + a.shares[p][e0 + i]);
+    // wrapping sum of the shares (src/main.rs:603-607) in packed u16 lanes, all loads issued up front
+    u16x8 num[kSlots], den[kSlots];
+#pragma unroll
+    for (int sl = 0; sl < kSlots; ++sl) {
+        const uint32_t i = lane + 64 * sl;
+        if (i < kWords) {
+            den[sl] = load_word(denoms, e0, ne, i, aligned);
+            num[sl] = load_word(a.shares[0], e0, ne, i, aligned);
+        }
+    }
+    for (uint32_t p = 1; p < a.parts; ++p)
+#pragma unroll
+        for (int sl = 0; sl < kSlots; ++sl) {
+            const uint32_t i = lane + 64 * sl;
+            if (i < kWords) num[sl] += load_word(a.shares[p], e0, ne, i, aligned);
+        }
+#pragma unroll
+    for (int sl = 0; sl < kSlots; ++sl) {
+        const uint32_t i = lane + 64 * sl;
+        if (i < kWords) {
+            *(u16x8 *)&sh_num[ws][8 * i] = num[sl];
+            *(u16x8 *)&sh_den[ws][8 * i] = den[sl];
+        }
     }
     __syncthreads();
     if ((uint64_t)lane < rows) {

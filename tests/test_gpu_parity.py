@@ -368,6 +368,34 @@ def test_resolver_fused_matches_oracle(device, golden):
     assert z.index == 2**64 - 1 and z.distance == np.inf
 
 
+@pytest.mark.parametrize("offset", [0, 2, 6])
+def test_resolver_device_alignment(device, offset):
+    """Device form with arrays at 16-B aligned and misaligned addresses (the kernel's
+    16-B word path and its element-wise fallback) and a ragged tail (n % 64 != 0)."""
+    rng = np.random.default_rng(offset)
+    n = 1000 + 37
+    parts = [rng.integers(0, 2**16, (n, ROT), dtype=np.uint16) for _ in range(2)]
+    den = rng.integers(0, 12801, (n, ROT), dtype=np.uint16)
+    want = oc.resolver_combine(np.stack(parts), den)
+    best, idx = oc.argmin(want)
+    ptrs = []
+    for a in parts + [den]:
+        p = device.alloc(a.nbytes + 16)
+        device.h2d(p + offset, a)
+        ptrs.append(p)
+    dist = device.alloc(n * 8)
+    try:
+        m = ih.resolver_search_device(device, [p + offset for p in ptrs[:2]], ptrs[2] + offset, n,
+                                      dist_out_device=dist)
+        got = np.empty(n, np.float64)
+        device.d2h(got, dist)
+    finally:
+        for p in ptrs + [dist]:
+            device.free(p)
+    assert m.index == idx and bits_eq(m.distance, best)
+    assert bits_eq(got, want)
+
+
 def test_mpc_end_to_end(device, layout):
     """The reference's MPC flow on synthetic data: the resolver holds the masks,
     3 participants hold additive shares of encode(template); DistanceEngine on
