@@ -55,12 +55,13 @@ def parse():
     ap.add_argument("--layout", choices=["tiles", "lanes"], default="tiles",
                     help="tiles = MFMA kernels (default), lanes = VALU kernels")
     ap.add_argument("--queries", type=int, default=1024, help="queries per batch (workload batch)")
-    ap.add_argument("--workload", choices=["search", "masks", "shares", "batch", "resolver", "prepare"],
+    ap.add_argument("--workload", choices=["search", "masks", "shares", "batch", "resolver", "resolve-masks", "prepare"],
                     default="search",
                     help="search = Template masked Hamming + argmin (configs[1], default); "
                          "masks = MasksEngine denominators; shares = DistanceEngine u16 share dot (configs[3]); "
                          "batch = --queries queries x 31 rotations x N templates in one pass (configs[2]); "
                          "resolver = fused share sum + decode + argmin over --parties [n][31] outputs; "
+                         "resolve-masks = the same with the denominators computed on the fly from a masks DB; "
                          "prepare = GPU share preparation of n templates into --parties share DBs + masks")
     ap.add_argument("--parties", type=int, default=3, help="parties (workloads resolver, prepare)")
     return ap.parse_args()
@@ -151,6 +152,24 @@ def run_aux(args, dev):
         kname, unit = "resolver", "records/s"
         rec_bytes = (P + 1) * ROT * 2  # P share rows + the denominator row, read once
         workload = f"resolver: {P} participants' [u16;31] outputs + denominators -> min/argmin (src/main.rs:597-621)"
+    elif args.workload == "resolve-masks":
+        n = args.n_per_gpu
+        shares = rng.integers(0, 65536, (P, n, ROT), dtype=np.uint16)
+        for j in range(P):
+            ptrs.append(dev.alloc(n * ROT * 2))
+            dev.h2d(ptrs[j], shares[j])
+        mdb = ih.Database(dev, ih.KIND_MASKS, n)
+        mdb.generate(n, SEED)
+        qmask = oc.gen_templates(SEED + 1, 0, 1)[0][200:].copy()
+        eng = ih.MasksEngine(dev, qmask)
+
+        def step():
+            return eng.resolve(mdb, ptrs[:P])
+
+        kname, unit = "masks_resolve", "records/s"
+        rec_bytes = 1600 + P * ROT * 2  # the mask + P share rows; no denominators in memory
+        workload = (f"resolver step with on-the-fly denominators: masks DB + {P} participants' [u16;31] "
+                    "outputs -> min/argmin (src/main.rs:510-519 + 597-621)")
     else:
         n = min(args.n_per_gpu, 1_000_000)  # 3 share DBs of 1M = 77 GB
         tdb = ih.Database(dev, ih.KIND_TEMPLATES, n)
@@ -180,7 +199,13 @@ def run_aux(args, dev):
     dev.set_profiling(False)
     launches, kms, items = dev.kernel_stats(kname)
     achieved = rec_bytes * items / (kms * 1e-3) / 1e9
-    if args.workload == "resolver":
+    if args.workload == "resolve-masks":  # denominators from the (separately tested) masks engine
+        denoms = np.empty((n, ROT), np.uint16)
+        eng.batch_process(denoms, mdb)
+        sample = np.random.default_rng(1).choice(n, 64, replace=False)
+        assert (denoms[sample] == oc.masks_batch(qmask, mdb.read(0, n)[sample] if n <= 100_000 else
+                                                 np.stack([mdb.read(int(i), 1)[0] for i in sample]))).all()
+    if args.workload in ("resolver", "resolve-masks"):
         best, idx = oc.argmin(oc.resolver_combine(shares, denoms))
         ok = m.index == idx and np.float64(m.distance).view(np.uint64) == np.float64(best).view(np.uint64)
         check = {"oracle_index": int(idx), "found_index": int(m.index), "ok": bool(ok)}
@@ -194,6 +219,7 @@ def run_aux(args, dev):
         check = {"sampled_templates_vs_oracle": len(sample), "ok": bool(ok)}
     line = {
         "metric": {"resolver": "resolver records/s (share sum + decode + argmin)",
+                   "resolve-masks": "resolver records/s (masks engine + share sum + decode + argmin, fused)",
                    "prepare": "templates prepared/s (shares + masks)"}[args.workload],
         "value": n * args.steps / elapsed, "unit": unit, "n_gpus": 1, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
@@ -202,7 +228,8 @@ def run_aux(args, dev):
         "config": {"workload": workload, "records_per_gpu": n, "parties": P},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": load_traffic(args.workload, n, "tiles")[0] if args.workload == "resolver" else None},
+                     "traffic": load_traffic(args.workload, n, "tiles")[0]
+                     if args.workload in ("resolver", "resolve-masks") else None},
         "kernel": {"name": kname, "avg_ms": kms / max(1, launches), "launches": launches,
                    "bytes_per_record": rec_bytes},
         "cpu_baseline": None,
@@ -242,7 +269,7 @@ def main():
     lo = rank * n
     total = n * world
     dev = ih.Device(ordinal)
-    if args.workload in ("resolver", "prepare"):
+    if args.workload in ("resolver", "resolve-masks", "prepare"):
         if world > 1:
             raise SystemExit("workloads resolver / prepare are single-GPU lines (run without torchrun)")
         return run_aux(args, dev)

@@ -238,6 +238,16 @@ int iris_template_batch_search(iris_engine_t *engine, const iris_db_t *db, uint6
 int iris_resolver_search(iris_device_t *dev, const uint16_t *const *shares_device, uint32_t parts,
                          const uint16_t *denoms_device, uint64_t n, uint64_t index_base, double *dist_out_device,
                          iris_match_t *out);
+/* The resolver step with the denominators computed on the fly: `engine` is
+ * the MasksEngine of the query mask, records [first, first+n) of the masks
+ * database give the denominators (MasksEngine::batch_process, never written
+ * to memory on the TILES layout), shares_device[p] are DEVICE arrays of n*31
+ * uint16_t with row i belonging to record first+i (src/main.rs:510-519 +
+ * 597-621 in one pass).  Same result as iris_resolver_search over the
+ * engine's output; indices are i + index_base. */
+int iris_resolver_search_masks(iris_engine_t *engine, const iris_db_t *masks_db, uint64_t first, uint64_t n,
+                               const uint16_t *const *shares_device, uint32_t parts, uint64_t index_base,
+                               double *dist_out_device, iris_match_t *out);
 /* Host form: shares[p] and denoms are host arrays (uploaded in chunks). */
 int iris_resolver_search_host(iris_device_t *dev, const uint16_t *const *shares, uint32_t parts,
                               const uint16_t *denoms, uint64_t n, uint64_t index_base, iris_match_t *out);

@@ -745,6 +745,50 @@ int iris_resolver_search(iris_device_t *d, const uint16_t *const *shares, uint32
     return 0;
 }
 
+// The resolver step with the denominators computed on the fly from the masks
+// database (src/main.rs:510-519 + 597-621): TILES runs the fused
+// masks_mfma_kernel<MASKS_RESOLVE>; LANES the masks kernel into a workspace
+// and then the resolver kernel.
+int iris_resolver_search_masks(iris_engine_t *e, const iris_db_t *db, uint64_t first, uint64_t n,
+                               const uint16_t *const *shares_device, uint32_t parts, uint64_t index_base,
+                               double *dist_out_device, iris_match_t *out) {
+    ARG(e && db && out, "NULL argument");
+    ARG(parts >= 1 && parts <= 8, "parts must be 1..8");
+    ARG(e->kind == IRIS_KIND_MASKS && db->k.kind == IRIS_KIND_MASKS, "needs a masks engine and a masks database");
+    ARG(e->dev == db->dev, "engine and database live on different devices");
+    ARG(n == 0 || shares_device, "NULL argument");
+    for (uint32_t p = 0; n && p < parts; ++p) ARG(shares_device[p], "NULL share array");
+    iris_device *d = e->dev;
+    std::lock_guard<std::recursive_mutex> g(d->mu);
+    CHK(set_device(d));
+    CHK(range_ok(db, first, n));
+    LaunchRange r{first, n};
+    Partial res{};
+    if (db->k.layout == IRIS_LAYOUT_TILES) {
+        const uint32_t np = n ? masks_resolve_partials(r) : 0;
+        CHK(ensure(d->partials, (size_t)std::max<uint32_t>(np, 1) * sizeof(Partial)));
+        CHK(ensure(d->result, sizeof(Partial)));
+        CHK(timed(d, "masks_resolve", n, [&] {
+            return launch_masks_resolve(d->stream, db->data, e->qfrag, r, shares_device, parts, dist_out_device,
+                                        (Partial *)d->partials.p);
+        }));
+        CHK(resolver_finish(d, np, &res));
+    } else {
+        CHK(ensure(d->out_a, std::max<uint64_t>(n, 1) * kRot * 2));
+        CHK(timed(d, "masks", n, [&] { return launch_masks(d->stream, db->data, e->qtab, r, (uint16_t *)d->out_a.p); }));
+        const uint32_t np = resolver_partials(n);
+        CHK(ensure(d->partials, (size_t)std::max<uint32_t>(np, 1) * sizeof(Partial)));
+        CHK(ensure(d->result, sizeof(Partial)));
+        CHK(timed(d, "resolver", n, [&] {
+            return launch_resolver(d->stream, shares_device, parts, (const uint16_t *)d->out_a.p, n, dist_out_device,
+                                   (Partial *)d->partials.p);
+        }));
+        CHK(resolver_finish(d, n ? np : 0, &res));
+    }
+    match_from(res, n > 0, index_base, out);
+    return 0;
+}
+
 int iris_resolver_search_host(iris_device_t *d, const uint16_t *const *shares, uint32_t parts, const uint16_t *denoms,
                               uint64_t n, uint64_t index_base, iris_match_t *out) {
     ARG(d && out, "NULL argument");

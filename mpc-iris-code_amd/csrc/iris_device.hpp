@@ -59,4 +59,36 @@ __device__ __forceinline__ void store_tile_rows(uint16_t *__restrict__ out, uint
     }
 }
 
+// Candidate order of the resolver / search argmin: exact fraction (u32 cross-
+// multiplication, num and den < 2^16), then the lowest index; den = 0 is "no
+// candidate" (NaN / +inf in the reference, never selected by a strict <).
+__device__ __forceinline__ bool partial_better_dev(const Partial &a, const Partial &b) {
+    if (a.den == 0) return false;
+    if (b.den == 0) return true;
+    const uint32_t l = a.num * b.den, r = b.num * a.den;
+    if (l != r) return l < r;
+    return a.idx < b.idx;
+}
+
+__device__ __forceinline__ Partial partial_shfl_xor(const Partial &c, int off) {
+    Partial o;
+    o.num = __shfl_xor(c.num, off);
+    o.den = __shfl_xor(c.den, off);
+    o.rot = __shfl_xor(c.rot, off);
+    o.pad = 0;
+    const uint32_t lo = __shfl_xor((uint32_t)c.idx, off), hi = __shfl_xor((uint32_t)(c.idx >> 32), off);
+    o.idx = ((uint64_t)hi << 32) | lo;
+    return o;
+}
+
+__device__ __forceinline__ Partial partial_none() {
+    Partial p;
+    p.num = 0;
+    p.den = 0;
+    p.rot = 0;
+    p.pad = 0;
+    p.idx = ~0ull;
+    return p;
+}
+
 }  // namespace iris

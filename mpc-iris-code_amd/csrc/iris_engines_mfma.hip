@@ -67,14 +67,34 @@ __device__ __forceinline__ void mask_chunk(uint32_t x, const v8i &a, v16f &acc) 
     acc = mfma_fp4(a, b, acc);
 }
 
+// Fused resolver operands (MASKS_RESOLVE): the participants' [n][31] u16
+// outputs, row i = record first + i (src/main.rs:597-607).
+struct MaskResolve {
+    const uint16_t *shares[8];
+    uint32_t parts;
+    bool aligned;  // every share array 16-B aligned
+    double *dist_out;
+    Partial *partials;
+};
+
+enum { MASKS_OUT = 0, MASKS_RESOLVE = 1 };
+
 // Persistent: each wave walks the tile groups wave, wave + nwaves, ... as one
 // flat stream of (group, step) K-steps, so the loads of the next group are in
 // flight while the current group's rows are written out (a wave that exits
 // after its stores leaves its slot idle until they are acknowledged).  The
 // compact query (51 KB) is staged in LDS once per workgroup.
+//
+// MASKS_RESOLVE replaces the [u16;31] output with the resolver step
+// (src/main.rs:510-519 + 597-621): the tile's summed shares are staged in LDS,
+// each lane decodes its 16 (template, rotation) cells against the
+// denominators still in its accumulators (decode_distance, src/lib.rs:97-107),
+// and a running (fraction, lowest index) best per lane becomes one partial per
+// workgroup — the denominators never reach memory.
+template <int MODE>
 __global__ void __launch_bounds__(256, 2)
     masks_mfma_kernel(const uint4 *__restrict__ db, const uint4 *__restrict__ qfrag, uint64_t tile0, uint64_t ntiles,
-                      uint64_t first, uint64_t end, uint16_t *__restrict__ out) {
+                      uint64_t first, uint64_t end, uint16_t *__restrict__ out, MaskResolve rs) {
     constexpr int T = kMasksTiles;
     constexpr uint32_t kSteps = kMaskChunks / 4;  // 50 steps of 4 chunks
     __shared__ uint4 sq[kMaskFragUint4];
@@ -86,9 +106,10 @@ __global__ void __launch_bounds__(256, 2)
     const uint64_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaveSlots + (threadIdx.x >> 6));
     const uint64_t nwaves = (uint64_t)gridDim.x * kWaveSlots;
     const uint64_t ngroups = (ntiles + T - 1) / T;
-    if (wave >= ngroups) return;
-    const uint32_t total = (uint32_t)((ngroups - wave + nwaves - 1) / nwaves) * kSteps;
+    if (MODE == MASKS_OUT && wave >= ngroups) return;
+    const uint32_t total = wave < ngroups ? (uint32_t)((ngroups - wave + nwaves - 1) / nwaves) * kSteps : 0;
     uint16_t *lds = sh_out[threadIdx.x >> 6];
+    Partial best = partial_none();
 
     v16f acc[T];
     auto zero = [&] {
@@ -97,54 +118,134 @@ __global__ void __launch_bounds__(256, 2)
 #pragma unroll
             for (int i = 0; i < 16; ++i) acc[t][i] = 0.f;
     };
-    zero();
-    struct Stage {
-        uint4 d[T];
-        uint4 w;
-    };
-    auto load = [&](Stage &st, uint32_t s) {
-        s = s < total ? s : total - 1;
-        const uint32_t j = s / kSteps, g = s - j * kSteps;
-        const uint64_t tw = (wave + (uint64_t)j * nwaves) * T;
-#pragma unroll
-        for (int t = 0; t < T; ++t) {
-            const uint64_t rel = (tw + t < ntiles) ? tw + t : ntiles - 1;
-            st.d[t] = nt_load(db + (tile0 + rel) * (uint64_t)kMaskTileUint4 + g * 64 + lane);
+    // resolver epilogue of one tile (records t0 .. t0+31 of the database)
+    auto resolve_tile = [&](uint64_t t0, bool tv, const v16f &den) {
+        const bool full = tv && t0 >= first && t0 + 32 <= end && ((t0 - first) & 7) == 0 && rs.aligned;
+        const uint64_t e0 = (t0 - first) * kRot;  // first share element of the tile (when full)
+        if (full) {  // wave-uniform: 124 16-B words per share array
+            typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
+            for (int i = lane; i < 32 * kRot / 8; i += 64) {
+                u16x8 v = *(const u16x8 *)(rs.shares[0] + e0 + 8 * i);
+                for (uint32_t p = 1; p < rs.parts; ++p) v += *(const u16x8 *)(rs.shares[p] + e0 + 8 * i);
+                *(u16x8 *)&lds[8 * i] = v;
+            }
+        } else {
+            for (int i = lane; i < 32 * kRot; i += 64) {
+                const uint64_t tg = t0 + (uint64_t)(i / kRot);
+                uint16_t v = 0;
+                if (tv && tg >= first && tg < end) {
+                    const uint64_t e = (tg - first) * kRot + (uint64_t)(i % kRot);
+                    for (uint32_t p = 0; p < rs.parts; ++p) v = (uint16_t)(v + rs.shares[p][e]);
+                }
+                lds[i] = v;
+            }
         }
-        st.w = sq[g * 64 + lane];
-        __builtin_amdgcn_sched_barrier(0);
-    };
-    auto compute = [&](const Stage &st, uint32_t s) {
-        if (s >= total) return;
-        const v8i a0 = mask_a(st.w.x), a1 = mask_a(st.w.y), a2 = mask_a(st.w.z), a3 = mask_a(st.w.w);
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes landed
+        __builtin_amdgcn_wave_barrier();
+        const int h = lane >> 5;
+        uint32_t bn = 0, bd = 0;
+        int br = 0;
 #pragma unroll
-        for (int t = 0; t < T; ++t) {
-            mask_chunk(st.d[t].x, a0, acc[t]);
-            mask_chunk(st.d[t].y, a1, acc[t]);
-            mask_chunk(st.d[t].z, a2, acc[t]);
-            mask_chunk(st.d[t].w, a3, acc[t]);
+        for (int r = 0; r < 16; ++r) {
+            const int k = (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (k >= kRot) continue;
+            const uint32_t d = (uint32_t)den[r] & 0xFFFFu;  // the MasksEngine output value (u16)
+            const uint32_t u = (uint16_t)(d - lds[(lane & 31) * kRot + k]) >> 1;  // src/lib.rs:104
+            if (d != 0 && (bd == 0 || u * bd < bn * d)) {  // k ascending within a half
+                bn = u;
+                bd = d;
+                br = k;
+            }
         }
-        const uint32_t j = s / kSteps;
-        if (s - j * kSteps == kSteps - 1) {  // group j done: write its rows
+        const uint32_t pn = __shfl_xor(bn, 32), pd = __shfl_xor(bd, 32);
+        const int pr = __shfl_xor(br, 32);
+        if (pd != 0 && (bd == 0 || pn * bd < bn * pd || (pn * bd == bn * pd && pr < br))) {
+            bn = pn;
+            bd = pd;
+            br = pr;
+        }
+        const uint64_t tg = t0 + (lane & 31);
+        const bool valid = tv && tg >= first && tg < end;
+        if (valid && rs.dist_out && h == 0) rs.dist_out[tg - first] = bd ? (double)bn / (double)bd : __builtin_inf();
+        Partial c;
+        c.num = bn;
+        c.den = valid ? bd : 0;
+        c.rot = br;
+        c.pad = 0;
+        c.idx = tg - first;
+        if (partial_better_dev(c, best)) best = c;
+        __builtin_amdgcn_wave_barrier();  // LDS reads done before the next tile overwrites
+    };
+    if (total) {
+        zero();
+        struct Stage {
+            uint4 d[T];
+            uint4 w;
+        };
+        auto load = [&](Stage &st, uint32_t s) {
+            s = s < total ? s : total - 1;
+            const uint32_t j = s / kSteps, g = s - j * kSteps;
             const uint64_t tw = (wave + (uint64_t)j * nwaves) * T;
 #pragma unroll
-            for (int t = 0; t < T; ++t)
-                store_tile_rows(out, lds, (tile0 + tw + t) * kTile, first, end, tw + t < ntiles, lane,
-                                [&](int r) { return (uint16_t)(uint32_t)acc[t][r]; });
-            zero();
-        }
-    };
-    Stage sa, sb, sc;
-    load(sa, 0);
-    load(sb, 1);
+            for (int t = 0; t < T; ++t) {
+                const uint64_t rel = (tw + t < ntiles) ? tw + t : ntiles - 1;
+                st.d[t] = nt_load(db + (tile0 + rel) * (uint64_t)kMaskTileUint4 + g * 64 + lane);
+            }
+            st.w = sq[g * 64 + lane];
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        auto compute = [&](const Stage &st, uint32_t s) {
+            if (s >= total) return;
+            const v8i a0 = mask_a(st.w.x), a1 = mask_a(st.w.y), a2 = mask_a(st.w.z), a3 = mask_a(st.w.w);
+#pragma unroll
+            for (int t = 0; t < T; ++t) {
+                mask_chunk(st.d[t].x, a0, acc[t]);
+                mask_chunk(st.d[t].y, a1, acc[t]);
+                mask_chunk(st.d[t].z, a2, acc[t]);
+                mask_chunk(st.d[t].w, a3, acc[t]);
+            }
+            const uint32_t j = s / kSteps;
+            if (s - j * kSteps == kSteps - 1) {  // group j done: write its rows / resolve it
+                const uint64_t tw = (wave + (uint64_t)j * nwaves) * T;
+#pragma unroll
+                for (int t = 0; t < T; ++t) {
+                    if constexpr (MODE == MASKS_OUT)
+                        store_tile_rows(out, lds, (tile0 + tw + t) * kTile, first, end, tw + t < ntiles, lane,
+                                        [&](int r) { return (uint16_t)(uint32_t)acc[t][r]; });
+                    else
+                        resolve_tile((tile0 + tw + t) * kTile, tw + t < ntiles, acc[t]);
+                }
+                zero();
+            }
+        };
+        Stage sa, sb, sc;
+        load(sa, 0);
+        load(sb, 1);
 #pragma unroll 1
-    for (uint32_t s = 0; s < total; s += 3) {
-        load(sc, s + 2);
-        compute(sa, s);
-        load(sa, s + 3);
-        compute(sb, s + 1);
-        load(sb, s + 4);
-        compute(sc, s + 2);
+        for (uint32_t s = 0; s < total; s += 3) {
+            load(sc, s + 2);
+            compute(sa, s);
+            load(sa, s + 3);
+            compute(sb, s + 1);
+            load(sb, s + 4);
+            compute(sc, s + 2);
+        }
+    }
+    if constexpr (MODE == MASKS_RESOLVE) {
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            const Partial o = partial_shfl_xor(best, off);
+            if (partial_better_dev(o, best)) best = o;
+        }
+        __shared__ Partial sh_best[kWaveSlots];
+        if (lane == 0) sh_best[threadIdx.x >> 6] = best;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            Partial b = sh_best[0];
+            for (int w = 1; w < kWaveSlots; ++w)
+                if (partial_better_dev(sh_best[w], b)) b = sh_best[w];
+            rs.partials[blockIdx.x] = b;
+        }
     }
 }
 
@@ -152,8 +253,35 @@ int launch_masks_mfma(void *stream, const void *db, const void *qfrag, LaunchRan
     if (r.n == 0) return 0;
     const Tiles t = tiles_of(r, kMasksTiles);
     const uint64_t grid = std::min<uint64_t>(t.grid, resident_blocks(2));
-    hipLaunchKernelGGL(masks_mfma_kernel, dim3((uint32_t)grid), dim3(256), 0, (hipStream_t)stream,
-                       (const uint4 *)db, (const uint4 *)qfrag, t.tile0, t.ntiles, r.first, r.first + r.n, out);
+    hipLaunchKernelGGL(masks_mfma_kernel<MASKS_OUT>, dim3((uint32_t)grid), dim3(256), 0, (hipStream_t)stream,
+                       (const uint4 *)db, (const uint4 *)qfrag, t.tile0, t.ntiles, r.first, r.first + r.n, out,
+                       MaskResolve{});
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+uint32_t masks_resolve_partials(LaunchRange r) {
+    const Tiles t = tiles_of(r, kMasksTiles);
+    return (uint32_t)std::min<uint64_t>(t.grid, resident_blocks(2));
+}
+
+int launch_masks_resolve(void *stream, const void *db, const void *qfrag, LaunchRange r,
+                         const uint16_t *const *shares, uint32_t parts, double *dist_out, Partial *partials) {
+    if (r.n == 0) return 0;
+    if (parts == 0 || parts > 8) return -1;
+    const Tiles t = tiles_of(r, kMasksTiles);
+    const uint64_t grid = masks_resolve_partials(r);
+    MaskResolve rs{};
+    rs.aligned = true;
+    for (uint32_t p = 0; p < parts; ++p) {
+        rs.shares[p] = shares[p];
+        rs.aligned &= ((uintptr_t)shares[p] & 15) == 0;
+    }
+    rs.parts = parts;
+    rs.dist_out = dist_out;
+    rs.partials = partials;
+    hipLaunchKernelGGL(masks_mfma_kernel<MASKS_RESOLVE>, dim3((uint32_t)grid), dim3(256), 0, (hipStream_t)stream,
+                       (const uint4 *)db, (const uint4 *)qfrag, t.tile0, t.ntiles, r.first, r.first + r.n,
+                       (uint16_t *)nullptr, rs);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

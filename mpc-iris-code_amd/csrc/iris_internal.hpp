@@ -191,6 +191,9 @@ int launch_unpack_tiles_kind(void *stream, int kind, const void *db, void *stagi
 int launch_generate_tiles_kind(void *stream, int kind, void *db, uint64_t t_first, uint64_t n, uint64_t seed,
                                uint64_t global_index0);
 int launch_masks_mfma(void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *out);
+uint32_t masks_resolve_partials(LaunchRange r);
+int launch_masks_resolve(void *stream, const void *db, const void *qfrag, LaunchRange r,
+                         const uint16_t *const *shares, uint32_t parts, double *dist_out, Partial *partials);
 uint32_t resolver_partials(uint64_t n);
 struct BatchGeometry {
     uint64_t tile0, ntiles;

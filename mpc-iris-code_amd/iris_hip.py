@@ -102,6 +102,8 @@ def load_library(path=None):
             "iris_db_save_file": ([P, ctypes.c_char_p, u64, u64], ctypes.c_int),
             "iris_templates_read_json": ([ctypes.c_char_p, P, u64, ctypes.POINTER(u64)], ctypes.c_int),
             "iris_templates_write_json": ([ctypes.c_char_p, P, u64], ctypes.c_int),
+            "iris_resolver_search_masks": ([P, P, u64, u64, P, ctypes.c_uint32, u64, P, ctypes.POINTER(Match)],
+                                           ctypes.c_int),
             "iris_prepare_shares": ([P, u64, u64, u64, P, u64, ctypes.c_uint32, P, P], ctypes.c_int),
             "iris_masks_engine_new": ([P, P, PP], ctypes.c_int),
             "iris_distance_engine_new": ([P, P, PP], ctypes.c_int),
@@ -150,7 +152,7 @@ def exported_symbols():
         "iris_resolver_search_host", "iris_dot_bool_batch", "iris_dot_u16_batch", "iris_bits_rotated", "iris_encoded_rotated", "iris_encode",
         "iris_decode_distance", "iris_match_merge", "iris_db_load_file", "iris_db_save_file",
         "iris_templates_read_json", "iris_templates_write_json", "iris_prepare_shares",
-        "iris_db_truncate", "iris_memcpy_h2d",
+        "iris_db_truncate", "iris_memcpy_h2d", "iris_resolver_search_masks",
     ]
 
 
@@ -631,6 +633,37 @@ class MasksEngine(_Engine):
         h = ctypes.c_void_p()
         _check(load_library().iris_masks_engine_new(device.handle, _ptr(_c(q, np.uint64)), ctypes.byref(h)))
         self.handle = h
+
+    def resolve(self, db, shares, first=0, n=None, index_base=0, dist_out_device=None):
+        """The resolver step with this engine's denominators computed on the fly
+        (src/main.rs:510-519 + 597-621): shares = the participants' [n,31] u16 outputs,
+        host arrays (uploaded here) or device pointers.  -> Match."""
+        if n is None:
+            n = len(db) - int(first)
+        dev = self.device
+        tmp = []
+        try:
+            ptrs = []
+            for a in shares:
+                if isinstance(a, int):
+                    ptrs.append(a)
+                    continue
+                a = _c(a, np.uint16)
+                if a.shape != (n, ROTATIONS):
+                    raise IrisError(-1, "shares must be [n, 31] uint16")
+                p = dev.alloc(max(a.nbytes, 16))
+                tmp.append(p)
+                dev.h2d(p, a)
+                ptrs.append(p)
+            arr = (ctypes.c_void_p * len(ptrs))(*ptrs)
+            m = Match()
+            _check(load_library().iris_resolver_search_masks(self.handle, db.handle, int(first), int(n), arr,
+                                                             len(ptrs), int(index_base),
+                                                             ctypes.c_void_p(dist_out_device or 0), ctypes.byref(m)))
+            return m
+        finally:
+            for p in tmp:
+                dev.free(p)
 
 
 class DistanceEngine(_Engine):

@@ -458,3 +458,37 @@ def test_batch_search_matches_single(device):
             assert sub[q].index == (7 + 1000 + si if si != 2**64 - 1 else si) and bits_eq(sub[q].distance, sd), q
     assert got[3].index == 4321 and got[3].distance == 0.0
     assert got[5].index == 2**64 - 1
+
+
+# ---------------------------------------------------------------- fused masks + resolver
+
+
+@pytest.mark.parametrize("first,n", [(0, 3000), (37, 1000), (64, 64), (5, 1)])
+def test_resolver_masks_fused(device, layout, first, n):
+    """MasksEngine.resolve == MasksEngine.batch_process + resolver_search == oracle, on
+    random participant outputs (ties, den = 0 rows) and a planted near-copy."""
+    total = 3100
+    masks = oc.gen_templates(61, 0, total)[:, 200:].copy()
+    q = masks[first + n // 2].copy()
+    rng = np.random.default_rng(first + n)
+    parts = [rng.integers(0, 2**16, (n, ROT), dtype=np.uint16) for _ in range(3)]
+    with ih.Database(device, ih.KIND_MASKS, total, layout) as db, ih.MasksEngine(device, q) as eng:
+        db.append(masks)
+        den = np.empty((n, ROT), np.uint16)
+        eng.batch_process(den, db, first=first, n=n)
+        assert (den == oc.masks_batch(q, masks[first:first + n])).all()
+        # make the planted record's shares decode to a small distance
+        parts[2][n // 2] = (den[n // 2] - 20 - parts[0][n // 2] - parts[1][n // 2]).astype(np.uint16)
+        want = oc.resolver_combine(np.stack(parts), den)
+        best, idx = oc.argmin(want)
+        dist = device.alloc(n * 8)
+        try:
+            m = eng.resolve(db, parts, first=first, n=n, index_base=1000, dist_out_device=dist)
+            got = np.empty(n, np.float64)
+            device.d2h(got, dist)
+        finally:
+            device.free(dist)
+    assert m.index == 1000 + idx and bits_eq(m.distance, best)
+    assert bits_eq(got, want)
+    ref = ih.resolver_search(parts, den, index_base=1000, device=device)
+    assert ref.index == m.index and ref.rotation == m.rotation
