@@ -21,7 +21,7 @@
 // one partial per (query, workgroup), reduced by reduce_kernel per query.
 #include <hip/hip_runtime.h>
 
-#include "iris_internal.hpp"
+#include "iris_device.hpp"
 
 namespace iris {
 
@@ -42,25 +42,6 @@ constexpr int kTileU4 = kPlaneGroups * 64;        // 6400 uint4 per tile
 
 __device__ __forceinline__ v16f mfma4(const v8i &a, const v8i &b, const v16f &c) {
     return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, c, 4, 4, 0, 127, 0, 127);
-}
-
-__device__ __forceinline__ bool b_better(const Partial &a, const Partial &b) {
-    if (a.den == 0) return false;
-    if (b.den == 0) return true;
-    const uint32_t l = a.num * b.den, r = b.num * a.den;
-    if (l != r) return l < r;
-    return a.idx < b.idx;
-}
-
-__device__ __forceinline__ Partial b_shfl(const Partial &c, int off) {
-    Partial o;
-    o.num = __shfl_xor(c.num, off);
-    o.den = __shfl_xor(c.den, off);
-    o.rot = __shfl_xor(c.rot, off);
-    o.pad = 0;
-    const uint32_t lo = __shfl_xor((uint32_t)c.idx, off), hi = __shfl_xor((uint32_t)(c.idx >> 32), off);
-    o.idx = ((uint64_t)hi << 32) | lo;
-    return o;
 }
 
 // s_waitcnt with only the vector-memory count bounded (expcnt, lgkmcnt at max)
@@ -232,7 +213,7 @@ __global__ void __launch_bounds__(512, 1)
                 c.rot = br;
                 c.pad = 0;
                 c.idx = tg - first;
-                if (b_better(c, best[qi])) best[qi] = c;
+                if (partial_better_dev(c, best[qi])) best[qi] = c;
             }
         zero();
     }
@@ -240,8 +221,8 @@ __global__ void __launch_bounds__(512, 1)
     for (int qi = 0; qi < WQ; ++qi)
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) {
-            const Partial o = b_shfl(best[qi], off);
-            if (b_better(o, best[qi])) best[qi] = o;
+            const Partial o = partial_shfl_xor(best[qi], off);
+            if (partial_better_dev(o, best[qi])) best[qi] = o;
         }
     // the ring is idle (every DMA was waited for): reuse it for the cross-wave reduction
     VMCNT(0);
@@ -255,7 +236,7 @@ __global__ void __launch_bounds__(512, 1)
         const int qi = tid % WQ, wl = tid / WQ;
         Partial b = sP[wl * WQ + qi];
         for (int ts = 1; ts < 8 / kQW; ++ts)
-            if (b_better(sP[(ts * kQW + wl) * WQ + qi], b)) b = sP[(ts * kQW + wl) * WQ + qi];
+            if (partial_better_dev(sP[(ts * kQW + wl) * WQ + qi], b)) b = sP[(ts * kQW + wl) * WQ + qi];
         partials[(uint64_t)(qg * BQ + tid) * G + gi] = b;
     }
 }
@@ -272,12 +253,12 @@ __global__ void __launch_bounds__(256) batch_reduce_kernel(const Partial *__rest
     c.idx = ~0ull;
     for (uint32_t i = threadIdx.x; i < G; i += blockDim.x) {
         const Partial p = partials[(uint64_t)q * G + i];
-        if (b_better(p, c)) c = p;
+        if (partial_better_dev(p, c)) c = p;
     }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
-        const Partial o = b_shfl(c, off);
-        if (b_better(o, c)) c = o;
+        const Partial o = partial_shfl_xor(c, off);
+        if (partial_better_dev(o, c)) c = o;
     }
     __shared__ Partial sh[4];
     if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = c;
@@ -285,7 +266,7 @@ __global__ void __launch_bounds__(256) batch_reduce_kernel(const Partial *__rest
     if (threadIdx.x == 0) {
         Partial b = sh[0];
         for (int i = 1; i < 4; ++i)
-            if (b_better(sh[i], b)) b = sh[i];
+            if (partial_better_dev(sh[i], b)) b = sh[i];
         out[q] = b;
     }
 }

@@ -76,25 +76,6 @@ __device__ __forceinline__ bool better_rot(uint32_t an, uint32_t ad, int ar, uin
     return ar < br;
 }
 
-__device__ __forceinline__ bool better_idx(const Partial &a, const Partial &b) {
-    if (a.den == 0) return false;
-    if (b.den == 0) return true;
-    const uint32_t l = a.num * b.den, r = b.num * a.den;
-    if (l != r) return l < r;
-    return a.idx < b.idx;
-}
-
-__device__ __forceinline__ Partial shfl_partial(const Partial &c, int off) {
-    Partial o;
-    o.num = __shfl_xor(c.num, off);
-    o.den = __shfl_xor(c.den, off);
-    o.rot = __shfl_xor(c.rot, off);
-    o.pad = 0;
-    const uint32_t lo = __shfl_xor((uint32_t)c.idx, off), hi = __shfl_xor((uint32_t)(c.idx >> 32), off);
-    o.idx = ((uint64_t)hi << 32) | lo;
-    return o;
-}
-
 enum { MF_COUNTS = 0, MF_SEARCH = 1 };
 
 template <int MODE>
@@ -225,14 +206,14 @@ __global__ void __launch_bounds__(256, 2)
             c.rot = br;
             c.pad = 0;
             c.idx = o;
-            if (better_idx(c, best)) best = c;
+            if (partial_better_dev(c, best)) best = c;
         }
     }
     if (MODE == MF_SEARCH) {
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) {
-            const Partial ot = shfl_partial(best, off);
-            if (better_idx(ot, best)) best = ot;
+            const Partial ot = partial_shfl_xor(best, off);
+            if (partial_better_dev(ot, best)) best = ot;
         }
         __shared__ Partial sh[kWaveSlots];
         if (lane == 0) sh[wslot] = best;
@@ -241,7 +222,7 @@ __global__ void __launch_bounds__(256, 2)
             Partial b = sh[0];
 #pragma unroll
             for (int w = 1; w < kWaveSlots; ++w)
-                if (better_idx(sh[w], b)) b = sh[w];
+                if (partial_better_dev(sh[w], b)) b = sh[w];
             partials[blockIdx.x] = b;
         }
     }

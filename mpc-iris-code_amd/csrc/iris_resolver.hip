@@ -13,7 +13,7 @@
 // candidate".  The winner's f64 is computed once with IEEE division.
 #include <hip/hip_runtime.h>
 
-#include "iris_internal.hpp"
+#include "iris_device.hpp"
 
 namespace iris {
 
@@ -24,25 +24,6 @@ struct ResolverArgs {
     const uint16_t *shares[kMaxParts];
     uint32_t parts;
 };
-
-__device__ __forceinline__ bool res_better(const Partial &a, const Partial &b) {
-    if (a.den == 0) return false;
-    if (b.den == 0) return true;
-    const uint32_t l = a.num * b.den, r = b.num * a.den;  // <= 32767 * 65535 < 2^32
-    if (l != r) return l < r;
-    return a.idx < b.idx;
-}
-
-__device__ __forceinline__ Partial res_shfl(const Partial &c, int off) {
-    Partial o;
-    o.num = __shfl_xor(c.num, off);
-    o.den = __shfl_xor(c.den, off);
-    o.rot = __shfl_xor(c.rot, off);
-    o.pad = 0;
-    const uint32_t lo = __shfl_xor((uint32_t)c.idx, off), hi = __shfl_xor((uint32_t)(c.idx >> 32), off);
-    o.idx = ((uint64_t)hi << 32) | lo;
-    return o;
-}
 
 typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
 
@@ -123,15 +104,15 @@ __global__ void __launch_bounds__(256) resolver_kernel(ResolverArgs a, const uin
     }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
-        const Partial o = res_shfl(c, off);
-        if (res_better(o, c)) c = o;
+        const Partial o = partial_shfl_xor(c, off);
+        if (partial_better_dev(o, c)) c = o;
     }
     if (lane == 0) sh_best[ws] = c;
     __syncthreads();
     if (threadIdx.x == 0) {
         Partial b = sh_best[0];
         for (int w = 1; w < kWaveSlots; ++w)
-            if (res_better(sh_best[w], b)) b = sh_best[w];
+            if (partial_better_dev(sh_best[w], b)) b = sh_best[w];
         partials[blockIdx.x] = b;
     }
 }
