@@ -492,3 +492,30 @@ def test_resolver_masks_fused(device, layout, first, n):
     assert bits_eq(got, want)
     ref = ih.resolver_search(parts, den, index_base=1000, device=device)
     assert ref.index == m.index and ref.rotation == m.rotation
+
+
+def test_empty_ranges(device, layout):
+    """Every entry point accepts an empty range (the reference's loops over empty slices)."""
+    masks = oc.gen_templates(71, 0, 40)
+    with ih.Database(device, ih.KIND_MASKS, 40, layout) as mdb, ih.MasksEngine(device, masks[0, 200:]) as me, \
+            ih.Database(device, ih.KIND_SHARES, 8, layout) as sdb, \
+            ih.DistanceEngine(device, np.zeros(12800, np.uint16)) as de, \
+            ih.Database(device, ih.KIND_TEMPLATES, 40, layout) as tdb:
+        out = np.empty((0, ROT), np.uint16)
+        me.batch_process(out, mdb)                      # empty database
+        de.batch_process(out, sdb)
+        mdb.append(masks[:, 200:])
+        tdb.append(masks)
+        me.batch_process(out, mdb, first=40, n=0)       # empty range at the end
+        m = me.resolve(mdb, [np.empty((0, ROT), np.uint16)], first=3, n=0)
+        assert m.index == 2**64 - 1 and m.distance == np.inf
+        r = ih.resolver_search([np.empty((0, ROT), np.uint16)], np.empty((0, ROT), np.uint16), device=device)
+        assert r.index == 2**64 - 1
+        sh = ih.Database(device, ih.KIND_SHARES, 8, layout)
+        ih.prepare_shares(tdb, [sh], first=40, n=0)
+        assert len(sh) == 0
+        sh.close()
+        if layout == ih.LAYOUT_TILES:  # the batched engine runs on TILES databases
+            with ih.TemplateBatchEngine(device, masks[:3]) as be:
+                ms = be.search(tdb, first=0, n=0)
+                assert all(x.index == 2**64 - 1 for x in ms)
