@@ -59,6 +59,21 @@ __device__ __forceinline__ void store_tile_rows(uint16_t *__restrict__ out, uint
     }
 }
 
+// Shares TILES planes: 16 u16 elements (8 dwords) -> the low-byte and
+// high-byte planes, each byte XOR 0x80 (the byte - 128 as i8), 16 B each.
+__device__ __forceinline__ void split_bytes(const uint32_t *src8, uint4 &lo, uint4 &hi) {
+    uint32_t l[4], hh[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t a = src8[2 * q], b = src8[2 * q + 1];  // elements 4q..4q+3
+        // v_perm_b32: bytes 0-3 of the selector space are a's, 4-7 are b's
+        l[q] = __builtin_amdgcn_perm(b, a, 0x06040200u) ^ 0x80808080u;   // a0 a2 b0 b2
+        hh[q] = __builtin_amdgcn_perm(b, a, 0x07050301u) ^ 0x80808080u;  // a1 a3 b1 b3
+    }
+    lo = make_uint4(l[0], l[1], l[2], l[3]);
+    hi = make_uint4(hh[0], hh[1], hh[2], hh[3]);
+}
+
 // Candidate order of the resolver / search argmin: exact fraction (u32 cross-
 // multiplication, num and den < 2^16), then the lowest index; den = 0 is "no
 // candidate" (NaN / +inf in the reference, never selected by a strict <).

@@ -436,19 +436,6 @@ __global__ void __launch_bounds__(256) generate_masks_tiles(uint4 *__restrict__ 
 }
 
 // shares: thread per (record, chunk c, half h): elements 32c + 16h .. +15 -> lo / hi byte planes ^ 0x80
-__device__ __forceinline__ void split_bytes(const uint32_t *src8, uint4 &lo, uint4 &hi) {
-    uint32_t l[4], hh[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const uint32_t a = src8[2 * q], b = src8[2 * q + 1];  // elements 4q..4q+3
-        l[q] = ((a & 0xFFu) | ((a >> 8) & 0xFF00u) | ((b & 0xFFu) << 16) | ((b << 8) & 0xFF000000u)) ^ 0x80808080u;
-        hh[q] = (((a >> 8) & 0xFFu) | ((a >> 16) & 0xFF00u) | (((b >> 8) & 0xFFu) << 16) | (b & 0xFF000000u)) ^
-                0x80808080u;
-    }
-    lo = make_uint4(l[0], l[1], l[2], l[3]);
-    hi = make_uint4(hh[0], hh[1], hh[2], hh[3]);
-}
-
 __device__ __forceinline__ void join_bytes(const uint4 &lo_, const uint4 &hi_, uint32_t *dst8) {
     const uint32_t lo[4] = {lo_.x ^ 0x80808080u, lo_.y ^ 0x80808080u, lo_.z ^ 0x80808080u, lo_.w ^ 0x80808080u};
     const uint32_t hi[4] = {hi_.x ^ 0x80808080u, hi_.y ^ 0x80808080u, hi_.z ^ 0x80808080u, hi_.w ^ 0x80808080u};

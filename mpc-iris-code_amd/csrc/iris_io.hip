@@ -377,29 +377,45 @@ extern "C" int iris_prepare_shares(const iris_db_t *templates, uint64_t first, u
     if (first > templates->len || n > templates->len - first)
         return fail(IRIS_E_RANGE, "record range outside the database");
     if (n == 0) return 0;
-    // staging: templates (3200 B) | masks (1600 B) | parties shares (25600 B each) per record
+    // staging per record: template (3200 B) | mask (1600 B) | the shares (25600 B each) unless
+    // every share database is TILES, which the keystream kernel writes in place
+    bool direct = true;
+    for (uint32_t j = 0; j < parties; ++j) direct &= shares[j]->k.layout == IRIS_LAYOUT_TILES;
     const size_t tb = kind_info(IRIS_KIND_TEMPLATES, IRIS_LAYOUT_TILES).rec_bytes;
     const size_t mb = kind_info(IRIS_KIND_MASKS, IRIS_LAYOUT_TILES).rec_bytes;
     const size_t sb = kind_info(IRIS_KIND_SHARES, IRIS_LAYOUT_TILES).rec_bytes;
-    const size_t per = tb + mb + (size_t)parties * sb;
+    const size_t per = tb + mb + (direct ? 0 : (size_t)parties * sb);
     const uint64_t ch = std::max<uint64_t>(64, (kStagingBytes / per) / 64 * 64);
     const uint64_t m0 = std::min<uint64_t>(ch, n);
     CHK(ensure(d->staging, m0 * per));
     char *st_t = (char *)d->staging.p, *st_m = st_t + m0 * tb, *st_s = st_m + m0 * mb;
-    std::vector<uint64_t> base(parties);
-    for (uint32_t j = 0; j < parties; ++j) base[j] = shares[j]->len;
+    std::vector<uint64_t> base(parties), tf(parties);
+    std::vector<void *> dbp(parties);
+    for (uint32_t j = 0; j < parties; ++j) {
+        base[j] = shares[j]->len;
+        dbp[j] = shares[j]->data;
+    }
     const uint64_t mbase = masks ? masks->len : 0;
     for (uint64_t off = 0; off < n; off += ch) {
         const uint64_t m = std::min<uint64_t>(ch, n - off);
         CHK(timed(d, "unpack", m,
                   [&] { return launch_unpack(d->stream, templates->k, templates->data, st_t, first + off, m); }));
-        CHK(timed(d, "prepare", m, [&] {
-            return launch_prepare_shares(d->stream, st_t, m, index_base + first + off, key, nonce, parties, st_s);
-        }));
-        for (uint32_t j = 0; j < parties; ++j)
-            CHK(timed(d, "pack", m, [&] {
-                return launch_pack(d->stream, shares[j]->k, st_s + (size_t)j * m * sb, shares[j]->data, base[j] + off, m);
+        if (direct) {
+            for (uint32_t j = 0; j < parties; ++j) tf[j] = base[j] + off;
+            CHK(timed(d, "prepare", m, [&] {
+                return launch_prepare_shares_tiles(d->stream, st_t, m, index_base + first + off, key, nonce, parties,
+                                                   dbp.data(), tf.data());
             }));
+        } else {
+            CHK(timed(d, "prepare", m, [&] {
+                return launch_prepare_shares(d->stream, st_t, m, index_base + first + off, key, nonce, parties, st_s);
+            }));
+            for (uint32_t j = 0; j < parties; ++j)
+                CHK(timed(d, "pack", m, [&] {
+                    return launch_pack(d->stream, shares[j]->k, st_s + (size_t)j * m * sb, shares[j]->data,
+                                       base[j] + off, m);
+                }));
+        }
         if (masks) {
             HIPCHK(hipMemcpy2DAsync(st_m, mb, st_t + mb, tb, mb, m, hipMemcpyDeviceToDevice, d->stream));
             CHK(timed(d, "pack", m, [&] { return launch_pack(d->stream, masks->k, st_m, masks->data, mbase + off, m); }));

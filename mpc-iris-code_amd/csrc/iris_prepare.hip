@@ -20,7 +20,7 @@
 // 0..parties-2, and the last share's row as encode minus their sum.
 #include <hip/hip_runtime.h>
 
-#include "iris_internal.hpp"
+#include "iris_device.hpp"
 
 namespace iris {
 
@@ -66,6 +66,13 @@ __device__ __forceinline__ void chacha20_block(const ChachaKey &key, uint64_t no
 
 constexpr int kBlocks = IRIS_BITS / 32;  // 400 keystream blocks per share
 
+// two independent u16 lanes: (a - b) mod 2^16 per half (v_pk_sub_u16)
+__device__ __forceinline__ uint32_t pk_sub_u16(uint32_t a, uint32_t b) {
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    const u16x2 r = __builtin_bit_cast(u16x2, a) - __builtin_bit_cast(u16x2, b);
+    return __builtin_bit_cast(uint32_t, r);
+}
+
 // templates: m reference-layout records (pattern dwords 0..399, mask 400..799)
 // shares: [parties][m][12800] u16
 __global__ void __launch_bounds__(256) prepare_shares_kernel(const uint32_t *__restrict__ templates, uint64_t m,
@@ -95,17 +102,80 @@ __global__ void __launch_bounds__(256) prepare_shares_kernel(const uint32_t *__r
 #pragma unroll
             for (int q = 0; q < 4; ++q) dst[q] = make_uint4(r[4 * q], r[4 * q + 1], r[4 * q + 2], r[4 * q + 3]);
 #pragma unroll
-            for (int w = 0; w < 16; ++w) {
-                const uint32_t lo = (last[w] - r[w]) & 0xFFFFu;
-                const uint32_t hi = ((last[w] >> 16) - (r[w] >> 16)) & 0xFFFFu;
-                last[w] = lo | (hi << 16);
-            }
+            for (int w = 0; w < 16; ++w) last[w] = pk_sub_u16(last[w], r[w]);
         }
         uint4 *dst = (uint4 *)(shares + ((uint64_t)(parties - 1) * m + i) * IRIS_BITS + 32 * b);
 #pragma unroll
         for (int q = 0; q < 4; ++q)
             dst[q] = make_uint4(last[4 * q], last[4 * q + 1], last[4 * q + 2], last[4 * q + 3]);
     }
+}
+
+// Direct form for TILES share databases: a workgroup takes 64 consecutive
+// templates (lane = template) and its 4 waves split the 400 blocks, so each
+// (share, block) store of a wave is two 512-B runs of the TILES byte planes
+// (split_bytes) and the template dwords come through L1 (a 64 x 128-B window).
+// No staging copy of the shares: they are written once, in place.
+struct ShareDsts {
+    uint4 *db[kMaxPrepParties];
+    uint64_t t_first[kMaxPrepParties];  // database index of template 0 of the launch
+};
+
+__device__ __forceinline__ void store_share_block(uint4 *db, uint64_t t, int b, const uint32_t w[16]) {
+    uint4 *base = db + (t / 32) * (uint64_t)kShareTileUint4 + (t % 32);
+    uint4 lo, hi;
+    split_bytes(w, lo, hi);  // elements 32b .. 32b+15: half 0
+    base[(2 * b) * 64] = lo;
+    base[(2 * b + 1) * 64] = hi;
+    split_bytes(w + 8, lo, hi);  // elements 32b+16 .. 32b+31: half 1
+    base[(2 * b) * 64 + 32] = lo;
+    base[(2 * b + 1) * 64 + 32] = hi;
+}
+
+__global__ void __launch_bounds__(256) prepare_shares_tiles_kernel(const uint32_t *__restrict__ templates, uint64_t m,
+                                                                   uint64_t g0, ChachaKey key, uint64_t nonce,
+                                                                   uint32_t parties, ShareDsts dst) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint64_t i = (uint64_t)blockIdx.x * 64 + lane;
+    if (i >= m) return;
+    const uint32_t *rec = templates + i * (2 * kPlaneDwords);
+    const uint64_t g = g0 + i;
+    for (int b = w; b < kBlocks; b += 4) {
+        const uint32_t pw = rec[b], mw = rec[kPlaneDwords + b];
+        uint32_t last[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const uint32_t m0 = (mw >> (2 * q)) & 1u, m1 = (mw >> (2 * q + 1)) & 1u;
+            const uint32_t p0 = (pw >> (2 * q)) & 1u, p1 = (pw >> (2 * q + 1)) & 1u;
+            last[q] = ((m0 - 2u * (p0 & m0)) & 0xFFFFu) | (((m1 - 2u * (p1 & m1)) & 0xFFFFu) << 16);
+        }
+        for (uint32_t j = 0; j + 1 < parties; ++j) {
+            uint32_t r[16];
+            chacha20_block(key, nonce, (g * (parties - 1) + j) * kBlocks + (uint64_t)b, r);
+            store_share_block(dst.db[j], dst.t_first[j] + i, b, r);
+#pragma unroll
+            for (int q = 0; q < 16; ++q) last[q] = pk_sub_u16(last[q], r[q]);
+        }
+        store_share_block(dst.db[parties - 1], dst.t_first[parties - 1] + i, b, last);
+    }
+}
+
+int launch_prepare_shares_tiles(void *stream, const void *templates, uint64_t m, uint64_t g0, const uint8_t key[32],
+                                uint64_t nonce, uint32_t parties, void *const *dbs, const uint64_t *t_first) {
+    if (m == 0) return 0;
+    if (parties == 0 || parties > (uint32_t)kMaxPrepParties) return -1;
+    ChachaKey k;
+    for (int i = 0; i < 8; ++i)
+        k.k[i] = (uint32_t)key[4 * i] | ((uint32_t)key[4 * i + 1] << 8) | ((uint32_t)key[4 * i + 2] << 16) |
+                 ((uint32_t)key[4 * i + 3] << 24);
+    ShareDsts d{};
+    for (uint32_t j = 0; j < parties; ++j) {
+        d.db[j] = (uint4 *)dbs[j];
+        d.t_first[j] = t_first[j];
+    }
+    hipLaunchKernelGGL(prepare_shares_tiles_kernel, dim3((uint32_t)((m + 63) / 64)), dim3(256), 0, (hipStream_t)stream,
+                       (const uint32_t *)templates, m, g0, k, nonce, parties, d);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int launch_prepare_shares(void *stream, const void *templates, uint64_t m, uint64_t g0, const uint8_t key[32],

@@ -33,15 +33,16 @@ def test_prepare_matches_oracle(device, layout, parties):
 
 
 def test_prepare_multi_chunk_sampled(device):
-    """4000 templates x 3 parties spans two staging chunks; sampled records are checked
-    against the oracle at their own global index, all of them via the share-sum identity."""
-    n = 4000
+    """60 000 templates x 3 parties span two staging chunks (55 872 templates each with
+    in-place TILES shares); sampled records are checked against the oracle at their own
+    global index, all of them via the share-sum identity."""
+    n = 60_000
     with ih.Database(device, ih.KIND_TEMPLATES, n) as tdb:
         tdb.generate(n, 99)
         sdbs = [ih.Database(device, ih.KIND_SHARES, n) for _ in range(3)]
         key = ih.prepare_shares(tdb, sdbs)  # random key from os.urandom
         assert len(key) == 32
-        for i in (0, 1, 3263, 3264, 3265, n - 1):
+        for i in (0, 1, 55871, 55872, 55873, n - 1):
             rec = tdb.read(i, 1)
             want, _ = oc.prepare_shares(rec, key, parties=3, index_base=i)
             for j in range(3):
