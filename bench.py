@@ -55,14 +55,16 @@ def parse():
     ap.add_argument("--layout", choices=["tiles", "lanes"], default="tiles",
                     help="tiles = MFMA kernels (default), lanes = VALU kernels")
     ap.add_argument("--queries", type=int, default=1024, help="queries per batch (workload batch)")
-    ap.add_argument("--workload", choices=["search", "masks", "shares", "batch", "resolver", "resolve-masks", "prepare"],
+    ap.add_argument("--workload", choices=["search", "masks", "shares", "batch", "resolver", "resolve-masks", "prepare",
+                                           "load"],
                     default="search",
                     help="search = Template masked Hamming + argmin (configs[1], default); "
                          "masks = MasksEngine denominators; shares = DistanceEngine u16 share dot (configs[3]); "
                          "batch = --queries queries x 31 rotations x N templates in one pass (configs[2]); "
                          "resolver = fused share sum + decode + argmin over --parties [n][31] outputs; "
                          "resolve-masks = the same with the denominators computed on the fly from a masks DB; "
-                         "prepare = GPU share preparation of n templates into --parties share DBs + masks")
+                         "prepare = GPU share preparation of n templates into --parties share DBs + masks; "
+                         "load = raw template file (page-cached) -> resident TILES database")
     ap.add_argument("--parties", type=int, default=3, help="parties (workloads resolver, prepare)")
     return ap.parse_args()
 
@@ -170,6 +172,21 @@ def run_aux(args, dev):
         rec_bytes = 1600 + P * ROT * 2  # the mask + P share rows; no denominators in memory
         workload = (f"resolver step with on-the-fly denominators: masks DB + {P} participants' [u16;31] "
                     "outputs -> min/argmin (src/main.rs:510-519 + 597-621)")
+    elif args.workload == "load":
+        n = min(args.n_per_gpu, 1_000_000)  # a 3.2 GB file
+        fpath = pathlib.Path(tempfile.gettempdir()) / f"iris_bench_{os.getpid()}.templates"
+        src = ih.Database(dev, ih.KIND_TEMPLATES, n)
+        src.generate(n, SEED)
+        src.save_file(fpath)  # also leaves the file in the page cache
+        tdb = ih.Database(dev, ih.KIND_TEMPLATES, n)
+
+        def step():
+            tdb.truncate(0)
+            return tdb.load_file(fpath)
+
+        kname, unit = "pack", "templates/s"
+        rec_bytes = 2 * 3200  # the transpose kernel: reference layout in, TILES out
+        workload = "raw template file (page cache) -> pinned double-buffered H2D -> TILES transpose (src/main.rs:386-400)"
     else:
         n = min(args.n_per_gpu, 1_000_000)  # 3 share DBs of 1M = 77 GB
         tdb = ih.Database(dev, ih.KIND_TEMPLATES, n)
@@ -209,6 +226,11 @@ def run_aux(args, dev):
         best, idx = oc.argmin(oc.resolver_combine(shares, denoms))
         ok = m.index == idx and np.float64(m.distance).view(np.uint64) == np.float64(best).view(np.uint64)
         check = {"oracle_index": int(idx), "found_index": int(m.index), "ok": bool(ok)}
+    elif args.workload == "load":
+        sample = [0, n // 3, n - 1]
+        ok = m == n and all((tdb.read(i, 1) == src.read(i, 1)).all() for i in sample)
+        fpath.unlink()
+        check = {"sampled_templates_vs_source": len(sample), "ok": bool(ok)}
     else:
         sample = [0, n // 3, n - 1]
         ok = True
@@ -220,7 +242,8 @@ def run_aux(args, dev):
     line = {
         "metric": {"resolver": "resolver records/s (share sum + decode + argmin)",
                    "resolve-masks": "resolver records/s (masks engine + share sum + decode + argmin, fused)",
-                   "prepare": "templates prepared/s (shares + masks)"}[args.workload],
+                   "prepare": "templates prepared/s (shares + masks)",
+                   "load": "templates loaded/s (file -> resident database, PCIe-inclusive)"}[args.workload],
         "value": n * args.steps / elapsed, "unit": unit, "n_gpus": 1, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u16",
@@ -232,6 +255,7 @@ def run_aux(args, dev):
                      if args.workload in ("resolver", "resolve-masks") else None},
         "kernel": {"name": kname, "avg_ms": kms / max(1, launches), "launches": launches,
                    "bytes_per_record": rec_bytes},
+        "file_GBps": (n * 3200 * args.steps / elapsed / 1e9) if args.workload == "load" else None,
         "cpu_baseline": None,
         "check": check,
     }
@@ -269,7 +293,7 @@ def main():
     lo = rank * n
     total = n * world
     dev = ih.Device(ordinal)
-    if args.workload in ("resolver", "resolve-masks", "prepare"):
+    if args.workload in ("resolver", "resolve-masks", "prepare", "load"):
         if world > 1:
             raise SystemExit("workloads resolver / prepare are single-GPU lines (run without torchrun)")
         return run_aux(args, dev)

@@ -34,7 +34,7 @@ using namespace iris_api;
 namespace {
 
 constexpr size_t kIoChunkBytes = 64ull << 20;  // per pinned buffer
-constexpr int kReadThreads = 4;
+constexpr int kReadThreads = 8;
 
 struct Fd {
     int fd = -1;
