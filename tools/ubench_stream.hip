@@ -29,21 +29,63 @@ __global__ void __launch_bounds__(256) stream_kernel(const uint4 *__restrict__ s
     if (acc == 0x12345678u) out[0] = acc;
 }
 
+// each wave streams its own contiguous slice of rows
+template <int DEPTH>
+__global__ void __launch_bounds__(256) stream_slice_kernel(const uint4 *__restrict__ src, uint64_t rows, uint32_t *out) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t wave = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint64_t nwaves = (uint64_t)gridDim.x * 4;
+    const uint64_t per = (rows + nwaves - 1) / nwaves;
+    const uint64_t r0 = wave * per, r1 = r0 + per < rows ? r0 + per : rows;
+    uint32_t acc = 0;
+    for (uint64_t r = r0; r < r1; r += DEPTH) {
+        u32x4 v[DEPTH];
+#pragma unroll
+        for (int d = 0; d < DEPTH; ++d) {
+            const uint64_t rr = r + d < r1 ? r + d : r;
+            v[d] = __builtin_nontemporal_load((const u32x4 *)(src + rr * 64 + lane));
+        }
+#pragma unroll
+        for (int d = 0; d < DEPTH; ++d) acc ^= v[d].x ^ v[d].y ^ v[d].z ^ v[d].w;
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
+template <int DEPTH>
+void run_slice(const uint4 *buf, uint64_t bytes, int blocks_per_cu, uint32_t *out) {
+    const uint64_t rows = bytes / 1024;
+    const int grid = 256 * blocks_per_cu;
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    for (int i = 0; i < 2; ++i) hipLaunchKernelGGL((stream_slice_kernel<DEPTH>), grid, 256, 0, 0, buf, rows, out);
+    const int reps = 10;
+    (void)hipEventRecord(e0);
+    for (int i = 0; i < reps; ++i) hipLaunchKernelGGL((stream_slice_kernel<DEPTH>), grid, 256, 0, 0, buf, rows, out);
+    (void)hipEventRecord(e1);
+    (void)hipEventSynchronize(e1);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    ms /= reps;
+    printf("slice stream depth=%2d nt    waves/CU=%2d  %8.3f ms  %7.0f GB/s\n", DEPTH, 4 * blocks_per_cu, ms,
+           bytes / (ms * 1e-3) / 1e9);
+}
+
 template <int DEPTH, bool NT>
 void run(const uint4 *buf, uint64_t bytes, int blocks_per_cu, uint32_t *out) {
     const uint64_t rows = bytes / 1024;
     const int grid = 256 * blocks_per_cu;
     hipEvent_t e0, e1;
-    hipEventCreate(&e0);
-    hipEventCreate(&e1);
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
     for (int i = 0; i < 2; ++i) hipLaunchKernelGGL((stream_kernel<DEPTH, NT>), grid, 256, 0, 0, buf, rows, out);
     const int reps = 10;
-    hipEventRecord(e0);
+    (void)hipEventRecord(e0);
     for (int i = 0; i < reps; ++i) hipLaunchKernelGGL((stream_kernel<DEPTH, NT>), grid, 256, 0, 0, buf, rows, out);
-    hipEventRecord(e1);
-    hipEventSynchronize(e1);
+    (void)hipEventRecord(e1);
+    (void)hipEventSynchronize(e1);
     float ms = 0;
-    hipEventElapsedTime(&ms, e0, e1);
+    (void)hipEventElapsedTime(&ms, e0, e1);
     ms /= reps;
     printf("read stream  depth=%2d %-5s waves/CU=%2d  %8.3f ms  %7.0f GB/s\n", DEPTH, NT ? "nt" : "plain",
            4 * blocks_per_cu, ms, bytes / (ms * 1e-3) / 1e9);
@@ -57,15 +99,18 @@ int main() {
         printf("alloc failed\n");
         return 1;
     }
-    hipMemset(buf, 0x5A, bytes);
-    hipDeviceSynchronize();
-    for (int bpc : {2, 4, 8}) {
+    (void)hipMemset(buf, 0x5A, bytes);
+    (void)hipDeviceSynchronize();
+    for (int bpc : {2, 3, 4, 8}) {
         run<2, true>(buf, bytes, bpc, out);
         run<4, true>(buf, bytes, bpc, out);
+        run<6, true>(buf, bytes, bpc, out);
         run<8, true>(buf, bytes, bpc, out);
         run<4, false>(buf, bytes, bpc, out);
+        run_slice<4>(buf, bytes, bpc, out);
+        run_slice<8>(buf, bytes, bpc, out);
     }
-    hipFree(buf);
-    hipFree(out);
+    (void)hipFree(buf);
+    (void)hipFree(out);
     return 0;
 }
