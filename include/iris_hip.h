@@ -59,9 +59,9 @@ extern "C" {
 #define IRIS_KIND_TEMPLATES 3 /* records are Template (plaintext masked Hamming, src/template.rs) */
 
 /* Device layouts of a database (iris_db_create_ex) */
-#define IRIS_LAYOUT_DEFAULT 0 /* TILES for templates, LANES otherwise          */
+#define IRIS_LAYOUT_DEFAULT 0 /* TILES                                          */
 #define IRIS_LAYOUT_LANES 1   /* record-per-lane blocks of 64 (VALU kernels)   */
-#define IRIS_LAYOUT_TILES 2   /* 32-record fp4-MFMA tiles (templates only)     */
+#define IRIS_LAYOUT_TILES 2   /* 32-record MFMA tiles (fp4 / i8 kernels)        */
 
 typedef struct iris_template {
     uint64_t pattern[IRIS_LIMBS];
