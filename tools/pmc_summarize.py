@@ -12,7 +12,8 @@ PMC = ROOT / "gpurun_out" / "pmc"
 KERNELS = {"search": ("template_mfma_kernel<1>", 10_000_000, 3200),
            "masks": ("masks_mfma_kernel", 10_000_000, 1600 + 62),
            "shares": ("shares_mfma_kernel", 10_000_000, 25600 + 62),
-           "resolver": ("resolver_kernel", 10_000_000, 4 * 62)}
+           "resolver": ("resolver_kernel", 10_000_000, 4 * 62),
+           "resolve-masks": ("masks_mfma_kernel<1>", 10_000_000, 1600 + 3 * 62)}
 
 
 def counter(dirname, name, kernel):

@@ -16,4 +16,6 @@ run masks 300 --workload masks --steps 20 --warmup 3
 run shares 300 --workload shares --steps 5 --warmup 1
 run batch 300 --workload batch --queries 1024 --steps 1 --warmup 1
 run resolver 300 --workload resolver --steps 20 --warmup 3
+run resolve-masks 300 --workload resolve-masks --steps 20 --warmup 3
 run prepare 300 --workload prepare --steps 2 --warmup 1
+run load 300 --workload load --steps 2 --warmup 1
