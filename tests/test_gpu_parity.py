@@ -519,3 +519,45 @@ def test_empty_ranges(device, layout):
             with ih.TemplateBatchEngine(device, masks[:3]) as be:
                 ms = be.search(tdb, first=0, n=0)
                 assert all(x.index == 2**64 - 1 for x in ms)
+
+
+def test_concurrent_callers(device):
+    """Engines are Sync in the reference (shared across rayon workers, called from
+    spawn_blocking threads, src/main.rs:425,510,597): concurrent calls on one device
+    from several host threads give the sequential results."""
+    import threading
+
+    n = 2000
+    t = oc.gen_templates(81, 0, n)
+    queries = [t[i].copy() for i in (3, 700, 1500, 1999)]
+    with ih.Database(device, ih.KIND_TEMPLATES, n) as tdb, ih.Database(device, ih.KIND_MASKS, n) as mdb:
+        tdb.append(t)
+        mdb.append(t[:, 200:])
+        want = []
+        for q in queries:
+            with ih.TemplateEngine(device, q) as te, ih.MasksEngine(device, q[200:]) as me:
+                out = np.empty((n, ROT), np.uint16)
+                me.batch_process(out, mdb)
+                want.append((te.search(tdb), out))
+        got = [None] * len(queries)
+        errors = []
+
+        def work(i):
+            try:
+                for _ in range(5):
+                    with ih.TemplateEngine(device, queries[i]) as te, ih.MasksEngine(device, queries[i][200:]) as me:
+                        out = np.empty((n, ROT), np.uint16)
+                        me.batch_process(out, mdb)
+                        got[i] = (te.search(tdb), out)
+            except Exception as ex:  # reported below
+                errors.append(ex)
+
+        threads = [threading.Thread(target=work, args=(i,)) for i in range(len(queries))]
+        for th in threads:
+            th.start()
+        for th in threads:
+            th.join()
+    assert not errors
+    for (wm, wo), (gm, go) in zip(want, got):
+        assert gm.index == wm.index and bits_eq(gm.distance, wm.distance)
+        assert (go == wo).all()
