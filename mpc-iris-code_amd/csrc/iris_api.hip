@@ -97,6 +97,7 @@ int run_u16_engine(iris_engine *e, const iris_db *db, uint64_t first, uint64_t n
 
 void engine_free(iris_engine *e) {
     if (!e) return;
+    for (iris_engine *c : e->sub) engine_free(c);
     if (e->qtab) (void)hipFree(e->qtab);
     if (e->qfrag) (void)hipFree(e->qfrag);
     delete e;
@@ -639,6 +640,24 @@ int iris_template_batch_engine_new(iris_device_t *d, const iris_template_t *quer
     ARG(nq > 0, "a batch needs at least one query");
     std::lock_guard<std::recursive_mutex> g(d->mu);
     CHK(set_device(d));
+    if (nq <= kBatchSingles) {
+        iris_engine *e = new (std::nothrow) iris_engine();
+        if (!e) return fail(IRIS_E_NOMEM, "out of host memory");
+        e->dev = d;
+        e->kind = IRIS_KIND_TEMPLATES;
+        e->nq = nq;
+        for (uint32_t i = 0; i < nq; ++i) {
+            iris_engine_t *c = nullptr;
+            const int rc = iris_template_engine_new(d, queries + i, &c);
+            if (rc != 0) {
+                engine_free(e);
+                return rc;
+            }
+            e->sub.push_back(c);
+        }
+        *out = e;
+        return 0;
+    }
     const uint32_t nqp = (nq + 3) / 4 * 4;  // padded to the kernel's query groups (zero tiles: no candidate)
     const size_t tile_dw = (size_t)4 * kPlaneGroups * 64;
     std::vector<uint32_t> tiles((size_t)nqp * tile_dw, 0u);
@@ -662,6 +681,10 @@ int iris_template_batch_search(iris_engine_t *e, const iris_db_t *db, uint64_t f
     std::lock_guard<std::recursive_mutex> g(d->mu);
     CHK(set_device(d));
     CHK(range_ok(db, first, n));
+    if (!e->sub.empty()) {
+        for (uint32_t q = 0; q < e->nq; ++q) CHK(search_locked(e->sub[q], db, first, n, index_base, nullptr, out + q));
+        return 0;
+    }
     LaunchRange r{first, n};
     const BatchGeometry geo = batch_geometry(r, e->nq);
     const uint32_t nqp = geo.nqg * 4;

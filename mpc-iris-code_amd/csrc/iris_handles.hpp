@@ -81,7 +81,13 @@ struct iris_engine {
     void *qtab = nullptr;     // SGPR rotated-query table (LANES kernels)
     void *qfrag = nullptr;    // fp4 query fragments (TILES kernel, templates only)
     uint32_t nq = 0;          // > 0: batched template engine (qfrag = nq padded query tiles)
+    std::vector<iris_engine *> sub;  // batched engine of <= kBatchSingles queries: one single-query engine each
 };
+
+// Up to this many queries a batch runs as single-query streaming searches: the
+// batched GEMM pads to groups of 4 queries, and below 3 queries the single-query
+// kernels (HBM-bound, ~4.8 ms per query per 10M) finish first.
+constexpr uint32_t kBatchSingles = 2;
 
 namespace iris_api {
 

@@ -433,16 +433,21 @@ def test_mpc_end_to_end(device, layout):
 # ---------------------------------------------------------------- batched queries (configs[2])
 
 
-def test_batch_search_matches_single(device):
-    """9 queries (a padded query group) against 5000 templates (a partial
-    N-group): every query's best equals the single-query search and the oracle."""
-    n, nq = 5000, 9
+@pytest.mark.parametrize("nq", [1, 2, 3, 9])
+def test_batch_search_matches_single(device, nq):
+    """nq queries (1-2: the single-query dispatch; 3, 9: padded query groups of the
+    batched kernel) against 5000 templates (a partial N-group): every query's best
+    equals the single-query search and the oracle."""
+    n = 5000
     db_ref = oc.gen_templates(61, 0, n)
-    queries = oc.gen_templates(62, 0, nq)
+    queries = oc.gen_templates(62, 0, max(nq, 9))
     queries[3] = db_ref[4321]          # exact member -> distance 0
     queries[7, :200] = db_ref[17, :200] ^ np.uint64(0x5)
     queries[7, 200:] = db_ref[17, 200:]
     queries[5, 200:] = 0               # empty query mask -> no candidate
+    queries[0] = queries[3] if nq < 3 else queries[0]
+    queries[1] = queries[5] if nq < 3 else queries[1]
+    queries = queries[:nq].copy()
     with ih.Database(device, ih.KIND_TEMPLATES, n) as db:
         db.append(db_ref)
         with ih.TemplateBatchEngine(device, queries) as be:
@@ -456,8 +461,13 @@ def test_batch_search_matches_single(device):
             assert (one.index, one.num, one.den, one.rotation) == (got[q].index, got[q].num, got[q].den, got[q].rotation)
             sd, si = oc.argmin(oc.template_distances(queries[q], db_ref[1000:4333]))
             assert sub[q].index == (7 + 1000 + si if si != 2**64 - 1 else si) and bits_eq(sub[q].distance, sd), q
-    assert got[3].index == 4321 and got[3].distance == 0.0
-    assert got[5].index == 2**64 - 1
+    if nq > 5:
+        assert got[3].index == 4321 and got[3].distance == 0.0
+        assert got[5].index == 2**64 - 1
+    if nq < 3:
+        assert got[0].index == 4321 and got[0].distance == 0.0
+    if nq == 2:
+        assert got[1].index == 2**64 - 1
 
 
 # ---------------------------------------------------------------- fused masks + resolver
