@@ -154,31 +154,24 @@ __global__ void __launch_bounds__(256, 2)
     // C layout: lane l holds template (l & 31) of the tile and rotation rows
     // k = (r & 3) + 8 (r >> 2) + 4 (l >> 5), r = 0..15.
     const int h = lane >> 5;
-    Partial best;
-    best.num = 0;
-    best.den = 0;
-    best.rot = 0;
-    best.pad = 0;
-    best.idx = ~0ull;
+    Partial best = partial_none();
 #pragma unroll
     for (int t = 0; t < T; ++t) {
-        const uint64_t tg = (tile0 + tw + t) * kTileRecs + (lane & 31);  // global template index
-        const bool valid = active && (tw + t < ntiles) && tg >= first && tg < end;
-        const uint64_t o = tg - first;
+        const uint64_t t0 = (tile0 + tw + t) * kTileRecs;  // global index of the tile's first template
+        const bool tv = active && (tw + t < ntiles);
         if constexpr (MODE == MF_COUNTS) {
             __shared__ __attribute__((aligned(16))) uint16_t sh_out[kWaveSlots][1024];
             uint16_t *lds = sh_out[wslot];
-            const uint64_t t0 = (tile0 + tw + t) * kTileRecs;
-            const bool tv = active && (tw + t < ntiles);
             if (num_out)
                 store_tile_rows(num_out, lds, t0, first, end, tv, lane,
                                 [&](int r) { return (uint16_t)(((int)den[t][r] - (int)s[t][r]) >> 1); });
             if (den_out)
                 store_tile_rows(den_out, lds, t0, first, end, tv, lane,
                                 [&](int r) { return (uint16_t)(uint32_t)den[t][r]; });
-            (void)valid;
-            (void)o;
         } else {
+            const uint64_t tg = t0 + (lane & 31);
+            const bool valid = tv && tg >= first && tg < end;
+            const uint64_t o = tg - first;
             uint32_t bn = 0, bd = 0;
             int br = 0;
 #pragma unroll
@@ -209,7 +202,7 @@ __global__ void __launch_bounds__(256, 2)
             if (partial_better_dev(c, best)) best = c;
         }
     }
-    if (MODE == MF_SEARCH) {
+    if constexpr (MODE == MF_SEARCH) {
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) {
             const Partial ot = partial_shfl_xor(best, off);
