@@ -56,7 +56,7 @@ def parse():
                     help="tiles = MFMA kernels (default), lanes = VALU kernels")
     ap.add_argument("--queries", type=int, default=1024, help="queries per batch (workload batch)")
     ap.add_argument("--workload", choices=["search", "masks", "shares", "batch", "resolver", "resolve-masks", "prepare",
-                                           "load"],
+                                           "load", "host-shares", "host-masks"],
                     default="search",
                     help="search = Template masked Hamming + argmin (configs[1], default); "
                          "masks = MasksEngine denominators; shares = DistanceEngine u16 share dot (configs[3]); "
@@ -64,7 +64,8 @@ def parse():
                          "resolver = fused share sum + decode + argmin over --parties [n][31] outputs; "
                          "resolve-masks = the same with the denominators computed on the fly from a masks DB; "
                          "prepare = GPU share preparation of n templates into --parties share DBs + masks; "
-                         "load = raw template file (page-cached) -> resident TILES database")
+                         "load = raw template file (page-cached) -> resident TILES database; "
+                         "host-shares / host-masks = batch_process over host slices (the reference signature)")
     ap.add_argument("--parties", type=int, default=3, help="parties (workloads resolver, prepare)")
     return ap.parse_args()
 
@@ -187,6 +188,25 @@ def run_aux(args, dev):
         kname, unit = "pack", "templates/s"
         rec_bytes = 2 * 3200  # the transpose kernel: reference layout in, TILES out
         workload = "raw template file (page cache) -> pinned double-buffered H2D -> TILES transpose (src/main.rs:386-400)"
+    elif args.workload in ("host-shares", "host-masks"):
+        shares_wl = args.workload == "host-shares"
+        n = min(args.n_per_gpu, 200_000 if shares_wl else 2_000_000)  # 5.1 GB / 3.2 GB of host records
+        qt = oc.gen_templates(SEED + 1, 0, 1)[0]
+        if shares_wl:
+            host = rng.integers(0, 65536, (n, 12800), dtype=np.uint16)
+            eng = ih.DistanceEngine(dev, ih.encode(ih.Template.from_array(qt)))
+        else:
+            host = oc.gen_templates(SEED, 0, n)[:, 200:].copy()
+            eng = ih.MasksEngine(dev, qt[200:])
+        hout = np.empty((n, ROT), np.uint16)
+
+        def step():
+            eng.batch_process(hout, host)
+
+        kname, unit = ("shares" if shares_wl else "masks"), "records/s"
+        rec_bytes = host.shape[1] * host.itemsize
+        workload = (f"{'DistanceEngine' if shares_wl else 'MasksEngine'}::batch_process(out, db: &[T]) over a host "
+                    "slice (src/lib.rs:42-52, 69-79): pinned 2-slot pipeline, PCIe-inclusive")
     else:
         n = min(args.n_per_gpu, 1_000_000)  # 3 share DBs of 1M = 77 GB
         tdb = ih.Database(dev, ih.KIND_TEMPLATES, n)
@@ -226,6 +246,12 @@ def run_aux(args, dev):
         best, idx = oc.argmin(oc.resolver_combine(shares, denoms))
         ok = m.index == idx and np.float64(m.distance).view(np.uint64) == np.float64(best).view(np.uint64)
         check = {"oracle_index": int(idx), "found_index": int(m.index), "ok": bool(ok)}
+    elif args.workload in ("host-shares", "host-masks"):
+        sample = np.random.default_rng(2).choice(n, 16, replace=False)
+        want = (oc.distance_batch(ih.encode(ih.Template.from_array(qt)).values, host[sample])
+                if args.workload == "host-shares" else oc.masks_batch(qt[200:], host[sample]))
+        ok = bool((hout[sample] == want).all())
+        check = {"sampled_outputs_vs_oracle": len(sample), "ok": ok}
     elif args.workload == "load":
         sample = [0, n // 3, n - 1]
         ok = m == n and all((tdb.read(i, 1) == src.read(i, 1)).all() for i in sample)
@@ -243,7 +269,9 @@ def run_aux(args, dev):
         "metric": {"resolver": "resolver records/s (share sum + decode + argmin)",
                    "resolve-masks": "resolver records/s (masks engine + share sum + decode + argmin, fused)",
                    "prepare": "templates prepared/s (shares + masks)",
-                   "load": "templates loaded/s (file -> resident database, PCIe-inclusive)"}[args.workload],
+                   "load": "templates loaded/s (file -> resident database, PCIe-inclusive)",
+                   "host-shares": "share records/s through batch_process over host slices (PCIe-inclusive)",
+                   "host-masks": "mask records/s through batch_process over host slices (PCIe-inclusive)"}[args.workload],
         "value": n * args.steps / elapsed, "unit": unit, "n_gpus": 1, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u16",
@@ -256,6 +284,8 @@ def run_aux(args, dev):
         "kernel": {"name": kname, "avg_ms": kms / max(1, launches), "launches": launches,
                    "bytes_per_record": rec_bytes},
         "file_GBps": (n * 3200 * args.steps / elapsed / 1e9) if args.workload == "load" else None,
+        "host_input_GBps": (n * rec_bytes * args.steps / elapsed / 1e9)
+        if args.workload in ("host-shares", "host-masks") else None,
         "cpu_baseline": None,
         "check": check,
     }
@@ -293,7 +323,7 @@ def main():
     lo = rank * n
     total = n * world
     dev = ih.Device(ordinal)
-    if args.workload in ("resolver", "resolve-masks", "prepare", "load"):
+    if args.workload in ("resolver", "resolve-masks", "prepare", "load", "host-shares", "host-masks"):
         if world > 1:
             raise SystemExit("workloads resolver / prepare are single-GPU lines (run without torchrun)")
         return run_aux(args, dev)
