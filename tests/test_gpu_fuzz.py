@@ -1,0 +1,71 @@
+"""Randomised ranges against the oracle: 24 draws of (records, first, n, layout) per
+entry point exercise every tile / block boundary case of the kernels' epilogues
+(ragged first and last tiles, offsets that are not multiples of 8 — the element-wise
+store path — and one-record ranges).  Fixed seed, so failures reproduce."""
+import numpy as np
+import pytest
+
+import iris_hip as ih
+from oracle import oracle_c as oc
+
+pytestmark = pytest.mark.gpu
+ROT = 31
+DRAWS = 24
+
+
+def _draws(seed, max_records):
+    rng = np.random.default_rng(seed)
+    for _ in range(DRAWS):
+        total = int(rng.integers(1, max_records))
+        first = int(rng.integers(0, total))
+        n = int(rng.integers(0, total - first + 1))
+        layout = [ih.LAYOUT_TILES, ih.LAYOUT_LANES][int(rng.integers(0, 2))]
+        yield total, first, n, layout
+
+
+def bits_eq(a, b):
+    return (np.asarray(a, np.float64).view(np.uint64) == np.asarray(b, np.float64).view(np.uint64)).all()
+
+
+def test_fuzz_templates(device):
+    recs = oc.gen_templates(101, 0, 700)
+    for i, (total, first, n, layout) in enumerate(_draws(1, 700)):
+        q = recs[(i * 37) % total].copy()
+        q[:200] ^= np.uint64(1 << (i % 64))
+        with ih.Database(device, ih.KIND_TEMPLATES, total, layout) as db, ih.TemplateEngine(device, q) as eng:
+            db.append(recs[:total])
+            num, den = eng.counts(db, first, n)
+            wn, wd = oc.template_counts(q, recs[first:first + n])
+            assert (num == wn).all() and (den == wd).all(), (total, first, n, layout)
+            d = eng.distances(db, first, n)
+            wdist = oc.template_distances(q, recs[first:first + n])
+            assert bits_eq(d, wdist), (total, first, n, layout)
+            m = eng.search(db, first, n, index_base=5)
+            best, idx = oc.argmin(wdist) if n else (np.inf, 2**64 - 1)
+            assert bits_eq(m.distance, best)
+            assert m.index == (idx + 5 + first if idx != 2**64 - 1 else idx), (total, first, n, layout)
+
+
+def test_fuzz_masks_and_shares(device):
+    masks = oc.gen_templates(102, 0, 600)[:, 200:].copy()
+    shares = np.random.default_rng(103).integers(0, 2**16, (300, 12800), dtype=np.uint16)
+    for i, (total, first, n, layout) in enumerate(_draws(2, 300)):
+        qm = masks[(i * 11) % total]
+        qs = shares[(i * 7) % total]
+        with ih.Database(device, ih.KIND_MASKS, total, layout) as mdb, ih.MasksEngine(device, qm) as me, \
+                ih.Database(device, ih.KIND_SHARES, total, layout) as sdb, ih.DistanceEngine(device, qs) as de:
+            mdb.append(masks[:total])
+            sdb.append(shares[:total])
+            out = np.empty((n, ROT), np.uint16)
+            me.batch_process(out, mdb, first=first, n=n)
+            assert (out == oc.masks_batch(qm, masks[first:first + n])).all(), (total, first, n, layout)
+            out2 = np.empty((n, ROT), np.uint16)
+            de.batch_process(out2, sdb, first=first, n=n)
+            assert (out2 == oc.distance_batch(qs, shares[first:first + n])).all(), (total, first, n, layout)
+            parts = [np.random.default_rng(i + p).integers(0, 2**16, (n, ROT), dtype=np.uint16) for p in range(2)]
+            m = me.resolve(mdb, parts, first=first, n=n)
+            if n:
+                best, idx = oc.argmin(oc.resolver_combine(np.stack(parts), out))
+                assert m.index == idx and bits_eq(m.distance, best), (total, first, n, layout)
+            else:
+                assert m.index == 2**64 - 1
