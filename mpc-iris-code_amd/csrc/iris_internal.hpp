@@ -176,6 +176,9 @@ int launch_prepare_shares(void *stream, const void *templates, uint64_t m, uint6
 constexpr int kMaxPrepParties = 64;
 int launch_prepare_shares_tiles(void *stream, const void *templates, uint64_t m, uint64_t g0, const uint8_t key[32],
                                 uint64_t nonce, uint32_t parties, void *const *dbs, const uint64_t *t_first);
+int launch_prepare_direct(void *stream, const void *tdb, uint64_t t_first, uint64_t m, uint64_t g0,
+                          const uint8_t key[32], uint64_t nonce, uint32_t parties, void *const *dbs,
+                          const uint64_t *s_first, void *masks, uint64_t m_first);
 int launch_unpack(void *stream, const KindInfo &k, const void *db, void *staging, uint64_t t_first, uint64_t n);
 int launch_generate(void *stream, const KindInfo &k, void *db, uint64_t t_first, uint64_t n, uint64_t seed,
                     uint64_t global_index0);

@@ -377,6 +377,24 @@ extern "C" int iris_prepare_shares(const iris_db_t *templates, uint64_t first, u
     if (first > templates->len || n > templates->len - first)
         return fail(IRIS_E_RANGE, "record range outside the database");
     if (n == 0) return 0;
+    bool all_tiles = templates->k.layout == IRIS_LAYOUT_TILES && (!masks || masks->k.layout == IRIS_LAYOUT_TILES);
+    for (uint32_t j = 0; j < parties; ++j) all_tiles &= shares[j]->k.layout == IRIS_LAYOUT_TILES;
+    if (all_tiles) {  // one in-place launch: TILES templates -> TILES shares + masks
+        std::vector<void *> dbp(parties);
+        std::vector<uint64_t> sf(parties);
+        for (uint32_t j = 0; j < parties; ++j) {
+            dbp[j] = shares[j]->data;
+            sf[j] = shares[j]->len;
+        }
+        CHK(timed(d, "prepare", n, [&] {
+            return launch_prepare_direct(d->stream, templates->data, first, n, index_base + first, key, nonce, parties,
+                                         dbp.data(), sf.data(), masks ? masks->data : nullptr, masks ? masks->len : 0);
+        }));
+        CHK(sync(d));
+        for (uint32_t j = 0; j < parties; ++j) shares[j]->len += n;
+        if (masks) masks->len += n;
+        return 0;
+    }
     // staging per record: template (3200 B) | mask (1600 B) | the shares (25600 B each) unless
     // every share database is TILES, which the keystream kernel writes in place
     bool direct = true;

@@ -160,6 +160,71 @@ __global__ void __launch_bounds__(256) prepare_shares_tiles_kernel(const uint32_
     }
 }
 
+// Fully in place: templates read from a TILES template database (one 8-byte
+// xpacked pair per (template, dword b), unpacked with xunpack), shares and the
+// optional masks written straight into TILES databases — one launch, no
+// staging.  The masks dword b of record t is component (b & 6) / 2 of the
+// 16-byte word (b / 8, half b & 1) of its tile (pack_masks_tiles' layout).
+__global__ void __launch_bounds__(256) prepare_direct_kernel(const uint4 *__restrict__ tdb, uint64_t t_first,
+                                                             uint64_t m, uint64_t g0, ChachaKey key, uint64_t nonce,
+                                                             uint32_t parties, ShareDsts dst, uint4 *masks,
+                                                             uint64_t m_first) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint64_t i = (uint64_t)blockIdx.x * 64 + lane;
+    if (i >= m) return;
+    const uint64_t tt = t_first + i;
+    const uint4 *tbase = tdb + (tt / 32) * (uint64_t)(kPlaneGroups * 64) + (tt % 32);
+    uint32_t *mbase = nullptr;
+    if (masks) {
+        const uint64_t mt = m_first + i;
+        mbase = (uint32_t *)(masks + (mt / 32) * (uint64_t)kMaskTileUint4 + (mt % 32));
+    }
+    const uint64_t g = g0 + i;
+    for (int b = w; b < kBlocks; b += 4) {
+        // dword b of the pattern / mask planes: word (b / 4, half b & 1), pair (b >> 1) & 1
+        const uint2 x = ((const uint2 *)(tbase + (b >> 2) * 64 + 32 * (b & 1)))[(b >> 1) & 1];
+        uint32_t emlo, eplo, emhi, ephi;
+        xunpack(x.x, emlo, eplo);
+        xunpack(x.y, emhi, ephi);
+        const uint32_t mw = emlo | (emhi << 16), pw = eplo | (ephi << 16);
+        if (mbase) mbase[4 * ((b >> 3) * 64 + 32 * (b & 1)) + ((b & 6) >> 1)] = mw;
+        uint32_t last[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const uint32_t m0 = (mw >> (2 * q)) & 1u, m1 = (mw >> (2 * q + 1)) & 1u;
+            const uint32_t p0 = (pw >> (2 * q)) & 1u, p1 = (pw >> (2 * q + 1)) & 1u;
+            last[q] = ((m0 - 2u * (p0 & m0)) & 0xFFFFu) | (((m1 - 2u * (p1 & m1)) & 0xFFFFu) << 16);
+        }
+        for (uint32_t j = 0; j + 1 < parties; ++j) {
+            uint32_t r[16];
+            chacha20_block(key, nonce, (g * (parties - 1) + j) * kBlocks + (uint64_t)b, r);
+            store_share_block(dst.db[j], dst.t_first[j] + i, b, r);
+#pragma unroll
+            for (int q = 0; q < 16; ++q) last[q] = pk_sub_u16(last[q], r[q]);
+        }
+        store_share_block(dst.db[parties - 1], dst.t_first[parties - 1] + i, b, last);
+    }
+}
+
+int launch_prepare_direct(void *stream, const void *tdb, uint64_t t_first, uint64_t m, uint64_t g0,
+                          const uint8_t key[32], uint64_t nonce, uint32_t parties, void *const *dbs,
+                          const uint64_t *s_first, void *masks, uint64_t m_first) {
+    if (m == 0) return 0;
+    if (parties == 0 || parties > (uint32_t)kMaxPrepParties) return -1;
+    ChachaKey k;
+    for (int i = 0; i < 8; ++i)
+        k.k[i] = (uint32_t)key[4 * i] | ((uint32_t)key[4 * i + 1] << 8) | ((uint32_t)key[4 * i + 2] << 16) |
+                 ((uint32_t)key[4 * i + 3] << 24);
+    ShareDsts d{};
+    for (uint32_t j = 0; j < parties; ++j) {
+        d.db[j] = (uint4 *)dbs[j];
+        d.t_first[j] = s_first[j];
+    }
+    hipLaunchKernelGGL(prepare_direct_kernel, dim3((uint32_t)((m + 63) / 64)), dim3(256), 0, (hipStream_t)stream,
+                       (const uint4 *)tdb, t_first, m, g0, k, nonce, parties, d, (uint4 *)masks, m_first);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 int launch_prepare_shares_tiles(void *stream, const void *templates, uint64_t m, uint64_t g0, const uint8_t key[32],
                                 uint64_t nonce, uint32_t parties, void *const *dbs, const uint64_t *t_first) {
     if (m == 0) return 0;
