@@ -77,6 +77,40 @@ def planted_record(query, rotation):
     return np.concatenate([p, m])
 
 
+def gen_records(dev, kind, n, seed):
+    """Host copies of records from the library's on-device generator."""
+    with ih.Database(dev, kind, max(n, 1)) as g:
+        g.generate(n, seed)
+        return g.read(0, n)
+
+
+# Result checks of the bench (numpy restatements, independent of the kernels; the
+# oracle/ package is used only by the cpu_baseline leg).
+def check_masks_rows(qmask, recs):
+    """[s, 31] popcount(rot(qmask, k-15) & rec) (src/lib.rs:69-79)."""
+    rot = np.stack([ih.Bits(qmask).rotated(k - 15).limbs for k in range(ROT)])
+    x = (np.asarray(recs, np.uint64)[:, None, :] & rot[None, :, :]).view(np.uint8)
+    return np.unpackbits(x, axis=-1).sum(axis=-1).astype(np.uint16)
+
+
+def check_shares_rows(q, recs):
+    """[s, 31] sum(rot(q, k-15) * rec) mod 2^16 (src/lib.rs:42-52)."""
+    rot = np.stack([ih.EncodedBits(q).rotated(k - 15).values for k in range(ROT)]).astype(np.uint64)
+    return ((np.asarray(recs, np.uint64) @ rot.T) % 65536).astype(np.uint16)
+
+
+def check_resolver(shares, denoms):
+    """The resolver loop (src/main.rs:597-621): wrapping share sum, decode_distance
+    (src/lib.rs:97-107), first strict minimum -> (distance, index)."""
+    num = np.add.reduce(np.asarray(shares, np.uint16), axis=0, dtype=np.uint16)
+    den = np.asarray(denoms, np.uint16)
+    uneq = ((den - num).astype(np.uint16) >> 1).astype(np.float64)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        d = np.where(den != 0, uneq / den.astype(np.float64), np.inf).min(axis=1)
+    idx = int(np.argmin(d))
+    return (float(d[idx]), idx) if np.isfinite(d[idx]) else (float("inf"), 2**64 - 1)
+
+
 def cpu_baseline(seconds):
     """The oracle's engine-style CPU path (test infrastructure), compiled for
     this host, timed on a bounded sample of the same workload."""
@@ -136,8 +170,6 @@ def load_traffic(workload, n_per_launch, layout):
 def run_aux(args, dev):
     """Single-GPU lines for the §8(f) workloads beside the hot path: the fused
     resolver (share sum + decode + argmin) and GPU share preparation."""
-    from oracle import oracle_c as oc  # result check only
-
     P = args.parties
     rng = np.random.default_rng(SEED)
     ptrs = []
@@ -163,7 +195,7 @@ def run_aux(args, dev):
             dev.h2d(ptrs[j], shares[j])
         mdb = ih.Database(dev, ih.KIND_MASKS, n)
         mdb.generate(n, SEED)
-        qmask = oc.gen_templates(SEED + 1, 0, 1)[0][200:].copy()
+        qmask = gen_records(dev, ih.KIND_MASKS, 1, SEED + 1)[0]
         eng = ih.MasksEngine(dev, qmask)
 
         def step():
@@ -191,12 +223,12 @@ def run_aux(args, dev):
     elif args.workload in ("host-shares", "host-masks"):
         shares_wl = args.workload == "host-shares"
         n = min(args.n_per_gpu, 200_000 if shares_wl else 2_000_000)  # 5.1 GB / 3.2 GB of host records
-        qt = oc.gen_templates(SEED + 1, 0, 1)[0]
+        qt = gen_records(dev, ih.KIND_TEMPLATES, 1, SEED + 1)[0]
         if shares_wl:
             host = rng.integers(0, 65536, (n, 12800), dtype=np.uint16)
             eng = ih.DistanceEngine(dev, ih.encode(ih.Template.from_array(qt)))
         else:
-            host = oc.gen_templates(SEED, 0, n)[:, 200:].copy()
+            host = gen_records(dev, ih.KIND_MASKS, n, SEED)
             eng = ih.MasksEngine(dev, qt[200:])
         hout = np.empty((n, ROT), np.uint16)
 
@@ -236,35 +268,36 @@ def run_aux(args, dev):
     dev.set_profiling(False)
     launches, kms, items = dev.kernel_stats(kname)
     achieved = rec_bytes * items / (kms * 1e-3) / 1e9
-    if args.workload == "resolve-masks":  # denominators from the (separately tested) masks engine
+    if args.workload == "resolve-masks":  # denominators from the (separately checked) masks engine
         denoms = np.empty((n, ROT), np.uint16)
         eng.batch_process(denoms, mdb)
         sample = np.random.default_rng(1).choice(n, 64, replace=False)
-        assert (denoms[sample] == oc.masks_batch(qmask, mdb.read(0, n)[sample] if n <= 100_000 else
-                                                 np.stack([mdb.read(int(i), 1)[0] for i in sample]))).all()
+        recs = np.stack([mdb.read(int(i), 1)[0] for i in sample])
+        assert (denoms[sample] == check_masks_rows(qmask, recs)).all()
     if args.workload in ("resolver", "resolve-masks"):
-        best, idx = oc.argmin(oc.resolver_combine(shares, denoms))
+        best, idx = check_resolver(shares, denoms)
         ok = m.index == idx and np.float64(m.distance).view(np.uint64) == np.float64(best).view(np.uint64)
-        check = {"oracle_index": int(idx), "found_index": int(m.index), "ok": bool(ok)}
+        check = {"expected_index": int(idx), "found_index": int(m.index), "ok": bool(ok)}
     elif args.workload in ("host-shares", "host-masks"):
         sample = np.random.default_rng(2).choice(n, 16, replace=False)
-        want = (oc.distance_batch(ih.encode(ih.Template.from_array(qt)).values, host[sample])
-                if args.workload == "host-shares" else oc.masks_batch(qt[200:], host[sample]))
+        want = (check_shares_rows(ih.encode(ih.Template.from_array(qt)).values, host[sample])
+                if args.workload == "host-shares" else check_masks_rows(qt[200:], host[sample]))
         ok = bool((hout[sample] == want).all())
-        check = {"sampled_outputs_vs_oracle": len(sample), "ok": ok}
+        check = {"sampled_outputs_checked": len(sample), "ok": ok}
     elif args.workload == "load":
         sample = [0, n // 3, n - 1]
         ok = m == n and all((tdb.read(i, 1) == src.read(i, 1)).all() for i in sample)
         fpath.unlink()
         check = {"sampled_templates_vs_source": len(sample), "ok": bool(ok)}
-    else:
+    else:  # EncodedBits::share identity: the shares sum to encode(template); masks copied
         sample = [0, n // 3, n - 1]
         ok = True
         for i in sample:
-            want, wm = oc.prepare_shares(tdb.read(i, 1), key, parties=P, index_base=i)
-            ok &= all((sdbs[j].read(i, 1)[0] == want[j, 0]).all() for j in range(P))
-            ok &= bool((mdb.read(i, 1)[0] == wm[0]).all())
-        check = {"sampled_templates_vs_oracle": len(sample), "ok": bool(ok)}
+            t = tdb.read(i, 1)[0]
+            total = np.add.reduce(np.stack([sdbs[j].read(i, 1)[0] for j in range(P)]), axis=0, dtype=np.uint16)
+            ok &= bool((total == ih.encode(ih.Template.from_array(t)).values).all())
+            ok &= bool((mdb.read(i, 1)[0] == t[200:]).all())
+        check = {"sampled_templates_share_identity": len(sample), "ok": bool(ok)}
     line = {
         "metric": {"resolver": "resolver records/s (share sum + decode + argmin)",
                    "resolve-masks": "resolver records/s (masks engine + share sum + decode + argmin, fused)",
@@ -335,9 +368,7 @@ def main():
     db.generate(n, SEED, global_index0=lo)
     gen_s = time.time() - t0
 
-    from oracle import oracle_c as oc  # query/plant construction only (host data)
-
-    query = oc.gen_templates(SEED + 1, 0, 1)[0]
+    query = gen_records(dev, ih.KIND_TEMPLATES, 1, SEED + 1)[0]
     plant_global = total * 3 // 4 + 12345
     plant_rot = 9
     out_dev = None
@@ -348,7 +379,7 @@ def main():
     if args.workload == "search":
         eng = ih.TemplateEngine(dev, query)
     elif args.workload == "batch":
-        batch_q = oc.gen_templates(SEED + 2, 0, nq)
+        batch_q = gen_records(dev, ih.KIND_TEMPLATES, nq, SEED + 2)
         batch_q[nq // 2] = query  # its best match is the planted record
         eng = ih.TemplateBatchEngine(dev, batch_q)
     elif args.workload == "masks":
@@ -409,13 +440,13 @@ def main():
         mq = m[nq // 2]
         ok = mq.index == plant_global and mq.rotation == plant_rot
         m = mq
-    else:  # spot-check 64 outputs against the oracle
+    else:  # spot-check 64 outputs
         sample = np.random.default_rng(0).choice(n, 64, replace=False)
         full = np.empty((n, ROT), np.uint16)
         dev.d2h(full, out_dev)
         recs = np.stack([db.read(int(i), 1)[0] for i in sample])
-        want = (oc.masks_batch(query[200:], recs) if args.workload == "masks"
-                else oc.distance_batch(ih.encode(ih.Template.from_array(query)).values, recs))
+        want = (check_masks_rows(query[200:], recs) if args.workload == "masks"
+                else check_shares_rows(ih.encode(ih.Template.from_array(query)).values, recs))
         ok = bool((full[sample] == want).all())
         del full
     launches, kms, items = dev.kernel_stats(kname)
@@ -485,7 +516,7 @@ def main():
             "cpu_baseline": cpu,
             "check": ({"planted_index": plant_global, "found_index": int(m.index), "rotation": int(m.rotation),
                        "distance": m.distance, "ok": bool(ok)} if args.workload in ("search", "batch")
-                      else {"sampled_outputs_vs_oracle": 64, "ok": bool(ok)}),
+                      else {"sampled_outputs_checked": 64, "ok": bool(ok)}),
             "setup": {"generate_s": gen_s},
         }
         print(json.dumps(line))
