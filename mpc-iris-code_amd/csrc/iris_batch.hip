@@ -29,13 +29,17 @@ typedef int v8i __attribute__((ext_vector_type(8)));
 typedef float v16f __attribute__((ext_vector_type(16)));
 
 constexpr int BQ = 4;                     // queries per workgroup
-constexpr int BT = 8;                     // template tiles per N-group
+#ifndef IRIS_BATCH_NW
+#define IRIS_BATCH_NW 8
+#endif
+constexpr int NW = IRIS_BATCH_NW;         // waves per workgroup (8: one workgroup per CU, 4: two)
 #ifndef IRIS_BATCH_WQ
 #define IRIS_BATCH_WQ 2
 #endif
 constexpr int WQ = IRIS_BATCH_WQ;         // queries per wave
 constexpr int WT = 4 / WQ;                // tiles per wave (WQ x WT = 4 accumulator pairs)
 constexpr int kQW = BQ / WQ;              // waves per tile set
+constexpr int BT = (NW / kQW) * WT;       // template tiles per N-group
 constexpr int KSTEP = 4;                  // chunks per K-step
 constexpr int NSTEPS = kPlaneDwords / 2 / KSTEP;  // 50
 constexpr int kTileU4 = kPlaneGroups * 64;        // 6400 uint4 per tile
@@ -49,7 +53,8 @@ __device__ __forceinline__ v16f mfma4(const v8i &a, const v8i &b, const v16f &c)
 
 constexpr int kRows = 2 * (BQ + BT);  // 1-KB rows per stage: 4 queries + 8 tiles, 2 chunk pairs each
 constexpr int kRing = 4;              // LDS stages: 3 in flight + the one being read
-constexpr int kRowsPerWave = kRows / 8;
+constexpr int kRowsPerWave = kRows / NW;
+static_assert(kRows % NW == 0, "DMA rows must split evenly over the waves");
 
 // Staging is LDS-DMA (global_load_lds_dwordx4, lane-linear 1-KB rows) into a
 // 4-stage ring: each K-step waits for its own rows with a counted vmcnt (the
@@ -57,7 +62,7 @@ constexpr int kRowsPerWave = kRows / 8;
 // step three ahead into the slot everyone finished reading a step ago.
 // Each workgroup walks its N-groups as one flat stream of K-steps, so the
 // pipeline never drains between N-groups.
-__global__ void __launch_bounds__(512, 1)
+__global__ void __launch_bounds__(64 * NW, 8 / NW)
     batch_kernel(const uint4 *__restrict__ db, const uint4 *__restrict__ qtiles, uint64_t tile0, uint64_t ntiles,
                  uint64_t first, uint64_t end, uint32_t nqg, uint32_t G, Partial *__restrict__ partials) {
     __shared__ uint4 ring[kRing][kRows][64];  // all LDS in one object (no vmcnt(0) before ds_reads)
@@ -74,7 +79,7 @@ __global__ void __launch_bounds__(512, 1)
     int row_t[kRowsPerWave];
 #pragma unroll
     for (int i = 0; i < kRowsPerWave; ++i) {
-        const int r = w + 8 * i;
+        const int r = w + NW * i;
         row_t[i] = r < 2 * BQ ? -1 : (r - 2 * BQ) >> 1;
         const int gp = r & 1;
         src_q[i] = r < 2 * BQ ? qtiles + (uint64_t)(qg * BQ + (r >> 1)) * kTileU4 + gp * 64 + lane
@@ -85,7 +90,7 @@ __global__ void __launch_bounds__(512, 1)
         const uint64_t ng = gi + (uint64_t)j * G;
 #pragma unroll
         for (int i = 0; i < kRowsPerWave; ++i) {
-            const int r = w + 8 * i;
+            const int r = w + NW * i;
             const uint4 *src;
             if (row_t[i] < 0) {
                 src = src_q[i] + (2 * k) * 64;
@@ -235,7 +240,7 @@ __global__ void __launch_bounds__(512, 1)
     if (tid < BQ) {  // query tid: waves with wq0 <= tid < wq0 + WQ, one per tile set
         const int qi = tid % WQ, wl = tid / WQ;
         Partial b = sP[wl * WQ + qi];
-        for (int ts = 1; ts < 8 / kQW; ++ts)
+        for (int ts = 1; ts < NW / kQW; ++ts)
             if (partial_better_dev(sP[(ts * kQW + wl) * WQ + qi], b)) b = sP[(ts * kQW + wl) * WQ + qi];
         partials[(uint64_t)(qg * BQ + tid) * G + gi] = b;
     }
@@ -287,7 +292,7 @@ BatchGeometry batch_geometry(LaunchRange r, uint32_t nq) {
 int launch_batch(void *stream, const void *db, const void *qtiles, LaunchRange r, const BatchGeometry &g,
                  Partial *partials, Partial *out) {
     if (r.n == 0) return 0;
-    hipLaunchKernelGGL(batch_kernel, dim3(g.nqg * g.G), dim3(512), 0, (hipStream_t)stream, (const uint4 *)db,
+    hipLaunchKernelGGL(batch_kernel, dim3(g.nqg * g.G), dim3(64 * NW), 0, (hipStream_t)stream, (const uint4 *)db,
                        (const uint4 *)qtiles, g.tile0, g.ntiles, r.first, r.first + r.n, g.nqg, g.G, partials);
     if (hipGetLastError() != hipSuccess) return -1;
     hipLaunchKernelGGL(batch_reduce_kernel, dim3(g.nqg * BQ), dim3(256), 0, (hipStream_t)stream, partials, g.G, out);
