@@ -2,6 +2,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 #include "iris_internal.hpp"
 
 namespace iris {
@@ -9,15 +11,15 @@ namespace iris {
 // Workgroups of one launch that fit on the current device at `per_cu` per CU
 // (persistent grids); cached per device ordinal.
 static inline uint64_t resident_blocks(int per_cu) {
-    static int cus[64] = {0};
+    static std::atomic<int> cus[64];  // zero-initialised (static storage)
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
-    if (cus[dev] == 0) {
-        int n = 0;
+    int n = cus[dev].load(std::memory_order_relaxed);
+    if (n == 0) {
         if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-        cus[dev] = n;
+        cus[dev].store(n, std::memory_order_relaxed);
     }
-    return (uint64_t)cus[dev] * per_cu;
+    return (uint64_t)n * per_cu;
 }
 
 typedef unsigned int u32x4_nt __attribute__((ext_vector_type(4)));
