@@ -34,7 +34,13 @@ def allgather_merge(local, device=None):
     if device is not None:
         t = t.to(device)
     world = dist.get_world_size()
-    out = [torch.empty_like(t) for _ in range(world)]
-    dist.all_gather(out, t)
-    recs = [ih.Match.from_buffer_copy(o.cpu().numpy().tobytes()) for o in out]
+    if t.is_cuda:  # RCCL: one [world * 32] byte tensor, one device-to-host copy
+        flat = torch.empty(world * RECORD_BYTES, dtype=torch.uint8, device=t.device)
+        dist.all_gather_into_tensor(flat, t)
+        raw = flat.cpu().numpy().tobytes()
+        recs = [ih.Match.from_buffer_copy(raw[i * RECORD_BYTES:(i + 1) * RECORD_BYTES]) for i in range(world)]
+    else:
+        out = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(out, t)
+        recs = [ih.Match.from_buffer_copy(o.numpy().tobytes()) for o in out]
     return ih.merge_matches(recs)

@@ -39,3 +39,24 @@ def test_bench_two_ranks(workload):
     assert d["n_gpus"] == 2 and d["check"]["ok"]
     assert d["config"]["total_templates"] == 400000
     assert d["check"]["planted_index"] >= 200000  # the answer lives in rank 1's shard
+
+
+def test_rccl_exchange_single_rank():
+    """The RCCL form of the exchange (all_gather_into_tensor on device tensors) on a
+    one-rank "nccl" process group: the code path the 8-GPU run takes."""
+    code = f"""
+import os, sys
+sys.path[:0] = [{str(ROOT)!r}, {str(ROOT / 'mpc-iris-code_amd')!r}]
+os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT="{_free_port()}")
+import torch, torch.distributed as dist
+import iris_hip as ih, iris_dist
+torch.cuda.set_device(0)
+dist.init_process_group("nccl", rank=0, world_size=1)
+m = ih.Match(0.25, 1234, 5, 20, -3, 0)
+r = iris_dist.allgather_merge(m, device="cuda:0")
+assert (r.index, r.num, r.den, r.rotation) == (1234, 5, 20, -3) and r.distance == 0.25, r
+dist.destroy_process_group()
+print("rccl ok")
+"""
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and "rccl ok" in r.stdout, r.stdout + r.stderr[-3000:]
