@@ -342,7 +342,9 @@ def main():
     # rehearses the same flow with CPU exchange tensors (e.g. 2 ranks on 1 GPU).
     backend = os.environ.get("IRIS_DIST_BACKEND", "nccl")
     ordinal = local
-    if world > 1:
+    # IRIS_FORCE_DIST=1 runs the process-group path even for one rank (a one-GPU rehearsal of
+    # the RCCL exchange, barriers and max-over-ranks timing)
+    if world > 1 or os.environ.get("IRIS_FORCE_DIST") == "1":
         import torch
         import torch.distributed as dist
 

@@ -60,3 +60,15 @@ print("rccl ok")
 """
     r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0 and "rccl ok" in r.stdout, r.stdout + r.stderr[-3000:]
+
+
+def test_bench_rccl_single_rank():
+    """bench.py's process-group path with the default "nccl" (RCCL) backend on one rank."""
+    env = dict(os.environ, IRIS_FORCE_DIST="1", IRIS_DIST_BACKEND="nccl")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(ROOT / "bench.py"),
+           "--steps", "3", "--warmup", "1", "--n-per-gpu", "300000", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert d["n_gpus"] == 1 and d["check"]["ok"]
