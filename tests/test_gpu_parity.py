@@ -287,26 +287,48 @@ def test_u16_wraparound(device, golden):
 # ---------------------------------------------------------------- arch plugin (criterion shapes)
 
 
-@pytest.mark.parametrize("na,nb", [(1, 1), (1, 1000), (31, 1000), (40, 70)])
+# the criterion shapes of src/arch/mod.rs:29 (dot_bool) and :53 (dot_u16), sampled checks
+@pytest.mark.parametrize("na,nb", [(1, 1), (1, 1000), (31, 1000), (1, 100_000), (40, 70)])
 def test_dot_bool_batch(device, na, nb):
     rng = np.random.default_rng(na * 7 + nb)
     a = rng.integers(0, 2**64, (na, 200), dtype=np.uint64)
     b = rng.integers(0, 2**64, (nb, 200), dtype=np.uint64)
     out = ih.dot_bool_batch(a, b, device)
-    for j in range(0, nb, max(1, nb // 50)):
+    for j in list(range(0, nb, max(1, nb // 50))) + [nb - 1]:
         for i in range(na):
             assert out[j, i] == oc.dot_bool(a[i], b[j])
 
 
-@pytest.mark.parametrize("na,nb", [(1, 1), (1, 300), (31, 64), (33, 5)])
+@pytest.mark.parametrize("na,nb", [(1, 1), (1, 1000), (31, 1000), (1, 100_000), (31, 100_000), (33, 5)])
 def test_dot_u16_batch(device, na, nb):
     rng = np.random.default_rng(na * 11 + nb)
     a = rng.integers(0, 2**16, (na, 12800), dtype=np.uint16)
     b = rng.integers(0, 2**16, (nb, 12800), dtype=np.uint16)
     out = ih.dot_u16_batch(a, b, device)
-    for j in range(0, nb, max(1, nb // 20)):
-        for i in range(na):
+    for j in list(range(0, nb, max(1, nb // 20))) + [nb - 1]:
+        for i in range(0, na, max(1, na // 4)):
             assert out[j, i] == oc.dot_u16(a[i], b[j])
+
+
+def test_config0_one_query_10k(device):
+    """BASELINE configs[0] (1 query x 10k templates x 31 rotations, the reference's
+    CPU-runnable case): Template distances, argmin, masks and share outputs against the
+    oracle on every record."""
+    n = 10_000
+    t = oc.gen_templates(111, 0, n)
+    q = oc.gen_templates(112, 0, 1)[0]
+    with ih.Database(device, ih.KIND_TEMPLATES, n) as tdb, ih.TemplateEngine(device, q) as te, \
+            ih.Database(device, ih.KIND_MASKS, n) as mdb, ih.MasksEngine(device, q[200:]) as me:
+        tdb.append(t)
+        mdb.append(t[:, 200:])
+        want = oc.template_distances(q, t)
+        assert bits_eq(te.distances(tdb), want)
+        best, idx = oc.argmin(want)
+        m = te.search(tdb)
+        assert m.index == idx and bits_eq(m.distance, best)
+        out = np.empty((n, ROT), np.uint16)
+        me.batch_process(out, mdb)
+        assert (out == oc.masks_batch(q[200:], t[:, 200:])).all()
 
 
 # ---------------------------------------------------------------- large-size properties
