@@ -603,6 +603,53 @@ static int search_locked(iris_engine_t *e, const iris_db_t *db, uint64_t first, 
     return 0;
 }
 
+// two queries in one streamed pass (TILES databases; LANES runs them one at a time)
+static int pair_search_locked(iris_engine_t *a, iris_engine_t *b, const iris_db_t *db, uint64_t first, uint64_t n,
+                              uint64_t index_base, iris_match_t *out) {
+    if (db->k.layout != IRIS_LAYOUT_TILES) {
+        CHK(search_locked(a, db, first, n, index_base, nullptr, out));
+        return search_locked(b, db, first, n, index_base, nullptr, out + 1);
+    }
+    iris_device *d = a->dev;
+    LaunchRange r{first, n};
+    const uint32_t np = multi_search_partials(r, 2);
+    CHK(ensure(d->partials, (size_t)std::max<uint32_t>(2 * np, 1) * sizeof(Partial)));
+    CHK(ensure(d->result, 2 * sizeof(Partial)));
+    const void *qf[2] = {a->qfrag, b->qfrag};
+    uint32_t written = 0;
+    CHK(timed(d, "template_batch", 2 * n, [&] {
+        return launch_template_multi_search(d->stream, db->data, qf, 2, r, (Partial *)d->partials.p, &written);
+    }));
+    Partial res[2] = {};
+    if (n > 0) {
+        for (int q = 0; q < 2; ++q)
+            CHK(timed(d, "reduce", written, [&] {
+                return launch_reduce(d->stream, (Partial *)d->partials.p + (size_t)q * written, written,
+                                     (Partial *)d->result.p + q);
+            }));
+        HIPCHK(hipMemcpyAsync(res, d->result.p, 2 * sizeof(Partial), hipMemcpyDeviceToHost, d->stream));
+    }
+    CHK(sync(d));
+    for (int q = 0; q < 2; ++q) {
+        iris_match_t &m = out[q];
+        if (n == 0 || res[q].den == 0) {
+            m.distance = INFINITY;
+            m.index = UINT64_MAX;
+            m.num = 0;
+            m.den = 0;
+            m.rotation = 0;
+        } else {
+            m.distance = (double)res[q].num / (double)res[q].den;
+            m.index = index_base + first + res[q].idx;
+            m.num = res[q].num;
+            m.den = res[q].den;
+            m.rotation = res[q].rot - IRIS_MAX_ROTATION;
+        }
+        m.reserved = 0;
+    }
+    return 0;
+}
+
 int iris_template_search(iris_engine_t *e, const iris_db_t *db, uint64_t first, uint64_t n, uint64_t index_base,
                          double *dist_out_device, iris_match_t *out) {
     CHK(template_args(e, db));
@@ -640,7 +687,7 @@ int iris_template_batch_engine_new(iris_device_t *d, const iris_template_t *quer
     ARG(nq > 0, "a batch needs at least one query");
     std::lock_guard<std::recursive_mutex> g(d->mu);
     CHK(set_device(d));
-    if (nq <= kBatchSingles) {
+    if (nq <= kBatchStreamMax) {
         iris_engine *e = new (std::nothrow) iris_engine();
         if (!e) return fail(IRIS_E_NOMEM, "out of host memory");
         e->dev = d;
@@ -682,7 +729,9 @@ int iris_template_batch_search(iris_engine_t *e, const iris_db_t *db, uint64_t f
     CHK(set_device(d));
     CHK(range_ok(db, first, n));
     if (!e->sub.empty()) {
-        for (uint32_t q = 0; q < e->nq; ++q) CHK(search_locked(e->sub[q], db, first, n, index_base, nullptr, out + q));
+        uint32_t q = 0;
+        for (; q + 2 <= e->nq; q += 2) CHK(pair_search_locked(e->sub[q], e->sub[q + 1], db, first, n, index_base, out + q));
+        if (q < e->nq) CHK(search_locked(e->sub[q], db, first, n, index_base, nullptr, out + q));
         return 0;
     }
     LaunchRange r{first, n};

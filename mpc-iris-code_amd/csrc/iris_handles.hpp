@@ -81,13 +81,15 @@ struct iris_engine {
     void *qtab = nullptr;     // SGPR rotated-query table (LANES kernels)
     void *qfrag = nullptr;    // fp4 query fragments (TILES kernel, templates only)
     uint32_t nq = 0;          // > 0: batched template engine (qfrag = nq padded query tiles)
-    std::vector<iris_engine *> sub;  // batched engine of <= kBatchSingles queries: one single-query engine each
+    std::vector<iris_engine *> sub;  // streaming batched engine: one single-query engine per query
 };
 
-// Up to this many queries a batch runs as single-query streaming searches: the
-// batched GEMM pads to groups of 4 queries, and below 3 queries the single-query
-// kernels (HBM-bound, ~4.8 ms per query per 10M) finish first.
-constexpr uint32_t kBatchSingles = 2;
+// Up to this many queries a batch runs as streaming passes over the database —
+// two queries per pass (template_multi_kernel<2>), an odd last one alone —
+// instead of the LDS-tiled GEMM (batch_kernel), which pads to groups of 4
+// queries.  Measured per 10M templates: 2 queries 7.5 ms (GEMM 13.4 ms), 3
+// queries 12.3 ms (GEMM ~14 ms); from 4 queries on the GEMM is ahead.
+constexpr uint32_t kBatchStreamMax = 3;
 
 namespace iris_api {
 

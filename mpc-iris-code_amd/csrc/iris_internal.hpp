@@ -189,6 +189,10 @@ int launch_template_mfma_counts(void *stream, const void *db, const void *qfrag,
 int launch_template_mfma_search(void *stream, const void *db, const void *qfrag, LaunchRange r, double *dist_out,
                                 Partial *partials, uint32_t *n_partials);
 uint32_t mfma_search_partials(LaunchRange r);
+// nq = 2 queries per streamed pass; partials [nq][*n_partials]
+uint32_t multi_search_partials(LaunchRange r, int nq);
+int launch_template_multi_search(void *stream, const void *db, const void *const *qfrags, int nq, LaunchRange r,
+                                 Partial *partials, uint32_t *n_partials);
 int launch_pack_tiles(void *stream, const void *staging, void *db, uint64_t t_first, uint64_t n);
 int launch_unpack_tiles(void *stream, const void *db, void *staging, uint64_t t_first, uint64_t n);
 int launch_generate_tiles(void *stream, void *db, uint64_t t_first, uint64_t n, uint64_t seed, uint64_t global_index0);

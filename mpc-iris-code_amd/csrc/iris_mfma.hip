@@ -221,6 +221,148 @@ __global__ void __launch_bounds__(256, 2)
     }
 }
 
+// ------------------------------------------------------------------ a few queries per pass
+
+// NQ queries against one streamed pass of the database: per 64-bit chunk and
+// tile 2 NQ MFMAs share one expansion of the template bits, so up to NQ = 2 the
+// pass stays near the HBM bound while one single-query pass per query would
+// stream the database NQ times.  T = 4 / NQ tiles per wave keeps the NQ x T x 2
+// accumulators at 128 VGPRs.  Partials: [NQ][gridDim.x].
+struct QueryFrags {
+    const uint4 *q[4];
+};
+
+template <int NQ>
+__global__ void __launch_bounds__(256, 2)
+    template_multi_kernel(const uint4 *__restrict__ db, QueryFrags qf, uint64_t tile0, uint64_t ntiles,
+                          uint64_t first, uint64_t end, Partial *__restrict__ partials) {
+    constexpr int T = 4 / NQ;
+    const int lane = threadIdx.x & 63;
+    const int wslot = threadIdx.x >> 6;
+    const uint64_t wave = (uint64_t)blockIdx.x * kWaveSlots + wslot;
+    const uint64_t tw = wave * T;
+    const bool active = tw < ntiles;  // wave-uniform
+
+    v16f den[NQ][T], s[NQ][T];
+#pragma unroll
+    for (int qi = 0; qi < NQ; ++qi)
+#pragma unroll
+        for (int t = 0; t < T; ++t)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                den[qi][t][i] = 0.f;
+                s[qi][t][i] = 0.f;
+            }
+
+    if (active) {
+        const uint4 *dp[T];
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+            const uint64_t rel = (tw + t < ntiles) ? tw + t : ntiles - 1;
+            dp[t] = db + (tile0 + rel) * (uint64_t)kTileUint4 + lane;
+        }
+        struct Stage {
+            uint4 d[T];
+            uint4 q[NQ][2];
+        };
+        auto load = [&](Stage &st, int g) {
+            g = g < kPlaneGroups ? g : kPlaneGroups - 1;
+#pragma unroll
+            for (int t = 0; t < T; ++t) st.d[t] = stream_load(dp[t] + g * 64);
+#pragma unroll
+            for (int qi = 0; qi < NQ; ++qi) {
+                st.q[qi][0] = qf.q[qi][(2 * g) * 64 + lane];
+                st.q[qi][1] = qf.q[qi][(2 * g + 1) * 64 + lane];
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        auto compute = [&](const Stage &st) {
+#pragma unroll
+            for (int qi = 0; qi < NQ; ++qi) {
+                const QFrag f0 = qfrag_of(st.q[qi][0]);
+#pragma unroll
+                for (int t = 0; t < T; ++t) chunk_step(st.d[t].x, st.d[t].y, f0, den[qi][t], s[qi][t]);
+                const QFrag f1 = qfrag_of(st.q[qi][1]);
+#pragma unroll
+                for (int t = 0; t < T; ++t) chunk_step(st.d[t].z, st.d[t].w, f1, den[qi][t], s[qi][t]);
+            }
+        };
+        Stage sa, sb, sc;
+        load(sa, 0);
+        load(sb, 1);
+        int g = 0;
+#pragma unroll 1
+        for (; g + 3 <= kPlaneGroups; g += 3) {
+            load(sc, g + 2);
+            compute(sa);
+            load(sa, g + 3);
+            compute(sb);
+            load(sb, g + 4);
+            compute(sc);
+        }
+        if (g < kPlaneGroups) compute(sa);
+    }
+
+    const int h = lane >> 5;
+    Partial best[NQ];
+#pragma unroll
+    for (int qi = 0; qi < NQ; ++qi) best[qi] = partial_none();
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        const uint64_t tg = (tile0 + tw + t) * kTileRecs + (lane & 31);
+        const bool valid = active && (tw + t < ntiles) && tg >= first && tg < end;
+#pragma unroll
+        for (int qi = 0; qi < NQ; ++qi) {
+            uint32_t bn = 0, bd = 0;
+            int br = 0;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int k = (r & 3) + 8 * (r >> 2) + 4 * h;
+                const uint32_t dd = (uint32_t)den[qi][t][r];
+                const uint32_t nn = (uint32_t)(((int)dd - (int)s[qi][t][r]) >> 1);
+                if (k < kRot && dd != 0 && (bd == 0 || nn * bd < bn * dd)) {
+                    bn = nn;
+                    bd = dd;
+                    br = k;
+                }
+            }
+            const uint32_t pn = __shfl_xor(bn, 32), pd = __shfl_xor(bd, 32);
+            const int pr = __shfl_xor(br, 32);
+            if (better_rot(pn, pd, pr, bn, bd, br)) {
+                bn = pn;
+                bd = pd;
+                br = pr;
+            }
+            Partial c;
+            c.num = bn;
+            c.den = valid ? bd : 0;
+            c.rot = br;
+            c.pad = 0;
+            c.idx = tg - first;
+            if (partial_better_dev(c, best[qi])) best[qi] = c;
+        }
+    }
+    __shared__ Partial sh[NQ][kWaveSlots];
+#pragma unroll
+    for (int qi = 0; qi < NQ; ++qi) {
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            const Partial ot = partial_shfl_xor(best[qi], off);
+            if (partial_better_dev(ot, best[qi])) best[qi] = ot;
+        }
+        if (lane == 0) sh[qi][wslot] = best[qi];
+    }
+    __syncthreads();
+    if (threadIdx.x < NQ) {
+        const int qi = threadIdx.x;
+        Partial b = sh[qi][0];
+#pragma unroll
+        for (int w = 1; w < kWaveSlots; ++w)
+            if (partial_better_dev(sh[qi][w], b)) b = sh[qi][w];
+        partials[(uint64_t)qi * gridDim.x + blockIdx.x] = b;
+    }
+}
+
 // ------------------------------------------------------------------ TILES layout plumbing
 
 // reference Template record (pattern dwords 0..399, mask dwords 400..799) ->
@@ -333,6 +475,25 @@ static TileRange tile_range(LaunchRange r) {
 }
 
 uint32_t mfma_search_partials(LaunchRange r) { return (uint32_t)tile_range(r).grid; }
+
+uint32_t multi_search_partials(LaunchRange r, int nq) {
+    const uint64_t tile0 = r.first / kTileRecs, tile1 = (r.first + r.n + kTileRecs - 1) / kTileRecs;
+    const uint64_t waves = (tile1 - tile0 + (4 / nq) - 1) / (4 / nq);
+    return (uint32_t)((waves + kWaveSlots - 1) / kWaveSlots);
+}
+
+int launch_template_multi_search(void *stream, const void *db, const void *const *qfrags, int nq, LaunchRange r,
+                                 Partial *partials, uint32_t *n_partials) {
+    *n_partials = multi_search_partials(r, nq);
+    if (r.n == 0) return 0;
+    if (nq != 2) return -1;
+    const uint64_t tile0 = r.first / kTileRecs, tile1 = (r.first + r.n + kTileRecs - 1) / kTileRecs;
+    QueryFrags qf{};
+    for (int i = 0; i < nq; ++i) qf.q[i] = (const uint4 *)qfrags[i];
+    hipLaunchKernelGGL(template_multi_kernel<2>, dim3(*n_partials), dim3(256), 0, (hipStream_t)stream,
+                       (const uint4 *)db, qf, tile0, tile1 - tile0, r.first, r.first + r.n, partials);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 int launch_template_mfma_counts(void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *num_out,
                                 uint16_t *den_out) {
