@@ -188,31 +188,16 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW)
         if (s - j * NSTEPS != NSTEPS - 1) continue;
         // N-group done: per template, min over the 16 rows of this lane, then the partner half
         const uint64_t ng = gi + (uint64_t)j * G;
-        const int h = lane >> 5;
 #pragma unroll
         for (int qi = 0; qi < WQ; ++qi)
 #pragma unroll
             for (int t = 0; t < WT; ++t) {
-                uint32_t bn = 0, bd = 0;
-                int br = 0;
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int k = (r & 3) + 8 * (r >> 2) + 4 * h;
-                    const uint32_t dd = (uint32_t)den[qi][t][r];
-                    const uint32_t nn = (uint32_t)(((int)dd - (int)sacc[qi][t][r]) >> 1);
-                    if (k < kRot && dd != 0 && (bd == 0 || nn * bd < bn * dd)) {
-                        bn = nn;
-                        bd = dd;
-                        br = k;
-                    }
-                }
-                const uint32_t pn = __shfl_xor(bn, 32), pd = __shfl_xor(bd, 32);
-                const int pr = __shfl_xor(br, 32);
-                if (pd != 0 && (bd == 0 || pn * bd < bn * pd || (pn * bd == bn * pd && pr < br))) {
-                    bn = pn;
-                    bd = pd;
-                    br = pr;
-                }
+                uint32_t bn, bd;
+                int br;
+                best_rotation(lane, [&](int r, uint32_t &nn, uint32_t &dd) {
+                    dd = (uint32_t)den[qi][t][r];
+                    nn = (uint32_t)(((int)dd - (int)sacc[qi][t][r]) >> 1);
+                }, bn, bd, br);
                 const uint64_t trel2 = ng * BT + wsub + t;
                 const uint64_t tg = (tile0 + trel2) * 32 + (lane & 31);
                 const bool valid = trel2 < ntiles && tg >= first && tg < end;

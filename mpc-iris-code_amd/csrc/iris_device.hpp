@@ -98,6 +98,37 @@ __device__ __forceinline__ Partial partial_shfl_xor(const Partial &c, int off) {
     return o;
 }
 
+// One template's best rotation from a 32x32 MFMA C tile: lane l holds rows
+// k = (r & 3) + 8 (r >> 2) + 4 (l >> 5), r = 0..15, of template l & 31, and
+// frac(r, num, den) yields row r's fraction.  Exact order (u32 cross-
+// multiplication; den = 0 is no candidate), lowest rotation on ties; after the
+// exchange with lane l ^ 32 both halves hold the template's best (k in 0..30).
+template <class F>
+__device__ __forceinline__ void best_rotation(int lane, F frac, uint32_t &bn, uint32_t &bd, int &br) {
+    const int h = lane >> 5;
+    bn = 0;
+    bd = 0;
+    br = 0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int k = (r & 3) + 8 * (r >> 2) + 4 * h;  // ascending in r within a half
+        uint32_t nn, dd;
+        frac(r, nn, dd);
+        if (k < kRot && dd != 0 && (bd == 0 || nn * bd < bn * dd)) {
+            bn = nn;
+            bd = dd;
+            br = k;
+        }
+    }
+    const uint32_t pn = __shfl_xor(bn, 32), pd = __shfl_xor(bd, 32);
+    const int pr = __shfl_xor(br, 32);
+    if (pd != 0 && (bd == 0 || pn * bd < bn * pd || (pn * bd == bn * pd && pr < br))) {
+        bn = pn;
+        bd = pd;
+        br = pr;
+    }
+}
+
 __device__ __forceinline__ Partial partial_none() {
     Partial p;
     p.num = 0;

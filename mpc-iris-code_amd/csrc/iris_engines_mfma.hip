@@ -143,27 +143,13 @@ __global__ void __launch_bounds__(256, 2)
         __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's LDS writes landed
         __builtin_amdgcn_wave_barrier();
         const int h = lane >> 5;
-        uint32_t bn = 0, bd = 0;
-        int br = 0;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
+        uint32_t bn, bd;
+        int br;
+        best_rotation(lane, [&](int r, uint32_t &u, uint32_t &d) {
             const int k = (r & 3) + 8 * (r >> 2) + 4 * h;
-            if (k >= kRot) continue;
-            const uint32_t d = (uint32_t)den[r] & 0xFFFFu;  // the MasksEngine output value (u16)
-            const uint32_t u = (uint16_t)(d - lds[(lane & 31) * kRot + k]) >> 1;  // src/lib.rs:104
-            if (d != 0 && (bd == 0 || u * bd < bn * d)) {  // k ascending within a half
-                bn = u;
-                bd = d;
-                br = k;
-            }
-        }
-        const uint32_t pn = __shfl_xor(bn, 32), pd = __shfl_xor(bd, 32);
-        const int pr = __shfl_xor(br, 32);
-        if (pd != 0 && (bd == 0 || pn * bd < bn * pd || (pn * bd == bn * pd && pr < br))) {
-            bn = pn;
-            bd = pd;
-            br = pr;
-        }
+            d = (uint32_t)den[r] & 0xFFFFu;  // the MasksEngine output value (u16)
+            u = k < kRot ? (uint32_t)((uint16_t)(d - lds[(lane & 31) * kRot + k]) >> 1) : 0;  // src/lib.rs:104
+        }, bn, bd, br);
         const uint64_t tg = t0 + (lane & 31);
         const bool valid = tv && tg >= first && tg < end;
         if (valid && rs.dist_out && h == 0) rs.dist_out[tg - first] = bd ? (double)bn / (double)bd : __builtin_inf();

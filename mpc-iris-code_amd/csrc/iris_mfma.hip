@@ -67,15 +67,6 @@ __device__ __forceinline__ uint4 stream_load(const uint4 *p) {
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
-// candidate order inside one template: fraction, then lowest rotation
-__device__ __forceinline__ bool better_rot(uint32_t an, uint32_t ad, int ar, uint32_t bn, uint32_t bd, int br) {
-    if (ad == 0) return false;
-    if (bd == 0) return true;
-    const uint32_t l = an * bd, r = bn * ad;
-    if (l != r) return l < r;
-    return ar < br;
-}
-
 enum { MF_COUNTS = 0, MF_SEARCH = 1 };
 
 template <int MODE>
@@ -172,26 +163,12 @@ __global__ void __launch_bounds__(256, 2)
             const uint64_t tg = t0 + (lane & 31);
             const bool valid = tv && tg >= first && tg < end;
             const uint64_t o = tg - first;
-            uint32_t bn = 0, bd = 0;
-            int br = 0;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int k = (r & 3) + 8 * (r >> 2) + 4 * h;
-                const uint32_t dd = (uint32_t)den[t][r];
-                const uint32_t nn = (uint32_t)(((int)dd - (int)s[t][r]) >> 1);
-                if (k < kRot && dd != 0 && (bd == 0 || nn * bd < bn * dd)) {
-                    bn = nn;
-                    bd = dd;
-                    br = k;
-                }
-            }
-            const uint32_t pn = __shfl_xor(bn, 32), pd = __shfl_xor(bd, 32);
-            const int pr = __shfl_xor(br, 32);
-            if (better_rot(pn, pd, pr, bn, bd, br)) {
-                bn = pn;
-                bd = pd;
-                br = pr;
-            }
+            uint32_t bn, bd;
+            int br;
+            best_rotation(lane, [&](int r, uint32_t &nn, uint32_t &dd) {
+                dd = (uint32_t)den[t][r];
+                nn = (uint32_t)(((int)dd - (int)s[t][r]) >> 1);  // num = (den - S) / 2
+            }, bn, bd, br);
             if (valid && dist_out && h == 0) dist_out[o] = bd ? (double)bn / (double)bd : __builtin_inf();
             Partial c;
             c.num = bn;
@@ -303,7 +280,6 @@ __global__ void __launch_bounds__(256, 2)
         if (g < kPlaneGroups) compute(sa);
     }
 
-    const int h = lane >> 5;
     Partial best[NQ];
 #pragma unroll
     for (int qi = 0; qi < NQ; ++qi) best[qi] = partial_none();
@@ -313,26 +289,12 @@ __global__ void __launch_bounds__(256, 2)
         const bool valid = active && (tw + t < ntiles) && tg >= first && tg < end;
 #pragma unroll
         for (int qi = 0; qi < NQ; ++qi) {
-            uint32_t bn = 0, bd = 0;
-            int br = 0;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int k = (r & 3) + 8 * (r >> 2) + 4 * h;
-                const uint32_t dd = (uint32_t)den[qi][t][r];
-                const uint32_t nn = (uint32_t)(((int)dd - (int)s[qi][t][r]) >> 1);
-                if (k < kRot && dd != 0 && (bd == 0 || nn * bd < bn * dd)) {
-                    bn = nn;
-                    bd = dd;
-                    br = k;
-                }
-            }
-            const uint32_t pn = __shfl_xor(bn, 32), pd = __shfl_xor(bd, 32);
-            const int pr = __shfl_xor(br, 32);
-            if (better_rot(pn, pd, pr, bn, bd, br)) {
-                bn = pn;
-                bd = pd;
-                br = pr;
-            }
+            uint32_t bn, bd;
+            int br;
+            best_rotation(lane, [&](int r, uint32_t &nn, uint32_t &dd) {
+                dd = (uint32_t)den[qi][t][r];
+                nn = (uint32_t)(((int)dd - (int)s[qi][t][r]) >> 1);
+            }, bn, bd, br);
             Partial c;
             c.num = bn;
             c.den = valid ? bd : 0;
