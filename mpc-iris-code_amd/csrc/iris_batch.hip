@@ -37,7 +37,10 @@ constexpr int NW = IRIS_BATCH_NW;         // waves per workgroup (8: one workgro
 #define IRIS_BATCH_WQ 2
 #endif
 constexpr int WQ = IRIS_BATCH_WQ;         // queries per wave
-constexpr int WT = 4 / WQ;                // tiles per wave (WQ x WT = 4 accumulator pairs)
+#ifndef IRIS_BATCH_WT
+#define IRIS_BATCH_WT (4 / IRIS_BATCH_WQ)
+#endif
+constexpr int WT = IRIS_BATCH_WT;         // tiles per wave (WQ x WT accumulator pairs)
 constexpr int kQW = BQ / WQ;              // waves per tile set
 constexpr int BT = (NW / kQW) * WT;       // template tiles per N-group
 constexpr int KSTEP = 4;                  // chunks per K-step
@@ -53,8 +56,8 @@ __device__ __forceinline__ v16f mfma4(const v8i &a, const v8i &b, const v16f &c)
 
 constexpr int kRows = 2 * (BQ + BT);  // 1-KB rows per stage: 4 queries + 8 tiles, 2 chunk pairs each
 constexpr int kRing = 4;              // LDS stages: 3 in flight + the one being read
-constexpr int kRowsPerWave = kRows / NW;
-static_assert(kRows % NW == 0, "DMA rows must split evenly over the waves");
+constexpr int kRowsPerWave = (kRows + NW - 1) / NW;  // waves w < kRows - NW (kRowsPerWave - 1) issue one more
+constexpr bool kEvenRows = kRows % NW == 0;
 
 // Staging is LDS-DMA (global_load_lds_dwordx4, lane-linear 1-KB rows) into a
 // 4-stage ring: each K-step waits for its own rows with a counted vmcnt (the
@@ -62,7 +65,7 @@ static_assert(kRows % NW == 0, "DMA rows must split evenly over the waves");
 // step three ahead into the slot everyone finished reading a step ago.
 // Each workgroup walks its N-groups as one flat stream of K-steps, so the
 // pipeline never drains between N-groups.
-__global__ void __launch_bounds__(64 * NW, 8 / NW)
+__global__ void __launch_bounds__(64 * NW, NW <= 8 ? 8 / NW : 1)
     batch_kernel(const uint4 *__restrict__ db, const uint4 *__restrict__ qtiles, uint64_t tile0, uint64_t ntiles,
                  uint64_t first, uint64_t end, uint32_t nqg, uint32_t G, Partial *__restrict__ partials) {
     __shared__ uint4 ring[kRing][kRows][64];  // all LDS in one object (no vmcnt(0) before ds_reads)
@@ -91,6 +94,7 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW)
 #pragma unroll
         for (int i = 0; i < kRowsPerWave; ++i) {
             const int r = w + NW * i;
+            if (!kEvenRows && r >= kRows) break;  // wave-uniform
             const uint4 *src;
             if (row_t[i] < 0) {
                 src = src_q[i] + (2 * k) * 64;
@@ -141,10 +145,11 @@ __global__ void __launch_bounds__(64 * NW, 8 / NW)
 #pragma unroll 1
     for (uint32_t s = 0; s < total; ++s) {
         // wait for this step's rows (this wave's), then for everyone's
+        const bool more = kEvenRows || w + NW * (kRowsPerWave - 1) < kRows;  // this wave's rows per step
         if (s + 2 < total) {
-            VMCNT(2 * kRowsPerWave);
+            if (more) VMCNT(2 * kRowsPerWave); else VMCNT(2 * (kRowsPerWave - 1));
         } else if (s + 1 < total) {
-            VMCNT(kRowsPerWave);
+            if (more) VMCNT(kRowsPerWave); else VMCNT(kRowsPerWave - 1);
         } else {
             VMCNT(0);
         }
