@@ -49,7 +49,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--n-per-gpu", type=int, default=10_000_000)
+    ap.add_argument("--n-per-gpu", type=int, default=None,
+                    help="records per GPU (default 10M; search with 2+ ranks: 12.5M, so 8 ranks are configs[4]'s 100M)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--layout", choices=["tiles", "lanes"], default="tiles",
@@ -354,6 +355,8 @@ def main():
         import iris_dist
     xdev = f"cuda:{ordinal}" if backend == "nccl" else "cpu"
 
+    if args.n_per_gpu is None:  # configs[1] at N=1; configs[4] (100M over 8 GPUs) at N=8
+        args.n_per_gpu = 12_500_000 if (args.workload == "search" and world > 1) else 10_000_000
     n = args.n_per_gpu
     lo = rank * n
     total = n * world
@@ -485,7 +488,7 @@ def main():
             "data": "synthetic (on-device counter-based generator, uniform random pattern+mask bits; planted known answer)",
             "config": {
                 "workload": {
-                    "search": "1 query x 31 rotations x N templates, Template masked Hamming + fused min/argmin (BASELINE configs[1] at N=1)",
+                    "search": "1 query x 31 rotations x N templates, Template masked Hamming + fused min/argmin (BASELINE configs[1] at N=1: 10M; 12.5M per GPU from 2 ranks, configs[4] = 100M over 8 GPUs)",
                     "masks": "MasksEngine: 1 query mask x 31 rotations x N masks, [u16;31] denominators left in HBM",
                     "shares": "DistanceEngine: 1 encoded query x 31 rotations x N u16 shares, [u16;31] left in HBM (BASELINE configs[3])",
                     "batch": f"{nq} queries x 31 rotations x N templates in one pass, per-query min/argmin (BASELINE configs[2])",
