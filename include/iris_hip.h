@@ -275,6 +275,19 @@ int iris_encode(const iris_template_t *t, uint16_t out[IRIS_BITS]);
 /* decode_distance(&[u16;31], &[u16;31]) -> f64 (src/lib.rs:97-107) */
 int iris_decode_distance(const uint16_t distances[IRIS_ROTATIONS], const uint16_t denominators[IRIS_ROTATIONS],
                          double *out);
+/* Diagnostics for the query tables an engine builds on the device
+ * (iris_query.hip): iris_engine_query_tables copies an engine's rotated-query
+ * table and MFMA fragments to the host; iris_host_query_tables builds the same
+ * bytes with the host reference builders.  kind = IRIS_KIND_*; for
+ * IRIS_KIND_TEMPLATES nq = 0 is a single-query engine and nq >= 4 the tiles of
+ * a batched engine of nq queries (`query` = nq templates; `tab` unused).  The
+ * sizes must be the layout's exactly (IRIS_E_ARG otherwise; see
+ * iris_query_table_sizes). */
+int iris_query_table_sizes(int kind, uint32_t nq, size_t *tab_bytes, size_t *frag_bytes);
+int iris_engine_query_tables(const iris_engine_t *engine, void *tab, size_t tab_bytes, void *frag,
+                             size_t frag_bytes);
+int iris_host_query_tables(int kind, const void *query, uint32_t nq, void *tab, size_t tab_bytes, void *frag,
+                           size_t frag_bytes);
 /* Merges per-shard search results into the global one (min fraction, then
  * lowest index) — the cross-shard step of the resolver's argmin (src/main.rs:616-621). */
 int iris_match_merge(const iris_match_t *records, uint64_t count, iris_match_t *out);

@@ -95,36 +95,121 @@ int run_u16_engine(iris_engine *e, const iris_db *db, uint64_t first, uint64_t n
     return 0;
 }
 
+constexpr size_t kQbufAlign = 256;
+constexpr size_t kQpoolMax = 16;
+
+inline size_t qalign(size_t b) { return (b + kQbufAlign - 1) / kQbufAlign * kQbufAlign; }
+
+// A query buffer of at least `bytes`: a pooled one of up to twice the size, else hipMalloc.
+int qbuf_take(iris_device *d, size_t bytes, void **p, size_t *got) {
+    size_t best = SIZE_MAX, bi = 0;
+    for (size_t i = 0; i < d->qpool.size(); ++i) {
+        const size_t b = d->qpool[i].first;
+        if (b >= bytes && b <= 2 * bytes && b < best) {
+            best = b;
+            bi = i;
+        }
+    }
+    if (best != SIZE_MAX) {
+        *p = d->qpool[bi].second;
+        *got = best;
+        d->qpool.erase(d->qpool.begin() + bi);
+        return 0;
+    }
+    hipError_t e = hipMalloc(p, bytes);
+    if (e != hipSuccess) return fail(IRIS_E_NOMEM, std::string("hipMalloc query buffer: ") + hipGetErrorString(e));
+    *got = bytes;
+    return 0;
+}
+
 void engine_free(iris_engine *e) {
     if (!e) return;
     for (iris_engine *c : e->sub) engine_free(c);
-    if (e->qtab) (void)hipFree(e->qtab);
-    if (e->qfrag) (void)hipFree(e->qfrag);
+    if (e->qbuf) {
+        iris_device *d = e->dev;
+        // later users of the buffer are ordered after this engine's kernels on the device stream
+        if (d->qpool.size() < kQpoolMax) d->qpool.emplace_back(e->qbuf_bytes, e->qbuf);
+        else (void)hipFree(e->qbuf);
+    }
     delete e;
 }
 
-// Uploads the LANES table and (optionally) the TILES fragments of a new engine.
-int engine_new(iris_device *dev, int kind, const void *table, size_t bytes, iris_engine **out,
-               const void *frag = nullptr, size_t frag_bytes = 0) {
+// A new engine whose query buffer holds [table | fragments | extra] (each 256-B aligned).
+int engine_alloc(iris_device *dev, int kind, size_t tab_bytes, size_t frag_bytes, size_t extra_bytes,
+                 iris_engine **out, void **extra = nullptr) {
     iris_engine *e = new (std::nothrow) iris_engine();
     if (!e) return fail(IRIS_E_NOMEM, "out of host memory");
     e->dev = dev;
     e->kind = kind;
-    hipError_t err = hipMalloc(&e->qtab, bytes);
-    if (err == hipSuccess && frag) err = hipMalloc(&e->qfrag, frag_bytes);
-    if (err != hipSuccess) {
-        engine_free(e);
-        return fail(IRIS_E_NOMEM, std::string("hipMalloc query table: ") + hipGetErrorString(err));
+    const size_t total = qalign(tab_bytes) + qalign(frag_bytes) + qalign(extra_bytes);
+    int rc = qbuf_take(dev, total, &e->qbuf, &e->qbuf_bytes);
+    if (rc != 0) {
+        delete e;
+        return rc;
     }
-    err = hipMemcpyAsync(e->qtab, table, bytes, hipMemcpyHostToDevice, dev->stream);
+    char *base = (char *)e->qbuf;
+    e->qtab = tab_bytes ? base : nullptr;
+    e->qfrag = frag_bytes ? base + qalign(tab_bytes) : nullptr;
+    if (extra) *extra = base + qalign(tab_bytes) + qalign(frag_bytes);
+    *out = e;
+    return 0;
+}
+
+// Uploads host-built tables (LANES table and, optionally, TILES fragments) of a new engine.
+int engine_new(iris_device *dev, int kind, const void *table, size_t bytes, iris_engine **out,
+               const void *frag = nullptr, size_t frag_bytes = 0) {
+    iris_engine *e = nullptr;
+    CHK(engine_alloc(dev, kind, bytes, frag ? frag_bytes : 0, 0, &e));
+    hipError_t err = hipMemcpyAsync(e->qtab, table, bytes, hipMemcpyHostToDevice, dev->stream);
     if (err == hipSuccess && frag) err = hipMemcpyAsync(e->qfrag, frag, frag_bytes, hipMemcpyHostToDevice, dev->stream);
-    if (err == hipSuccess) err = hipStreamSynchronize(dev->stream);
     if (err != hipSuccess) {
         engine_free(e);
         return fail(IRIS_E_HIP, std::string("upload query table: ") + hipGetErrorString(err));
     }
     *out = e;
     return 0;
+}
+
+// Uploads a query (`qbytes` from the host) and builds the engine's tables from it
+// on the device with `build(stream, query_dev, tab, frag)` (iris_query.hip).
+template <class B>
+int engine_from_query(iris_device *dev, int kind, const void *query, size_t qbytes, size_t tab_bytes,
+                      size_t frag_bytes, iris_engine **out, B &&build) {
+    iris_engine *e = nullptr;
+    void *qdev = nullptr;
+    CHK(engine_alloc(dev, kind, tab_bytes, frag_bytes, qbytes, &e, &qdev));
+    hipError_t err = hipMemcpyAsync(qdev, query, qbytes, hipMemcpyHostToDevice, dev->stream);
+    if (err != hipSuccess || build(dev->stream, qdev, (uint32_t *)e->qtab, (uint32_t *)e->qfrag) != 0) {
+        if (err == hipSuccess) err = hipGetLastError();
+        engine_free(e);
+        return fail(IRIS_E_HIP, std::string("build query tables: ") + hipGetErrorString(err));
+    }
+    *out = e;
+    return 0;
+}
+
+void device_teardown(iris_device *d) {
+    {
+        std::lock_guard<std::recursive_mutex> g(d->mu);
+        (void)hipSetDevice(d->ordinal);
+        (void)hipStreamSynchronize(d->stream);
+        for (DevBuf *b : {&d->partials, &d->result, &d->staging, &d->out_a, &d->out_b})
+            if (b->p) (void)hipFree(b->p);
+        for (auto &q : d->qpool) (void)hipFree(q.second);
+        d->qpool.clear();
+        for (auto &p : d->pending) {
+            (void)hipEventDestroy(p.a);
+            (void)hipEventDestroy(p.b);
+        }
+        for (auto e : d->event_pool) (void)hipEventDestroy(e);
+        (void)hipStreamDestroy(d->stream);
+    }
+    delete d;
+}
+
+inline void device_retain(iris_device *d) { d->refs.fetch_add(1, std::memory_order_relaxed); }
+inline void device_release(iris_device *d) {
+    if (d->refs.fetch_sub(1, std::memory_order_acq_rel) == 1) device_teardown(d);
 }
 
 constexpr size_t kMaskFragBytes = kMaskFragUint4 * 16;
@@ -178,20 +263,7 @@ int iris_device_open(int ordinal, iris_device_t **out) {
 
 int iris_device_close(iris_device_t *d) {
     if (!d) return 0;
-    {
-        std::lock_guard<std::recursive_mutex> g(d->mu);
-        (void)hipSetDevice(d->ordinal);
-        (void)hipStreamSynchronize(d->stream);
-        for (DevBuf *b : {&d->partials, &d->result, &d->staging, &d->out_a, &d->out_b})
-            if (b->p) (void)hipFree(b->p);
-        for (auto &p : d->pending) {
-            (void)hipEventDestroy(p.a);
-            (void)hipEventDestroy(p.b);
-        }
-        for (auto e : d->event_pool) (void)hipEventDestroy(e);
-        (void)hipStreamDestroy(d->stream);
-    }
-    delete d;
+    device_release(d);  // torn down now, or when its last database / engine is destroyed
     return 0;
 }
 
@@ -300,6 +372,7 @@ int iris_db_create_ex(iris_device_t *d, int kind, uint64_t capacity, int layout,
         delete db;
         return fail(IRIS_E_HIP, std::string("memset database: ") + hipGetErrorString(e));
     }
+    device_retain(d);
     *out = db;
     return 0;
 }
@@ -312,13 +385,15 @@ int iris_db_layout(const iris_db_t *db, int *layout) {
 
 int iris_db_destroy(iris_db_t *db) {
     if (!db) return 0;
+    iris_device *d = db->dev;
     {
-        std::lock_guard<std::recursive_mutex> g(db->dev->mu);
-        (void)hipSetDevice(db->dev->ordinal);
-        (void)hipStreamSynchronize(db->dev->stream);
+        std::lock_guard<std::recursive_mutex> g(d->mu);
+        (void)hipSetDevice(d->ordinal);
+        (void)hipStreamSynchronize(d->stream);
         if (db->data) (void)hipFree(db->data);
     }
     delete db;
+    device_release(d);
     return 0;
 }
 
@@ -413,55 +488,47 @@ int iris_masks_engine_new(iris_device_t *d, const uint64_t query_mask[IRIS_LIMBS
     ARG(d && query_mask && out, "NULL argument");
     std::lock_guard<std::recursive_mutex> g(d->mu);
     CHK(set_device(d));
-    std::vector<uint32_t> tab((size_t)kPlaneDwords * kSlotTabStride);
-    build_masks_rotations(query_mask, tab.data());
-    std::vector<uint64_t> rot((size_t)kRot * IRIS_LIMBS);
-    const uint64_t *ptrs[kRot];
-    for (int k = 0; k < kRot; ++k) {
-        bits_rotated(query_mask, k - 15, &rot[(size_t)k * IRIS_LIMBS]);
-        ptrs[k] = &rot[(size_t)k * IRIS_LIMBS];
-    }
-    std::vector<uint32_t> frag(kMaskFragBytes / 4);
-    build_masks_frags(ptrs, kRot, frag.data());
-    return engine_new(d, IRIS_KIND_MASKS, tab.data(), tab.size() * 4, out, frag.data(), kMaskFragBytes);
+    CHK(engine_from_query(d, IRIS_KIND_MASKS, query_mask, IRIS_LIMBS * 8, (size_t)kPlaneDwords * kSlotTabStride * 4,
+                          kMaskFragBytes, out, launch_query_masks));
+    device_retain(d);
+    return 0;
 }
 
 int iris_distance_engine_new(iris_device_t *d, const uint16_t query[IRIS_BITS], iris_engine_t **out) {
     ARG(d && query && out, "NULL argument");
     std::lock_guard<std::recursive_mutex> g(d->mu);
     CHK(set_device(d));
-    std::vector<uint32_t> tab((size_t)kShareDwords * kSlotTabStride);
-    build_shares_rotations(query, tab.data());
-    std::vector<uint16_t> rot((size_t)kRot * IRIS_BITS);
-    const uint16_t *ptrs[kRot];
-    for (int k = 0; k < kRot; ++k) {
-        encoded_rotated(query, k - 15, &rot[(size_t)k * IRIS_BITS]);
-        ptrs[k] = &rot[(size_t)k * IRIS_BITS];
-    }
-    std::vector<uint32_t> frag(kShareFragBytes / 4);
-    build_shares_frags(ptrs, kRot, frag.data());
-    return engine_new(d, IRIS_KIND_SHARES, tab.data(), tab.size() * 4, out, frag.data(), kShareFragBytes);
+    CHK(engine_from_query(d, IRIS_KIND_SHARES, query, IRIS_BITS * 2, (size_t)kShareDwords * kSlotTabStride * 4,
+                          kShareFragBytes, out, launch_query_shares));
+    device_retain(d);
+    return 0;
 }
+
+namespace {
+int template_engine_locked(iris_device *d, const iris_template_t *query, iris_engine **out) {
+    return engine_from_query(d, IRIS_KIND_TEMPLATES, query, sizeof(iris_template_t),
+                             (size_t)kPlaneDwords * kTemplateTabStride * 4, kTemplateFragDwords * 4, out,
+                             launch_query_template);
+}
+}  // namespace
 
 int iris_template_engine_new(iris_device_t *d, const iris_template_t *query, iris_engine_t **out) {
     ARG(d && query && out, "NULL argument");
     std::lock_guard<std::recursive_mutex> g(d->mu);
     CHK(set_device(d));
-    std::vector<uint32_t> tab((size_t)kPlaneDwords * kTemplateTabStride);
-    build_template_table(query, tab.data());
-    std::vector<uint32_t> frag(kTemplateFragDwords);
-    build_template_frags(query, frag.data());
-    return engine_new(d, IRIS_KIND_TEMPLATES, tab.data(), tab.size() * 4, out, frag.data(), frag.size() * 4);
+    CHK(template_engine_locked(d, query, out));
+    device_retain(d);
+    return 0;
 }
 
 int iris_engine_destroy(iris_engine_t *e) {
     if (!e) return 0;
+    iris_device *d = e->dev;
     {
-        std::lock_guard<std::recursive_mutex> g(e->dev->mu);
-        (void)hipSetDevice(e->dev->ordinal);
-        (void)hipStreamSynchronize(e->dev->stream);
-        engine_free(e);
+        std::lock_guard<std::recursive_mutex> g(d->mu);
+        engine_free(e);  // no wait: the buffers go back to the device's pool, reuse is stream-ordered
     }
+    device_release(d);
     return 0;
 }
 
@@ -694,26 +761,26 @@ int iris_template_batch_engine_new(iris_device_t *d, const iris_template_t *quer
         e->kind = IRIS_KIND_TEMPLATES;
         e->nq = nq;
         for (uint32_t i = 0; i < nq; ++i) {
-            iris_engine_t *c = nullptr;
-            const int rc = iris_template_engine_new(d, queries + i, &c);
+            iris_engine *c = nullptr;
+            const int rc = template_engine_locked(d, queries + i, &c);
             if (rc != 0) {
                 engine_free(e);
                 return rc;
             }
             e->sub.push_back(c);
         }
+        device_retain(d);
         *out = e;
         return 0;
     }
     const uint32_t nqp = (nq + 3) / 4 * 4;  // padded to the kernel's query groups (zero tiles: no candidate)
-    const size_t tile_dw = (size_t)4 * kPlaneGroups * 64;
-    std::vector<uint32_t> tiles((size_t)nqp * tile_dw, 0u);
-    for (uint32_t i = 0; i < nq; ++i) build_query_tile(queries + i, tiles.data() + i * tile_dw);
-    uint32_t dummy = 0;
-    iris_engine *e = nullptr;
-    CHK(engine_new(d, IRIS_KIND_TEMPLATES, &dummy, sizeof(dummy), &e, tiles.data(), tiles.size() * 4));
-    e->nq = nq;
-    *out = e;
+    const size_t tile_bytes = (size_t)16 * kPlaneGroups * 64;
+    CHK(engine_from_query(d, IRIS_KIND_TEMPLATES, queries, (size_t)nq * sizeof(iris_template_t), 0,
+                          (size_t)nqp * tile_bytes, out, [&](void *stream, const void *q, uint32_t *, uint32_t *frag) {
+                              return launch_query_tiles(stream, q, nq, nqp, frag);
+                          }));
+    (*out)->nq = nq;
+    device_retain(d);
     return 0;
 }
 
@@ -989,6 +1056,78 @@ int iris_decode_distance(const uint16_t distances[IRIS_ROTATIONS], const uint16_
         acc = rust_f64_min(acc, (double)uneq / (double)dd);        // src/lib.rs:105-106
     }
     *out = acc;
+    return 0;
+}
+
+int iris_query_table_sizes(int kind, uint32_t nq, size_t *tab_bytes, size_t *frag_bytes) {
+    ARG(tab_bytes && frag_bytes, "NULL argument");
+    switch (kind) {
+    case IRIS_KIND_TEMPLATES:
+        ARG(nq == 0 || nq > kBatchStreamMax, "nq must be 0 (single query) or a tiled batch (> 3 queries)");
+        *tab_bytes = nq ? 0 : (size_t)kPlaneDwords * kTemplateTabStride * 4;
+        *frag_bytes = nq ? (size_t)(nq + 3) / 4 * 4 * 16 * kPlaneGroups * 64 : kTemplateFragDwords * 4;
+        return 0;
+    case IRIS_KIND_MASKS:
+        *tab_bytes = (size_t)kPlaneDwords * kSlotTabStride * 4;
+        *frag_bytes = kMaskFragBytes;
+        return 0;
+    case IRIS_KIND_SHARES:
+        *tab_bytes = (size_t)kShareDwords * kSlotTabStride * 4;
+        *frag_bytes = kShareFragBytes;
+        return 0;
+    default: return fail(IRIS_E_ARG, "unknown record kind");
+    }
+}
+
+int iris_engine_query_tables(const iris_engine_t *e, void *tab, size_t tab_bytes, void *frag, size_t frag_bytes) {
+    ARG(e, "engine is NULL");
+    ARG(e->sub.empty(), "a streamed batch engine (<= 3 queries) holds one engine per query");
+    size_t tb = 0, fb = 0;
+    CHK(iris_query_table_sizes(e->kind, e->nq, &tb, &fb));
+    ARG(tab_bytes == tb && frag_bytes == fb, "table sizes do not match the engine's layout");
+    ARG((tb == 0 || tab) && frag, "NULL argument");
+    iris_device *d = e->dev;
+    std::lock_guard<std::recursive_mutex> g(d->mu);
+    CHK(set_device(d));
+    if (tb) HIPCHK(hipMemcpyAsync(tab, e->qtab, tb, hipMemcpyDeviceToHost, d->stream));
+    HIPCHK(hipMemcpyAsync(frag, e->qfrag, fb, hipMemcpyDeviceToHost, d->stream));
+    return sync(d);
+}
+
+int iris_host_query_tables(int kind, const void *query, uint32_t nq, void *tab, size_t tab_bytes, void *frag,
+                           size_t frag_bytes) {
+    ARG(query, "query is NULL");
+    size_t tb = 0, fb = 0;
+    CHK(iris_query_table_sizes(kind, nq, &tb, &fb));
+    ARG(tab_bytes == tb && frag_bytes == fb, "table sizes do not match the layout");
+    ARG((tb == 0 || tab) && frag, "NULL argument");
+    if (kind == IRIS_KIND_TEMPLATES && nq) {
+        const size_t tile_dw = (size_t)4 * kPlaneGroups * 64;
+        memset(frag, 0, fb);
+        for (uint32_t i = 0; i < nq; ++i)
+            build_query_tile((const iris_template_t *)query + i, (uint32_t *)frag + i * tile_dw);
+    } else if (kind == IRIS_KIND_TEMPLATES) {
+        build_template_table((const iris_template_t *)query, (uint32_t *)tab);
+        build_template_frags((const iris_template_t *)query, (uint32_t *)frag);
+    } else if (kind == IRIS_KIND_MASKS) {
+        build_masks_rotations((const uint64_t *)query, (uint32_t *)tab);
+        std::vector<uint64_t> rot((size_t)kRot * IRIS_LIMBS);
+        const uint64_t *ptrs[kRot];
+        for (int k = 0; k < kRot; ++k) {
+            bits_rotated((const uint64_t *)query, k - 15, &rot[(size_t)k * IRIS_LIMBS]);
+            ptrs[k] = &rot[(size_t)k * IRIS_LIMBS];
+        }
+        build_masks_frags(ptrs, kRot, (uint32_t *)frag);
+    } else {
+        build_shares_rotations((const uint16_t *)query, (uint32_t *)tab);
+        std::vector<uint16_t> rot((size_t)kRot * IRIS_BITS);
+        const uint16_t *ptrs[kRot];
+        for (int k = 0; k < kRot; ++k) {
+            encoded_rotated((const uint16_t *)query, k - 15, &rot[(size_t)k * IRIS_BITS]);
+            ptrs[k] = &rot[(size_t)k * IRIS_BITS];
+        }
+        build_shares_frags(ptrs, kRot, (uint32_t *)frag);
+    }
     return 0;
 }
 

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <map>
 #include <mutex>
 #include <string>
@@ -66,6 +67,12 @@ struct iris_device {
     std::vector<Pending> pending;
     std::vector<hipEvent_t> event_pool;
     DevBuf partials, result, staging, out_a, out_b;
+    // handles alive on this device (1 for the device handle itself + 1 per database
+    // and engine handle): the device is torn down when the last one is released,
+    // so handles may be destroyed in any order
+    std::atomic<int> refs{1};
+    // freed engines' query buffers, reused by later engines (stream-ordered)
+    std::vector<std::pair<size_t, void *>> qpool;
 };
 
 struct iris_db {
@@ -78,8 +85,10 @@ struct iris_db {
 struct iris_engine {
     iris_device *dev = nullptr;
     int kind = 0;             // IRIS_KIND_* of the DB it runs against
+    void *qbuf = nullptr;     // one device allocation holding qtab, qfrag and the query
+    size_t qbuf_bytes = 0;
     void *qtab = nullptr;     // SGPR rotated-query table (LANES kernels)
-    void *qfrag = nullptr;    // fp4 query fragments (TILES kernel, templates only)
+    void *qfrag = nullptr;    // MFMA query fragments (TILES kernels)
     uint32_t nq = 0;          // > 0: batched template engine (qfrag = nq padded query tiles)
     std::vector<iris_engine *> sub;  // streaming batched engine: one single-query engine per query
 };

@@ -129,7 +129,8 @@ constexpr size_t kShareFragUint4 = (size_t)kShareChunks * 64 * 2;  // + 32 int2 
 IRIS_HD inline int mask_frag_bit(int j) { return 4 * (j & 7) + (j >> 3); }
 constexpr size_t kTemplateFragDwords = (size_t)(kPlaneDwords / 2) * 64 * kFragDwords;  // 200 chunks
 
-// Rotated-query tables (built on the host, uploaded once per engine):
+// Rotated-query tables (built once per engine, on the device by iris_query.hip;
+// the host builders below are their reference):
 //   TEMPLATES: dword [w*64 + 2k] = mask_k word w, [w*64 + 2k+1] = pattern_k word w   (400 x 64)
 //   MASKS:     dword [w*32 + k]  = mask_k word w                                      (400 x 32)
 //   SHARES:    dword [d*32 + k]  = rot_k[2d] | rot_k[2d+1] << 16                       (6400 x 32)
@@ -171,6 +172,11 @@ struct LaunchRange {
 };
 
 int launch_pack(void *stream, const KindInfo &k, const void *staging, void *db, uint64_t t_first, uint64_t n);
+// per-engine query tables built on the device from the query (iris_query.hip)
+int launch_query_template(void *stream, const void *q, uint32_t *tab, uint32_t *frag);
+int launch_query_masks(void *stream, const void *qmask, uint32_t *tab, uint32_t *frag);
+int launch_query_shares(void *stream, const void *q, uint32_t *tab, uint32_t *frag);
+int launch_query_tiles(void *stream, const void *queries, uint32_t nq, uint32_t nqp, uint32_t *tiles);
 int launch_prepare_shares(void *stream, const void *templates, uint64_t m, uint64_t g0, const uint8_t key[32],
                           uint64_t nonce, uint32_t parties, void *shares);
 constexpr int kMaxPrepParties = 64;

@@ -128,6 +128,11 @@ def load_library(path=None):
             "iris_encode": ([P, P], ctypes.c_int),
             "iris_decode_distance": ([P, P, ctypes.POINTER(ctypes.c_double)], ctypes.c_int),
             "iris_match_merge": ([ctypes.POINTER(Match), u64, ctypes.POINTER(Match)], ctypes.c_int),
+            "iris_query_table_sizes": ([ctypes.c_int, ctypes.c_uint32, ctypes.POINTER(ctypes.c_size_t),
+                                        ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
+            "iris_engine_query_tables": ([P, P, ctypes.c_size_t, P, ctypes.c_size_t], ctypes.c_int),
+            "iris_host_query_tables": ([ctypes.c_int, P, ctypes.c_uint32, P, ctypes.c_size_t, P, ctypes.c_size_t],
+                                       ctypes.c_int),
         }
         for name, (args, res) in sig.items():
             f = getattr(lib, name)
@@ -153,7 +158,26 @@ def exported_symbols():
         "iris_decode_distance", "iris_match_merge", "iris_db_load_file", "iris_db_save_file",
         "iris_templates_read_json", "iris_templates_write_json", "iris_prepare_shares",
         "iris_db_truncate", "iris_memcpy_h2d", "iris_resolver_search_masks",
+        "iris_query_table_sizes", "iris_engine_query_tables", "iris_host_query_tables",
     ]
+
+
+def query_table_sizes(kind, nq=0):
+    """(table bytes, fragment bytes) of an engine's rotated-query tables."""
+    tb, fb = ctypes.c_size_t(), ctypes.c_size_t()
+    _check(load_library().iris_query_table_sizes(int(kind), int(nq), ctypes.byref(tb), ctypes.byref(fb)))
+    return tb.value, fb.value
+
+
+def host_query_tables(kind, query, nq=0):
+    """The rotated-query table and MFMA fragments of `query` built by the host reference
+    builders (CPU only) -> (table uint8 array, fragments uint8 array)."""
+    tb, fb = query_table_sizes(kind, nq)
+    q = np.ascontiguousarray(query)
+    tab, frag = np.zeros(tb, np.uint8), np.zeros(fb, np.uint8)
+    _check(load_library().iris_host_query_tables(int(kind), _ptr(q), int(nq), _ptr(tab) if tb else None, tb,
+                                                 _ptr(frag), fb))
+    return tab, frag
 
 
 def read_templates_json(path):
@@ -590,6 +614,14 @@ class _Engine:
             self.close()
         except Exception:
             pass
+
+    def query_tables(self):
+        """The engine's device-built rotated-query table and MFMA fragments, copied to
+        the host -> (table uint8 array, fragments uint8 array)."""
+        tb, fb = query_table_sizes(self.kind, getattr(self, "nq", 0))
+        tab, frag = np.zeros(tb, np.uint8), np.zeros(fb, np.uint8)
+        _check(load_library().iris_engine_query_tables(self.handle, _ptr(tab) if tb else None, tb, _ptr(frag), fb))
+        return tab, frag
 
     def batch_process(self, out, db, first=0, n=None):
         """batch_process(&self, out: &mut [[u16;31]], db: &[T]) (src/lib.rs:42-52, 69-79).
