@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--n-per-gpu", type=int, default=None,
                     help="records per GPU (default 10M; search with 2+ ranks: 12.5M, so 8 ranks are configs[4]'s 100M)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--reuse-engine", action="store_true",
+                    help="build the query engine once instead of once per step (default: per step, in the timed region)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--layout", choices=["tiles", "lanes"], default="tiles",
                     help="tiles = MFMA kernels (default), lanes = VALU kernels")
@@ -381,18 +383,27 @@ def main():
     if args.workload in ("search", "batch"):
         if lo <= plant_global < lo + n:
             db.write(plant_global - lo, planted_record(query, plant_rot)[None, :])
-    if args.workload == "search":
-        eng = ih.TemplateEngine(dev, query)
-    elif args.workload == "batch":
+    if args.workload == "batch":
         batch_q = gen_records(dev, ih.KIND_TEMPLATES, nq, SEED + 2)
         batch_q[nq // 2] = query  # its best match is the planted record
-        eng = ih.TemplateBatchEngine(dev, batch_q)
-    elif args.workload == "masks":
-        eng = ih.MasksEngine(dev, query[200:])
+    if args.workload in ("masks", "shares"):
         out_dev = dev.alloc(n * ROT * 2)
-    else:
-        eng = ih.DistanceEngine(dev, ih.encode(ih.Template.from_array(query)))
-        out_dev = dev.alloc(n * ROT * 2)
+    share_query = ih.encode(ih.Template.from_array(query)) if args.workload == "shares" else None
+
+    def new_engine():
+        """The query's engine: its 31 rotations in the kernels' layouts, built on the device
+        (DistanceEngine::new / MasksEngine::new, src/lib.rs:33-40, 60-67)."""
+        if args.workload == "search":
+            return ih.TemplateEngine(dev, query)
+        if args.workload == "batch":
+            return ih.TemplateBatchEngine(dev, batch_q)
+        if args.workload == "masks":
+            return ih.MasksEngine(dev, query[200:])
+        return ih.DistanceEngine(dev, share_query)
+
+    # by default every step prepares its query's engine and frees it again, as the reference's
+    # participant does per request (src/main.rs:427-431); --reuse-engine keeps one engine
+    eng = new_engine() if args.reuse_engine else None
 
     def sync_all():
         if dist is not None:
@@ -405,18 +416,23 @@ def main():
             dev.synchronize()
 
     def step():
-        if args.workload == "batch":
-            ms = eng.search(db, index_base=lo)
+        e = eng if eng is not None else new_engine()
+        try:
+            if args.workload == "batch":
+                ms = e.search(db, index_base=lo)
+                if dist is not None:
+                    ms = [iris_dist.allgather_merge(x, device=xdev) for x in ms]
+                return ms
+            if args.workload != "search":
+                e.batch_process_device(db, out_dev)  # [n][31] u16 left in HBM
+                return None
+            m = e.search(db, index_base=lo)
             if dist is not None:
-                ms = [iris_dist.allgather_merge(x, device=xdev) for x in ms]
-            return ms
-        if args.workload != "search":
-            eng.batch_process_device(db, out_dev)  # [n][31] u16 left in HBM
-            return None
-        m = eng.search(db, index_base=lo)
-        if dist is not None:
-            m = iris_dist.allgather_merge(m, device=xdev)
-        return m
+                m = iris_dist.allgather_merge(m, device=xdev)
+            return m
+        finally:
+            if eng is None:
+                e.close()
 
     for _ in range(args.warmup):
         m = step()
@@ -495,6 +511,7 @@ def main():
                 }[args.workload],
                 "templates_per_gpu": n, "total_templates": total, "queries": nq, "rotations": ROT,
                 "bytes_per_template": rec_bytes, "parallelism": f"db-shard x{world}", "layout": args.layout,
+                "engine_per_step": not args.reuse_engine,
             },
             "roofline": ({
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -531,7 +548,8 @@ def main():
         print(json.dumps(line))
     if out_dev is not None:
         dev.free(out_dev)
-    eng.close()
+    if eng is not None:
+        eng.close()
     db.close()
     dev.close()
     if dist is not None:
