@@ -6,10 +6,10 @@
 // 1024 queries x 10M templates, so it is tiled like a GEMM:
 //
 //   workgroup (8 waves) = 4 queries x 8 template tiles (256 templates)
-//   wave w              = query (w & 3) x tiles 4 (w >> 2) .. +3  (128 f32 acc)
-//   K-step              = 4 chunks of 64 bits, double-buffered in LDS:
-//                         A 4 queries x 4 chunks x 64 lanes x 8 B  (8 KB)
-//                         B 8 tiles   x 4 chunks x 64 lanes x 8 B  (16 KB)
+//   wave w              = 2 queries x 2 tiles (128 f32 accumulators)
+//   K-step              = 10 chunks of 64 bits, double-buffered in LDS:
+//                         A 4 queries x 10 chunks x 64 lanes x 8 B  (20 KB)
+//                         B 8 tiles   x 10 chunks x 64 lanes x 8 B  (40 KB)
 //
 // A (queries) is stored like a template tile: the 31 rotated copies of a query
 // packed with xpack (iris_internal.hpp) as records 0..30 of a TILES tile, so
@@ -43,8 +43,13 @@ constexpr int WQ = IRIS_BATCH_WQ;         // queries per wave
 constexpr int WT = IRIS_BATCH_WT;         // tiles per wave (WQ x WT accumulator pairs)
 constexpr int kQW = BQ / WQ;              // waves per tile set
 constexpr int BT = (NW / kQW) * WT;       // template tiles per N-group
-constexpr int KSTEP = 4;                  // chunks per K-step
-constexpr int NSTEPS = kPlaneDwords / 2 / KSTEP;  // 50
+#ifndef IRIS_BATCH_KSTEP
+#define IRIS_BATCH_KSTEP 10
+#endif
+constexpr int KSTEP = IRIS_BATCH_KSTEP;   // chunks per K-step
+constexpr int GP = KSTEP / 2;             // 1-KB chunk-pair rows per operand per K-step
+constexpr int NSTEPS = kPlaneDwords / 2 / KSTEP;  // 20
+static_assert(NSTEPS * KSTEP * 2 == kPlaneDwords && KSTEP % 2 == 0, "K-steps must tile the 200 chunks");
 constexpr int kTileU4 = kPlaneGroups * 64;        // 6400 uint4 per tile
 
 __device__ __forceinline__ v16f mfma4(const v8i &a, const v8i &b, const v16f &c) {
@@ -54,15 +59,22 @@ __device__ __forceinline__ v16f mfma4(const v8i &a, const v8i &b, const v16f &c)
 // s_waitcnt with only the vector-memory count bounded (expcnt, lgkmcnt at max)
 #define VMCNT(n) __builtin_amdgcn_s_waitcnt(0x0F70 | ((n) & 15) | (((n) >> 4) << 14))
 
-constexpr int kRows = 2 * (BQ + BT);  // 1-KB rows per stage: 4 queries + 8 tiles, 2 chunk pairs each
-constexpr int kRing = 4;              // LDS stages: 3 in flight + the one being read
+constexpr int kRows = GP * (BQ + BT);  // 1-KB rows per stage: 4 queries + 8 tiles, GP chunk pairs each
+#ifndef IRIS_BATCH_RING
+#define IRIS_BATCH_RING 2
+#endif
+constexpr int kRing = IRIS_BATCH_RING;  // LDS stages: kRing - 1 in flight + the one being read
+constexpr int kAhead = kRing - 1;
+static_assert(kAhead >= 1 && kAhead <= 3, "ring of 2..4 stages");
 constexpr int kRowsPerWave = (kRows + NW - 1) / NW;  // waves w < kRows - NW (kRowsPerWave - 1) issue one more
 constexpr bool kEvenRows = kRows % NW == 0;
 
 // Staging is LDS-DMA (global_load_lds_dwordx4, lane-linear 1-KB rows) into a
-// 4-stage ring: each K-step waits for its own rows with a counted vmcnt (the
-// next two steps stay in flight across the raw s_barrier), then issues the
-// step three ahead into the slot everyone finished reading a step ago.
+// ring of kRing stages: each K-step waits for its own rows with a counted
+// vmcnt (later steps stay in flight across the raw s_barrier), then issues the
+// step kRing - 1 ahead into the slot everyone finished reading a step ago.
+// Default: two stages of 10-chunk steps (120 KB) — fewer barriers per chunk
+// than 4-stage rings of 4-chunk steps (measured 2 % faster at 4..1024 queries).
 // Each workgroup walks its N-groups as one flat stream of K-steps, so the
 // pipeline never drains between N-groups.
 __global__ void __launch_bounds__(64 * NW, NW <= 8 ? 8 / NW : 1)
@@ -83,10 +95,10 @@ __global__ void __launch_bounds__(64 * NW, NW <= 8 ? 8 / NW : 1)
 #pragma unroll
     for (int i = 0; i < kRowsPerWave; ++i) {
         const int r = w + NW * i;
-        row_t[i] = r < 2 * BQ ? -1 : (r - 2 * BQ) >> 1;
-        const int gp = r & 1;
-        src_q[i] = r < 2 * BQ ? qtiles + (uint64_t)(qg * BQ + (r >> 1)) * kTileU4 + gp * 64 + lane
-                              : db + gp * 64 + lane;
+        row_t[i] = r < GP * BQ ? -1 : (r - GP * BQ) / GP;
+        const int gp = r % GP;
+        src_q[i] = r < GP * BQ ? qtiles + (uint64_t)(qg * BQ + r / GP) * kTileU4 + gp * 64 + lane
+                               : db + gp * 64 + lane;
     }
     auto issue = [&](uint32_t s) {
         const uint32_t j = s / NSTEPS, k = s - j * NSTEPS;
@@ -97,10 +109,10 @@ __global__ void __launch_bounds__(64 * NW, NW <= 8 ? 8 / NW : 1)
             if (!kEvenRows && r >= kRows) break;  // wave-uniform
             const uint4 *src;
             if (row_t[i] < 0) {
-                src = src_q[i] + (2 * k) * 64;
+                src = src_q[i] + (GP * k) * 64;
             } else {
                 const uint64_t trel = ng * BT + row_t[i];
-                src = src_q[i] + (tile0 + (trel < ntiles ? trel : ntiles - 1)) * (uint64_t)kTileU4 + (2 * k) * 64;
+                src = src_q[i] + (tile0 + (trel < ntiles ? trel : ntiles - 1)) * (uint64_t)kTileU4 + (GP * k) * 64;
             }
             // LDS-DMA in inline asm: hipcc's waitcnt pass would otherwise wait vmcnt(0)
             // before every ds_read of the ring; the counted VMCNT waits below own these
@@ -136,7 +148,7 @@ __global__ void __launch_bounds__(64 * NW, NW <= 8 ? 8 / NW : 1)
                 }
     };
     zero();
-    for (uint32_t s = 0; s < 3 && s < total; ++s) issue(s);
+    for (uint32_t s = 0; s < (uint32_t)kAhead && s < total; ++s) issue(s);
     // static priority for the second-dispatched half of the workgroup, the loser of VALU
     // arbitration against its SIMD partner (MI355X_MICROARCH.md, two waves per SIMD, item 4):
     // 3.37 -> 3.24 s on 1024 x 10M, same box
@@ -146,23 +158,24 @@ __global__ void __launch_bounds__(64 * NW, NW <= 8 ? 8 / NW : 1)
     for (uint32_t s = 0; s < total; ++s) {
         // wait for this step's rows (this wave's), then for everyone's
         const bool more = kEvenRows || w + NW * (kRowsPerWave - 1) < kRows;  // this wave's rows per step
-        if (s + 2 < total) {
+        const uint32_t younger = min((uint32_t)(kAhead - 1), total - 1 - s);  // later steps still in flight
+        if (kAhead >= 3 && younger >= 2) {
             if (more) VMCNT(2 * kRowsPerWave); else VMCNT(2 * (kRowsPerWave - 1));
-        } else if (s + 1 < total) {
+        } else if (kAhead >= 2 && younger >= 1) {
             if (more) VMCNT(kRowsPerWave); else VMCNT(kRowsPerWave - 1);
         } else {
             VMCNT(0);
         }
         __builtin_amdgcn_s_barrier();
-        if (s + 3 < total) issue(s + 3);
+        if (s + kAhead < total) issue(s + kAhead);
         const uint4(*st)[64] = ring[s % kRing];
 #pragma unroll
-        for (int gp = 0; gp < 2; ++gp) {
+        for (int gp = 0; gp < GP; ++gp) {
             uint4 a4[WQ], b4[WT];
 #pragma unroll
-            for (int qi = 0; qi < WQ; ++qi) a4[qi] = st[2 * (wq0 + qi) + gp][lane];
+            for (int qi = 0; qi < WQ; ++qi) a4[qi] = st[GP * (wq0 + qi) + gp][lane];
 #pragma unroll
-            for (int t = 0; t < WT; ++t) b4[t] = st[2 * BQ + 2 * (wsub + t) + gp][lane];
+            for (int t = 0; t < WT; ++t) b4[t] = st[GP * BQ + GP * (wsub + t) + gp][lane];
 #pragma unroll
             for (int h2 = 0; h2 < 2; ++h2) {
                 v8i aden[WQ], aenc[WQ];
