@@ -52,8 +52,22 @@ constexpr int NSTEPS = kPlaneDwords / 2 / KSTEP;  // 20
 static_assert(NSTEPS * KSTEP * 2 == kPlaneDwords && KSTEP % 2 == 0, "K-steps must tile the 200 chunks");
 constexpr int kTileU4 = kPlaneGroups * 64;        // 6400 uint4 per tile
 
+// Diagnostic builds (tools/, never the shipped library): IRIS_BATCH_DIAG = 1 drops the
+// MFMAs (a VALU fold keeps the operands live), 2 drops the LDS-DMA staging (the
+// ring's stale contents are computed on), 3 feeds the raw staged words to the
+// MFMAs without the fp4 expansion, 4 stages every row from the first query group
+// and N-group (L2-hot), 5 drops the per-K-step s_barrier.  Results are wrong by design.
+#ifndef IRIS_BATCH_DIAG
+#define IRIS_BATCH_DIAG 0
+#endif
 __device__ __forceinline__ v16f mfma4(const v8i &a, const v8i &b, const v16f &c) {
+#if IRIS_BATCH_DIAG == 1
+    v16f r = c;
+    r[0] += __builtin_bit_cast(float, (a[0] ^ b[1]) & 1);
+    return r;
+#else
     return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, c, 4, 4, 0, 127, 0, 127);
+#endif
 }
 
 // s_waitcnt with only the vector-memory count bounded (expcnt, lgkmcnt at max)
@@ -108,7 +122,9 @@ __global__ void __launch_bounds__(64 * NW, NW <= 8 ? 8 / NW : 1)
             const int r = w + NW * i;
             if (!kEvenRows && r >= kRows) break;  // wave-uniform
             const uint4 *src;
-            if (row_t[i] < 0) {
+            if (IRIS_BATCH_DIAG == 4) {  // every row from the first query group / N-group: L2-hot
+                src = row_t[i] < 0 ? src_q[i] - (uint64_t)(qg * BQ) * kTileU4 : src_q[i] + (tile0 + row_t[i]) * (uint64_t)kTileU4;
+            } else if (row_t[i] < 0) {
                 src = src_q[i] + (GP * k) * 64;
             } else {
                 const uint64_t trel = ng * BT + row_t[i];
@@ -118,6 +134,7 @@ __global__ void __launch_bounds__(64 * NW, NW <= 8 ? 8 / NW : 1)
             // before every ds_read of the ring; the counted VMCNT waits below own these
             const uint32_t dst = __builtin_amdgcn_readfirstlane(
                 (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void *)&ring[s % kRing][r][0]);
+            if (IRIS_BATCH_DIAG == 2) continue;
             uint32_t keep;
             asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                          : "=&s"(keep)
@@ -166,7 +183,7 @@ __global__ void __launch_bounds__(64 * NW, NW <= 8 ? 8 / NW : 1)
         } else {
             VMCNT(0);
         }
-        __builtin_amdgcn_s_barrier();
+        if (IRIS_BATCH_DIAG != 5) __builtin_amdgcn_s_barrier();
         if (s + kAhead < total) issue(s + kAhead);
         const uint4(*st)[64] = ring[s % kRing];
 #pragma unroll
@@ -182,18 +199,28 @@ __global__ void __launch_bounds__(64 * NW, NW <= 8 ? 8 / NW : 1)
 #pragma unroll
                 for (int qi = 0; qi < WQ; ++qi) {
                     const uint32_t ax = h2 ? a4[qi].z : a4[qi].x, ay = h2 ? a4[qi].w : a4[qi].y;
+#if IRIS_BATCH_DIAG == 3
+                    aden[qi] = v8i{(int)ax, (int)ay, (int)ax, (int)ay, 0, 0, 0, 0};
+                    aenc[qi] = v8i{(int)ay, (int)ax, (int)ay, (int)ax, 0, 0, 0, 0};
+#else
                     aden[qi] = v8i{(int)(ax & 0x22222222u), (int)((ax & 0x11111111u) << 2), (int)(ay & 0x22222222u),
                                    (int)((ay & 0x11111111u) << 2), 0, 0, 0, 0};
                     aenc[qi] = v8i{(int)(ax & 0xAAAAAAAAu), (int)((ax << 1) & 0xAAAAAAAAu), (int)(ay & 0xAAAAAAAAu),
                                    (int)((ay << 1) & 0xAAAAAAAAu), 0, 0, 0, 0};
+#endif
                 }
 #pragma unroll
                 for (int t = 0; t < WT; ++t) {
                     const uint32_t bx = h2 ? b4[t].z : b4[t].x, by = h2 ? b4[t].w : b4[t].y;
+#if IRIS_BATCH_DIAG == 3
+                    const v8i bden = {(int)bx, (int)by, (int)bx, (int)by, 0, 0, 0, 0};
+                    const v8i benc = {(int)by, (int)bx, (int)by, (int)bx, 0, 0, 0, 0};
+#else
                     const v8i bden = {(int)(bx & 0x22222222u), (int)(bx & 0x11111111u), (int)(by & 0x22222222u),
                                       (int)(by & 0x11111111u), 0, 0, 0, 0};
                     const v8i benc = {(int)(bx & 0xAAAAAAAAu), (int)((bx << 1) & 0xAAAAAAAAu),
                                       (int)(by & 0xAAAAAAAAu), (int)((by << 1) & 0xAAAAAAAAu), 0, 0, 0, 0};
+#endif
 #pragma unroll
                     for (int qi = 0; qi < WQ; ++qi) {
                         den[qi][t] = mfma4(aden[qi], bden, den[qi][t]);
