@@ -310,7 +310,13 @@ def run_aux(args, dev):
                    "host-masks": "mask records/s through batch_process over host slices (PCIe-inclusive)"}[args.workload],
         "value": n * args.steps / elapsed, "unit": unit, "n_gpus": 1, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "u16",
+        "scaling": "weak", "vs_baseline": None,
+        "dtype": {"resolver": "u16 (wrapping share sums) -> u32 cross-multiplied fractions",
+                  "resolve-masks": "fp4 e2m1 MFMA -> f32 denominators, u16 share sums",
+                  "prepare": "u32 (ChaCha20 keystream) -> u16 shares",
+                  "load": "u8 (record bytes)",
+                  "host-shares": "i8 MFMA -> i32 (u16 shares as biased byte planes)",
+                  "host-masks": "fp4 e2m1 MFMA -> f32 (0/1 products)"}[args.workload],
         "data": "synthetic (uniform random u16 / on-device generated templates)",
         "config": {"workload": workload, "records_per_gpu": n, "parties": P},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -500,7 +506,11 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "u32",
+            # the arithmetic the kernel computes in; every sum is an exact integer either way
+            "dtype": {("shares", "tiles"): "i8 MFMA -> i32 (u16 shares as biased byte planes)",
+                      ("shares", "lanes"): "u16 (v_pk_mad_u16)"}.get(
+                          (args.workload, args.layout),
+                          "fp4 e2m1 MFMA -> f32 (0/+-1 products)" if args.layout == "tiles" else "u32 (VALU popcount)"),
             "data": "synthetic (on-device counter-based generator, uniform random pattern+mask bits; planted known answer)",
             "config": {
                 "workload": {
