@@ -195,6 +195,7 @@ void device_teardown(iris_device *d) {
         (void)hipStreamSynchronize(d->stream);
         for (DevBuf *b : {&d->partials, &d->result, &d->staging, &d->out_a, &d->out_b})
             if (b->p) (void)hipFree(b->p);
+        if (d->host_result) (void)hipHostFree(d->host_result);
         for (auto &q : d->qpool) (void)hipFree(q.second);
         d->qpool.clear();
         for (auto &p : d->pending) {
@@ -639,7 +640,7 @@ static int search_locked(iris_engine_t *e, const iris_db_t *db, uint64_t first, 
     const bool tiles = db->k.layout == IRIS_LAYOUT_TILES;
     const uint32_t np = tiles ? mfma_search_partials(r) : search_partials(r);
     CHK(ensure(d->partials, (size_t)std::max<uint32_t>(np, 1) * sizeof(Partial)));
-    CHK(ensure(d->result, sizeof(Partial)));
+    CHK(ensure_host_result(d, sizeof(Partial)));
     uint32_t written = 0;
     CHK(timed(d, "template_search", n, [&] {
         return tiles ? launch_template_mfma_search(d->stream, db->data, e->qfrag, r, dist_dev, (Partial *)d->partials.p, &written)
@@ -647,10 +648,11 @@ static int search_locked(iris_engine_t *e, const iris_db_t *db, uint64_t first, 
     }));
     Partial res{};
     if (n > 0) {
-        CHK(timed(d, "reduce", written, [&] { return launch_reduce(d->stream, (Partial *)d->partials.p, written, (Partial *)d->result.p); }));
-        HIPCHK(hipMemcpyAsync(&res, d->result.p, sizeof(Partial), hipMemcpyDeviceToHost, d->stream));
+        // the reduce writes the winner straight into pinned host memory: no copy before the sync
+        CHK(timed(d, "reduce", written, [&] { return launch_reduce(d->stream, (Partial *)d->partials.p, written, (Partial *)d->host_result); }));
     }
     CHK(sync(d));
+    if (n > 0) memcpy(&res, d->host_result, sizeof(Partial));
     if (out) {
         if (n == 0 || res.den == 0) {
             out->distance = INFINITY;
@@ -681,7 +683,7 @@ static int pair_search_locked(iris_engine_t *a, iris_engine_t *b, const iris_db_
     LaunchRange r{first, n};
     const uint32_t np = multi_search_partials(r, 2);
     CHK(ensure(d->partials, (size_t)std::max<uint32_t>(2 * np, 1) * sizeof(Partial)));
-    CHK(ensure(d->result, 2 * sizeof(Partial)));
+    CHK(ensure_host_result(d, 2 * sizeof(Partial)));
     const void *qf[2] = {a->qfrag, b->qfrag};
     uint32_t written = 0;
     CHK(timed(d, "template_batch", 2 * n, [&] {
@@ -692,11 +694,11 @@ static int pair_search_locked(iris_engine_t *a, iris_engine_t *b, const iris_db_
         for (int q = 0; q < 2; ++q)
             CHK(timed(d, "reduce", written, [&] {
                 return launch_reduce(d->stream, (Partial *)d->partials.p + (size_t)q * written, written,
-                                     (Partial *)d->result.p + q);
+                                     (Partial *)d->host_result + q);
             }));
-        HIPCHK(hipMemcpyAsync(res, d->result.p, 2 * sizeof(Partial), hipMemcpyDeviceToHost, d->stream));
     }
     CHK(sync(d));
+    if (n > 0) memcpy(res, d->host_result, 2 * sizeof(Partial));
     for (int q = 0; q < 2; ++q) {
         iris_match_t &m = out[q];
         if (n == 0 || res[q].den == 0) {
@@ -807,13 +809,14 @@ int iris_template_batch_search(iris_engine_t *e, const iris_db_t *db, uint64_t f
     std::vector<Partial> res(nqp);
     if (n > 0) {
         CHK(ensure(d->partials, (size_t)nqp * geo.G * sizeof(Partial)));
-        CHK(ensure(d->result, (size_t)nqp * sizeof(Partial)));
+        CHK(ensure_host_result(d, (size_t)nqp * sizeof(Partial)));
         CHK(timed(d, "template_batch", n * e->nq, [&] {
-            return launch_batch(d->stream, db->data, e->qfrag, r, geo, (Partial *)d->partials.p, (Partial *)d->result.p);
+            return launch_batch(d->stream, db->data, e->qfrag, r, geo, (Partial *)d->partials.p,
+                                (Partial *)d->host_result);
         }));
-        HIPCHK(hipMemcpyAsync(res.data(), d->result.p, nqp * sizeof(Partial), hipMemcpyDeviceToHost, d->stream));
     }
     CHK(sync(d));
+    if (n > 0) memcpy(res.data(), d->host_result, nqp * sizeof(Partial));
     for (uint32_t q = 0; q < e->nq; ++q) {
         const Partial &p = res[q];
         iris_match_t &m = out[q];
@@ -839,10 +842,12 @@ int iris_template_batch_search(iris_engine_t *e, const iris_db_t *db, uint64_t f
 
 static int resolver_finish(iris_device *d, uint32_t np, Partial *res) {
     if (np) {
-        CHK(timed(d, "reduce", np, [&] { return launch_reduce(d->stream, (Partial *)d->partials.p, np, (Partial *)d->result.p); }));
-        HIPCHK(hipMemcpyAsync(res, d->result.p, sizeof(Partial), hipMemcpyDeviceToHost, d->stream));
+        CHK(ensure_host_result(d, sizeof(Partial)));
+        CHK(timed(d, "reduce", np, [&] { return launch_reduce(d->stream, (Partial *)d->partials.p, np, (Partial *)d->host_result); }));
     }
-    return sync(d);
+    CHK(sync(d));
+    if (np) memcpy(res, d->host_result, sizeof(Partial));
+    return 0;
 }
 
 static void match_from(const Partial &r, bool any, uint64_t base, iris_match_t *out) {
@@ -874,7 +879,6 @@ int iris_resolver_search(iris_device_t *d, const uint16_t *const *shares, uint32
     CHK(set_device(d));
     const uint32_t np = resolver_partials(n);
     CHK(ensure(d->partials, (size_t)std::max<uint32_t>(np, 1) * sizeof(Partial)));
-    CHK(ensure(d->result, sizeof(Partial)));
     CHK(timed(d, "resolver", n, [&] {
         return launch_resolver(d->stream, shares, parts, denoms, n, dist_out_device, (Partial *)d->partials.p);
     }));
@@ -906,7 +910,6 @@ int iris_resolver_search_masks(iris_engine_t *e, const iris_db_t *db, uint64_t f
     if (db->k.layout == IRIS_LAYOUT_TILES) {
         const uint32_t np = n ? masks_resolve_partials(r) : 0;
         CHK(ensure(d->partials, (size_t)std::max<uint32_t>(np, 1) * sizeof(Partial)));
-        CHK(ensure(d->result, sizeof(Partial)));
         CHK(timed(d, "masks_resolve", n, [&] {
             return launch_masks_resolve(d->stream, db->data, e->qfrag, r, shares_device, parts, dist_out_device,
                                         (Partial *)d->partials.p);
@@ -917,7 +920,6 @@ int iris_resolver_search_masks(iris_engine_t *e, const iris_db_t *db, uint64_t f
         CHK(timed(d, "masks", n, [&] { return launch_masks(d->stream, db->data, e->qtab, r, (uint16_t *)d->out_a.p); }));
         const uint32_t np = resolver_partials(n);
         CHK(ensure(d->partials, (size_t)std::max<uint32_t>(np, 1) * sizeof(Partial)));
-        CHK(ensure(d->result, sizeof(Partial)));
         CHK(timed(d, "resolver", n, [&] {
             return launch_resolver(d->stream, shares_device, parts, (const uint16_t *)d->out_a.p, n, dist_out_device,
                                    (Partial *)d->partials.p);

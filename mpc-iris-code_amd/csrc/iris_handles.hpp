@@ -67,6 +67,10 @@ struct iris_device {
     std::vector<Pending> pending;
     std::vector<hipEvent_t> event_pool;
     DevBuf partials, result, staging, out_a, out_b;
+    // pinned host words the reduce kernels write their final Partials into (no
+    // device-to-host copy between the last kernel and the stream sync)
+    void *host_result = nullptr;
+    size_t host_result_cap = 0;
     // handles alive on this device (1 for the device handle itself + 1 per database
     // and engine handle): the device is torn down when the last one is released,
     // so handles may be destroyed in any order
@@ -116,6 +120,19 @@ inline int ensure(DevBuf &b, size_t bytes) {
     hipError_t e = hipMalloc(&b.p, want);
     if (e != hipSuccess) return fail(IRIS_E_NOMEM, std::string("hipMalloc workspace: ") + hipGetErrorString(e));
     b.cap = want;
+    return 0;
+}
+
+// `bytes` of pinned, device-visible host memory for final results (grown on demand).
+inline int ensure_host_result(iris_device *d, size_t bytes) {
+    if (bytes <= d->host_result_cap) return 0;
+    if (d->host_result) HIPCHK(hipHostFree(d->host_result));
+    d->host_result = nullptr;
+    d->host_result_cap = 0;
+    const size_t want = std::max(bytes, (size_t)4096);
+    hipError_t e = hipHostMalloc(&d->host_result, want, hipHostMallocDefault);
+    if (e != hipSuccess) return fail(IRIS_E_NOMEM, std::string("hipHostMalloc result: ") + hipGetErrorString(e));
+    d->host_result_cap = want;
     return 0;
 }
 

@@ -223,7 +223,7 @@ int launch_resolver(void *stream, const uint16_t *const *shares, uint32_t parts,
 int launch_shares_mfma(void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *out);
 int launch_template_search(void *stream, const void *db, const void *qtab, LaunchRange r, double *dist_out,
                            Partial *partials, uint32_t *n_partials);
-int launch_reduce(void *stream, const Partial *partials, uint32_t n_partials, Partial *out);
+int launch_reduce(void *stream, Partial *partials, uint32_t n_partials, Partial *out);  // consumes partials
 int launch_masks(void *stream, const void *db, const void *qtab, LaunchRange r, uint16_t *out);
 int launch_shares(void *stream, const void *db, const void *qtab, LaunchRange r, uint16_t *out);
 

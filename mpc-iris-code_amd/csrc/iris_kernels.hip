@@ -282,8 +282,11 @@ __global__ void __launch_bounds__(256, 8)
 
 // ------------------------------------------------------------------ reduce
 
+// One workgroup folds partials[i * stride] for i < n into *out.  A single
+// workgroup reads ~10 B/clk, so tens of thousands of partials (one per search
+// workgroup) first go through reduce_stage_kernel below.
 __global__ void __launch_bounds__(1024) reduce_kernel(const Partial *__restrict__ partials, uint32_t n,
-                                                      Partial *__restrict__ out) {
+                                                      Partial *__restrict__ out, uint32_t stride = 1) {
     Partial c;
     c.num = 0;
     c.den = 0;
@@ -291,7 +294,7 @@ __global__ void __launch_bounds__(1024) reduce_kernel(const Partial *__restrict_
     c.pad = 0;
     c.idx = ~0ull;
     for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
-        const Partial p = partials[i];
+        const Partial p = partials[(uint64_t)i * stride];
         if (better(p, c)) c = p;
     }
     c = wave_best(c);
@@ -305,6 +308,35 @@ __global__ void __launch_bounds__(1024) reduce_kernel(const Partial *__restrict_
         for (int w = 1; w < nw; ++w)
             if (better(sh[w], b)) b = sh[w];
         *out = b;
+    }
+}
+
+constexpr uint32_t kReduceChunk = 1024;  // partials per first-stage workgroup
+
+// First stage: workgroup b folds partials[b * kReduceChunk, +kReduceChunk) and
+// writes its winner in place at partials[b * kReduceChunk] (a slot only it reads).
+__global__ void __launch_bounds__(256) reduce_stage_kernel(Partial *__restrict__ partials, uint32_t n) {
+    const uint64_t base = (uint64_t)blockIdx.x * kReduceChunk;
+    const uint32_t m = (uint32_t)min<uint64_t>(kReduceChunk, n - base);
+    Partial c;
+    c.num = 0;
+    c.den = 0;
+    c.rot = 0;
+    c.pad = 0;
+    c.idx = ~0ull;
+    for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
+        const Partial p = partials[base + i];
+        if (better(p, c)) c = p;
+    }
+    c = wave_best(c);
+    __shared__ Partial sh[4];
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = c;
+    __syncthreads();  // every read of the chunk is done before its first slot is overwritten
+    if (threadIdx.x == 0) {
+        Partial b = sh[0];
+        for (int w = 1; w < 4; ++w)
+            if (better(sh[w], b)) b = sh[w];
+        partials[base] = b;
     }
 }
 
@@ -454,8 +486,17 @@ int launch_template_search(void *stream, const void *db, const void *qtab, Launc
     return check_launch();
 }
 
-int launch_reduce(void *stream, const Partial *partials, uint32_t n_partials, Partial *out) {
-    hipLaunchKernelGGL(reduce_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, partials, n_partials, out);
+// Consumes the partials (a large set is folded in place by a first stage).
+int launch_reduce(void *stream, Partial *partials, uint32_t n_partials, Partial *out) {
+    if (n_partials <= 4 * kReduceChunk) {
+        hipLaunchKernelGGL(reduce_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, partials, n_partials, out, 1u);
+        return check_launch();
+    }
+    const uint32_t g = (n_partials + kReduceChunk - 1) / kReduceChunk;
+    hipLaunchKernelGGL(reduce_stage_kernel, dim3(g), dim3(256), 0, (hipStream_t)stream, partials, n_partials);
+    if (check_launch() != 0) return -1;
+    hipLaunchKernelGGL(reduce_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, (const Partial *)partials, g, out,
+                       kReduceChunk);
     return check_launch();
 }
 

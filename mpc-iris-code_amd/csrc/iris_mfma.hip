@@ -21,6 +21,7 @@
 // interleaved dwords turn into fp4 B-fragments with four v_and + two
 // shift-and per dword pair — fast VOP2 ops, hidden under the MFMAs.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 
 #include "iris_device.hpp"
 
@@ -69,13 +70,12 @@ __device__ __forceinline__ uint4 stream_load(const uint4 *p) {
 
 enum { MF_COUNTS = 0, MF_SEARCH = 1 };
 
-template <int MODE>
+template <int MODE, int T = kMfmaTiles>
 __global__ void __launch_bounds__(256, 2)
     template_mfma_kernel(const uint4 *__restrict__ db, const uint4 *__restrict__ qfrag, uint64_t tile0,
                          uint64_t ntiles, uint64_t first, uint64_t end, uint16_t *__restrict__ num_out,
                          uint16_t *__restrict__ den_out, double *__restrict__ dist_out,
                          Partial *__restrict__ partials) {
-    constexpr int T = kMfmaTiles;
     const int lane = threadIdx.x & 63;
     const int wslot = threadIdx.x >> 6;
     const uint64_t wave = (uint64_t)blockIdx.x * kWaveSlots + wslot;
@@ -424,14 +424,22 @@ int launch_generate_tiles(void *stream, void *db, uint64_t t_first, uint64_t n, 
 
 struct TileRange {
     uint64_t tile0, ntiles, grid;
+    int tiles_per_wave;
 };
+
+// Below this many tiles, 4 tiles per wave would leave CUs idle (fewer than 2
+// workgroups per CU): small ranges run one tile per wave, 4x the workgroups.
+constexpr uint64_t kSmallTiles = 4 * kWaveSlots * 256 * 2;
 
 static TileRange tile_range(LaunchRange r) {
     TileRange t;
     t.tile0 = r.first / kTileRecs;
     const uint64_t tile1 = (r.first + r.n + kTileRecs - 1) / kTileRecs;
     t.ntiles = tile1 - t.tile0;
-    const uint64_t waves = (t.ntiles + kMfmaTiles - 1) / kMfmaTiles;
+    t.tiles_per_wave = t.ntiles < kSmallTiles ? 1 : kMfmaTiles;
+    // test hook: IRIS_TILES_PER_WAVE=1|4 pins the variant (tests run both on small ranges)
+    if (const char *f = getenv("IRIS_TILES_PER_WAVE")) t.tiles_per_wave = atoi(f) == 1 ? 1 : kMfmaTiles;
+    const uint64_t waves = (t.ntiles + t.tiles_per_wave - 1) / t.tiles_per_wave;
     t.grid = (waves + kWaveSlots - 1) / kWaveSlots;
     return t;
 }
@@ -461,7 +469,8 @@ int launch_template_mfma_counts(void *stream, const void *db, const void *qfrag,
                                 uint16_t *den_out) {
     if (r.n == 0) return 0;
     const TileRange t = tile_range(r);
-    hipLaunchKernelGGL(template_mfma_kernel<MF_COUNTS>, dim3((uint32_t)t.grid), dim3(256), 0, (hipStream_t)stream,
+    auto kern = t.tiles_per_wave == 1 ? template_mfma_kernel<MF_COUNTS, 1> : template_mfma_kernel<MF_COUNTS>;
+    hipLaunchKernelGGL(kern, dim3((uint32_t)t.grid), dim3(256), 0, (hipStream_t)stream,
                        (const uint4 *)db, (const uint4 *)qfrag, t.tile0, t.ntiles, r.first, r.first + r.n, num_out,
                        den_out, (double *)nullptr, (Partial *)nullptr);
     return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -472,7 +481,8 @@ int launch_template_mfma_search(void *stream, const void *db, const void *qfrag,
     const TileRange t = tile_range(r);
     *n_partials = (uint32_t)t.grid;
     if (r.n == 0) return 0;
-    hipLaunchKernelGGL(template_mfma_kernel<MF_SEARCH>, dim3((uint32_t)t.grid), dim3(256), 0, (hipStream_t)stream,
+    auto kern = t.tiles_per_wave == 1 ? template_mfma_kernel<MF_SEARCH, 1> : template_mfma_kernel<MF_SEARCH>;
+    hipLaunchKernelGGL(kern, dim3((uint32_t)t.grid), dim3(256), 0, (hipStream_t)stream,
                        (const uint4 *)db, (const uint4 *)qfrag, t.tile0, t.ntiles, r.first, r.first + r.n,
                        (uint16_t *)nullptr, (uint16_t *)nullptr, dist_out, partials);
     return hipGetLastError() == hipSuccess ? 0 : -1;

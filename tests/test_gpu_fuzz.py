@@ -27,7 +27,11 @@ def bits_eq(a, b):
     return (np.asarray(a, np.float64).view(np.uint64) == np.asarray(b, np.float64).view(np.uint64)).all()
 
 
-def test_fuzz_templates(device):
+@pytest.mark.parametrize("tiles_per_wave", ["auto", "1", "4"])
+def test_fuzz_templates(device, monkeypatch, tiles_per_wave):
+    # small ranges run one tile per wave by default; "4" pins the large-range variant
+    if tiles_per_wave != "auto":
+        monkeypatch.setenv("IRIS_TILES_PER_WAVE", tiles_per_wave)
     recs = oc.gen_templates(101, 0, 700)
     for i, (total, first, n, layout) in enumerate(_draws(1, 700)):
         q = recs[(i * 37) % total].copy()
