@@ -170,6 +170,22 @@ int engine_new(iris_device *dev, int kind, const void *table, size_t bytes, iris
     return 0;
 }
 
+// A new engine whose tables `build(stream, host_query, tab, frag)` fills from the host
+// query passed in the kernel arguments (template and mask queries, iris_query.hip).
+template <class B>
+int engine_from_host_query(iris_device *dev, int kind, const void *query, size_t tab_bytes, size_t frag_bytes,
+                           iris_engine **out, B &&build) {
+    iris_engine *e = nullptr;
+    CHK(engine_alloc(dev, kind, tab_bytes, frag_bytes, 0, &e));
+    if (build(dev->stream, query, (uint32_t *)e->qtab, (uint32_t *)e->qfrag) != 0) {
+        const hipError_t err = hipGetLastError();
+        engine_free(e);
+        return fail(IRIS_E_HIP, std::string("build query tables: ") + hipGetErrorString(err));
+    }
+    *out = e;
+    return 0;
+}
+
 // Uploads a query (`qbytes` from the host) and builds the engine's tables from it
 // on the device with `build(stream, query_dev, tab, frag)` (iris_query.hip).
 template <class B>
@@ -489,8 +505,8 @@ int iris_masks_engine_new(iris_device_t *d, const uint64_t query_mask[IRIS_LIMBS
     ARG(d && query_mask && out, "NULL argument");
     std::lock_guard<std::recursive_mutex> g(d->mu);
     CHK(set_device(d));
-    CHK(engine_from_query(d, IRIS_KIND_MASKS, query_mask, IRIS_LIMBS * 8, (size_t)kPlaneDwords * kSlotTabStride * 4,
-                          kMaskFragBytes, out, launch_query_masks));
+    CHK(engine_from_host_query(d, IRIS_KIND_MASKS, query_mask, (size_t)kPlaneDwords * kSlotTabStride * 4,
+                               kMaskFragBytes, out, launch_query_masks));
     device_retain(d);
     return 0;
 }
@@ -507,9 +523,8 @@ int iris_distance_engine_new(iris_device_t *d, const uint16_t query[IRIS_BITS], 
 
 namespace {
 int template_engine_locked(iris_device *d, const iris_template_t *query, iris_engine **out) {
-    return engine_from_query(d, IRIS_KIND_TEMPLATES, query, sizeof(iris_template_t),
-                             (size_t)kPlaneDwords * kTemplateTabStride * 4, kTemplateFragDwords * 4, out,
-                             launch_query_template);
+    return engine_from_host_query(d, IRIS_KIND_TEMPLATES, query, (size_t)kPlaneDwords * kTemplateTabStride * 4,
+                                  kTemplateFragDwords * 4, out, launch_query_template);
 }
 }  // namespace
 

@@ -173,7 +173,7 @@ struct LaunchRange {
 
 int launch_pack(void *stream, const KindInfo &k, const void *staging, void *db, uint64_t t_first, uint64_t n);
 // per-engine query tables built on the device from the query (iris_query.hip)
-int launch_query_template(void *stream, const void *q, uint32_t *tab, uint32_t *frag);
+int launch_query_template(void *stream, const void *q, uint32_t *tab, uint32_t *frag);  // q, qmask: host
 int launch_query_masks(void *stream, const void *qmask, uint32_t *tab, uint32_t *frag);
 int launch_query_shares(void *stream, const void *q, uint32_t *tab, uint32_t *frag);
 int launch_query_tiles(void *stream, const void *queries, uint32_t nq, uint32_t nqp, uint32_t *tiles);

@@ -6,10 +6,12 @@
 // A-fragments of the TILES kernels (iris_internal.hpp).  Built here from the
 // query alone, so creating an engine costs one small upload and one launch
 // (the host builders in iris_host.cpp, bit by bit, took ~3.5 ms per template
-// query — as long as the 10M-template search itself).  The host builders stay
+// query — as long as the 10M-template search itself).  Template and mask
+// queries travel in the kernel arguments, so those engines cost one launch.  The host builders stay
 // as the reference the device tables are tested against
 // (iris_debug_query_tables, tests/test_gpu_query.py).
 #include <hip/hip_runtime.h>
+#include <string.h>
 
 #include "iris_internal.hpp"
 
@@ -40,12 +42,21 @@ __device__ __forceinline__ uint32_t rot_dword(const uint32_t *b, int r, int w) {
 // fragments [(c*64 + k + 32h) * 4 + j/8] nibble j%8 = fp4 encode() of bit
 // frag_bit(j) of plane dword w = 2c + h (+1.0 = 0x2, -1.0 = 0xA) — the layout of
 // build_template_table / build_template_frags.  Thread (w, k), k = 31 zero.
-__global__ void __launch_bounds__(256) query_template_kernel(const iris_template_t *__restrict__ q,
-                                                             uint32_t *__restrict__ tab, uint4 *__restrict__ frag) {
+// The query travels by value in the kernel arguments (3200 B of the 4 KB
+// kernarg segment): creating an engine is one launch, no separate upload.
+struct TemplateArg {
+    uint32_t pattern[kPlaneDwords], mask[kPlaneDwords];
+};
+struct MaskArg {
+    uint32_t mask[kPlaneDwords];
+};
+
+__global__ void __launch_bounds__(256) query_template_kernel(const TemplateArg q, uint32_t *__restrict__ tab,
+                                                             uint4 *__restrict__ frag) {
     __shared__ uint32_t sp[kPlaneDwords], sm[kPlaneDwords];
     for (int i = threadIdx.x; i < kPlaneDwords; i += blockDim.x) {
-        sp[i] = ((const uint32_t *)q->pattern)[i];
-        sm[i] = ((const uint32_t *)q->mask)[i];
+        sp[i] = q.pattern[i];
+        sm[i] = q.mask[i];
     }
     __syncthreads();
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
@@ -71,10 +82,10 @@ __global__ void __launch_bounds__(256) query_template_kernel(const iris_template
 // MASKS: table [w*32 + k] = mask_k dword w; compact fragments dword
 // [((c/4)*64 + k + 32h) * 4 + c%4] bit 4 (j%8) + {2,1,0,3}[j/8] = bit
 // mask_frag_bit(j) of dword w = 2c + h (build_masks_table / build_masks_frags).
-__global__ void __launch_bounds__(256) query_masks_kernel(const uint64_t *__restrict__ qmask,
-                                                          uint32_t *__restrict__ tab, uint32_t *__restrict__ frag) {
+__global__ void __launch_bounds__(256) query_masks_kernel(const MaskArg qmask, uint32_t *__restrict__ tab,
+                                                          uint32_t *__restrict__ frag) {
     __shared__ uint32_t sm[kPlaneDwords];
-    for (int i = threadIdx.x; i < kPlaneDwords; i += blockDim.x) sm[i] = ((const uint32_t *)qmask)[i];
+    for (int i = threadIdx.x; i < kPlaneDwords; i += blockDim.x) sm[i] = qmask.mask[i];
     __syncthreads();
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= kPlaneDwords * 32) return;
@@ -183,15 +194,21 @@ __global__ void __launch_bounds__(256) query_tiles_kernel(const iris_template_t 
     }
 }
 
+// q / qmask: HOST pointers (copied into the kernel arguments at launch)
 int launch_query_template(void *stream, const void *q, uint32_t *tab, uint32_t *frag) {
-    hipLaunchKernelGGL(query_template_kernel, dim3(kPlaneDwords * 32 / 256), dim3(256), 0, (hipStream_t)stream,
-                       (const iris_template_t *)q, tab, (uint4 *)frag);
+    TemplateArg a;
+    memcpy(a.pattern, ((const iris_template_t *)q)->pattern, sizeof(a.pattern));
+    memcpy(a.mask, ((const iris_template_t *)q)->mask, sizeof(a.mask));
+    hipLaunchKernelGGL(query_template_kernel, dim3(kPlaneDwords * 32 / 256), dim3(256), 0, (hipStream_t)stream, a,
+                       tab, (uint4 *)frag);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int launch_query_masks(void *stream, const void *qmask, uint32_t *tab, uint32_t *frag) {
-    hipLaunchKernelGGL(query_masks_kernel, dim3(kPlaneDwords * 32 / 256), dim3(256), 0, (hipStream_t)stream,
-                       (const uint64_t *)qmask, tab, frag);
+    MaskArg a;
+    memcpy(a.mask, qmask, sizeof(a.mask));
+    hipLaunchKernelGGL(query_masks_kernel, dim3(kPlaneDwords * 32 / 256), dim3(256), 0, (hipStream_t)stream, a, tab,
+                       frag);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
