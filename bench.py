@@ -427,7 +427,7 @@ def main():
             if args.workload == "batch":
                 ms = e.search(db, index_base=lo)
                 if dist is not None:
-                    ms = [iris_dist.allgather_merge(x, device=xdev) for x in ms]
+                    ms = iris_dist.allgather_merge_many(ms, device=xdev)
                 return ms
             if args.workload != "search":
                 e.batch_process_device(db, out_dev)  # [n][31] u16 left in HBM

@@ -26,18 +26,58 @@ def shard_range(n, rank, world):
     return lo, hi
 
 
+_BUFS = {}
+
+
+def _exchange_buffers(device, world, nbytes):
+    """Per (device, world, size) exchange tensors, allocated once: the per-step cost
+    is then one small H2D copy, the all-gather and one D2H copy into pinned memory."""
+    key = (str(device), world, nbytes)
+    if key not in _BUFS:
+        _BUFS[key] = (torch.empty(nbytes, dtype=torch.uint8, device=device),
+                      torch.empty(world * nbytes, dtype=torch.uint8, device=device),
+                      torch.empty(world * nbytes, dtype=torch.uint8).pin_memory())
+    return _BUFS[key]
+
+
+def allgather_merge_many(locals_, device=None):
+    """Per query: merge of every rank's Match, for a list of per-query Matches
+    (a batched search), with ONE all-gather of len(locals_) x 32 bytes per rank."""
+    nq = len(locals_)
+    if nq == 0:
+        return []
+    buf = np.frombuffer(b"".join(bytes(m) for m in locals_), dtype=np.uint8).copy()
+    t = torch.from_numpy(buf)
+    world = dist.get_world_size()
+    if device is not None and torch.device(device).type == "cuda":
+        send, flat, host = _exchange_buffers(device, world, nq * RECORD_BYTES)
+        send.copy_(t)
+        dist.all_gather_into_tensor(flat, send)
+        host.copy_(flat)
+        raw = host.numpy().tobytes()
+    else:
+        out = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(out, t)
+        raw = b"".join(o.numpy().tobytes() for o in out)
+    per_rank = nq * RECORD_BYTES
+    return [ih.merge_matches([ih.Match.from_buffer_copy(raw[r * per_rank + q * RECORD_BYTES:
+                                                            r * per_rank + (q + 1) * RECORD_BYTES])
+                              for r in range(world)]) for q in range(nq)]
+
+
 def allgather_merge(local, device=None):
     """All-gather every rank's Match and merge.  `device` is the torch device the
     exchange tensor lives on (a cuda device for RCCL, cpu for gloo)."""
     buf = np.frombuffer(bytes(local), dtype=np.uint8).copy()
     t = torch.from_numpy(buf)
-    if device is not None:
-        t = t.to(device)
     world = dist.get_world_size()
-    if t.is_cuda:  # RCCL: one [world * 32] byte tensor, one device-to-host copy
-        flat = torch.empty(world * RECORD_BYTES, dtype=torch.uint8, device=t.device)
-        dist.all_gather_into_tensor(flat, t)
-        raw = flat.cpu().numpy().tobytes()
+    if device is not None and torch.device(device).type == "cuda":
+        # RCCL: one [world * 32] byte all-gather into a device tensor, one D2H copy
+        send, flat, host = _exchange_buffers(device, world, RECORD_BYTES)
+        send.copy_(t)
+        dist.all_gather_into_tensor(flat, send)
+        host.copy_(flat)
+        raw = host.numpy().tobytes()
         recs = [ih.Match.from_buffer_copy(raw[i * RECORD_BYTES:(i + 1) * RECORD_BYTES]) for i in range(world)]
     else:
         out = [torch.empty_like(t) for _ in range(world)]

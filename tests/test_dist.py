@@ -44,8 +44,14 @@ def _worker(rank, world, port, n, seed, q, result_path):
     else:
         local = ih.Match(float("inf"), 2**64 - 1, 0, 0, 0, 0)
     merged = iris_dist.allgather_merge(local)
+    # the batched form: one all-gather of every query's Match
+    inf = ih.Match(float("inf"), 2**64 - 1, 0, 0, 0, 0)
+    ranked = ih.Match(0.5 - 0.1 * rank, lo, 5 - rank, 10, 0, 0)
+    many = iris_dist.allgather_merge_many([local, inf, ranked])
     if rank == 0:
-        np.save(result_path, np.array([merged.distance, float(merged.index), merged.num, merged.den]))
+        np.save(result_path, np.array([merged.distance, float(merged.index), merged.num, merged.den,
+                                       many[0].distance, float(many[0].index), many[1].distance,
+                                       float(many[1].index), many[2].distance, float(many[2].index)]))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -66,6 +72,10 @@ def test_gloo_shard_merge(tmp_path, world):
     got = np.load(result)
     want_d, want_i = oc.argmin(oc.template_distances(q, full))
     assert got[0] == want_d and int(got[1]) == want_i
+    assert got[4] == got[0] and got[5] == got[1]              # batched merge == single merge
+    assert got[6] == np.inf and got[7] == float(2**64 - 1)     # no candidate on any rank
+    last_lo = iris_dist.shard_range(n, world - 1, world)[0]
+    assert np.isclose(got[8], 0.5 - 0.1 * (world - 1)) and int(got[9]) == last_lo
     # shards tile the range exactly
     spans = [iris_dist.shard_range(n, r, world) for r in range(world)]
     assert spans[0][0] == 0 and spans[-1][1] == n
