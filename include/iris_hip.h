@@ -95,6 +95,10 @@ int iris_device_close(iris_device_t *dev);
 int iris_device_synchronize(iris_device_t *dev);
 /* The device's stream as a hipStream_t, for callers that order their own work. */
 int iris_device_stream(iris_device_t *dev, void **stream);
+/* Free and total device memory in bytes (sizing a resident database: a template
+ * takes 3200 B, a mask 1600 B, a share 25600 B; the reference mmaps its files
+ * instead, src/main.rs:389,458). */
+int iris_device_memory(iris_device_t *dev, size_t *free_bytes, size_t *total_bytes);
 /* Kernel timing with HIP events recorded on the device stream around every
  * launch of the named kernel family ("template_search", "template_counts",
  * "masks", "shares", ...).  Disabled by default. */

@@ -297,6 +297,14 @@ int iris_device_stream(iris_device_t *d, void **stream) {
     return 0;
 }
 
+int iris_device_memory(iris_device_t *d, size_t *free_bytes, size_t *total_bytes) {
+    ARG(d && free_bytes && total_bytes, "NULL argument");
+    std::lock_guard<std::recursive_mutex> g(d->mu);
+    CHK(set_device(d));
+    HIPCHK(hipMemGetInfo(free_bytes, total_bytes));
+    return 0;
+}
+
 int iris_device_set_profiling(iris_device_t *d, int enabled) {
     ARG(d, "device is NULL");
     std::lock_guard<std::recursive_mutex> g(d->mu);

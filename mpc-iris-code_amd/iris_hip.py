@@ -77,6 +77,8 @@ def load_library(path=None):
             "iris_device_close": ([P], ctypes.c_int),
             "iris_device_synchronize": ([P], ctypes.c_int),
             "iris_device_stream": ([P, PP], ctypes.c_int),
+            "iris_device_memory": ([P, ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_size_t)],
+                                   ctypes.c_int),
             "iris_device_set_profiling": ([P, ctypes.c_int], ctypes.c_int),
             "iris_device_kernel_stats": ([P, ctypes.c_char_p, ctypes.POINTER(u64), ctypes.POINTER(ctypes.c_double),
                                           ctypes.POINTER(u64)], ctypes.c_int),
@@ -158,7 +160,7 @@ def exported_symbols():
         "iris_decode_distance", "iris_match_merge", "iris_db_load_file", "iris_db_save_file",
         "iris_templates_read_json", "iris_templates_write_json", "iris_prepare_shares",
         "iris_db_truncate", "iris_memcpy_h2d", "iris_resolver_search_masks",
-        "iris_query_table_sizes", "iris_engine_query_tables", "iris_host_query_tables",
+        "iris_query_table_sizes", "iris_engine_query_tables", "iris_host_query_tables", "iris_device_memory",
     ]
 
 
@@ -436,6 +438,12 @@ class Device:
 
     def synchronize(self):
         _check(load_library().iris_device_synchronize(self.handle))
+
+    def memory(self):
+        """(free, total) device memory in bytes."""
+        f, t = ctypes.c_size_t(), ctypes.c_size_t()
+        _check(load_library().iris_device_memory(self.handle, ctypes.byref(f), ctypes.byref(t)))
+        return f.value, t.value
 
     def stream(self):
         s = ctypes.c_void_p()

@@ -366,6 +366,37 @@ def test_large_search_properties(device, layout):
             assert sample.shape == (1, 400)
 
 
+def test_max_capacity_search(device):
+    """A template database filling the HBM (≈85M templates, 272 GB on an MI355X): 64-bit
+    tile and record offsets past 2^32 bytes and ~170k search partials.  Planted known
+    answers at both ends, an equal-distance copy (lowest index wins), a tail range with
+    an unaligned offset, and sampled distances against the oracle."""
+    free, _ = device.memory()
+    n = min(85_000_000, (free - (8 << 30)) // 3200)
+    assert n > 40_000_000, f"only {free / 1e9:.0f} GB free"
+    rng = np.random.default_rng(5)
+    with ih.Database(device, ih.KIND_TEMPLATES, n) as db:
+        db.generate(n, 31337)
+        q = oc.gen_templates(777, 0, 1)[0]
+        rec = np.concatenate([oc.bits_rotated(q[:200], -7), oc.bits_rotated(q[200:], -7)])
+        rec[3] ^= np.uint64(0xF0F0)
+        last = n - 3
+        db.write(last, rec[None, :])
+        db.write(n - 40_000_001, rec[None, :])  # same distance, lower index: wins the full search
+        with ih.TemplateEngine(device, q) as eng:
+            m = eng.search(db)
+            assert m.index == n - 40_000_001 and m.rotation == -7
+            first = n - 1_000_003  # unaligned tail range: only the copy at `last` is inside
+            mt = eng.search(db, first, n - first, index_base=0)
+            assert mt.index == last and mt.rotation == -7 and bits_eq(mt.distance, m.distance)
+            ii = np.sort(rng.choice(n, 400, replace=False))
+            recs = np.stack([db.read(int(i), 1)[0] for i in ii])
+            d = np.array([eng.distances(db, int(i), 1)[0] for i in ii])
+            assert bits_eq(d, oc.template_distances(q, recs))
+            want = oc.template_distances(q, rec[None, :])[0]
+            assert bits_eq(m.distance, want)
+
+
 # ---------------------------------------------------------------- resolver (src/main.rs:597-621)
 
 
