@@ -34,6 +34,8 @@ def _exchange_buffers(device, world, nbytes):
     is then one small H2D copy, the all-gather and one D2H copy into pinned memory."""
     key = (str(device), world, nbytes)
     if key not in _BUFS:
+        if len(_BUFS) >= 8:  # many distinct batch sizes: keep the cache bounded
+            _BUFS.clear()
         _BUFS[key] = (torch.empty(nbytes, dtype=torch.uint8, device=device),
                       torch.empty(world * nbytes, dtype=torch.uint8, device=device),
                       torch.empty(world * nbytes, dtype=torch.uint8).pin_memory())
