@@ -80,6 +80,9 @@ constexpr int kRows = GP * (BQ + BT);  // 1-KB rows per stage: 4 queries + 8 til
 constexpr int kRing = IRIS_BATCH_RING;  // LDS stages: kRing - 1 in flight + the one being read
 constexpr int kAhead = kRing - 1;
 static_assert(kAhead >= 1 && kAhead <= 3, "ring of 2..4 stages");
+#ifndef IRIS_BATCH_SPREAD
+#define IRIS_BATCH_SPREAD 0
+#endif
 constexpr int kRowsPerWave = (kRows + NW - 1) / NW;  // waves w < kRows - NW (kRowsPerWave - 1) issue one more
 constexpr bool kEvenRows = kRows % NW == 0;
 
@@ -114,11 +117,12 @@ __global__ void __launch_bounds__(64 * NW, NW <= 8 ? 8 / NW : 1)
         src_q[i] = r < GP * BQ ? qtiles + (uint64_t)(qg * BQ + r / GP) * kTileU4 + gp * 64 + lane
                                : db + gp * 64 + lane;
     }
-    auto issue = [&](uint32_t s) {
+    auto issue = [&](uint32_t s, int ilo = 0, int ihi = kRowsPerWave) {
         const uint32_t j = s / NSTEPS, k = s - j * NSTEPS;
         const uint64_t ng = gi + (uint64_t)j * G;
 #pragma unroll
         for (int i = 0; i < kRowsPerWave; ++i) {
+            if (i < ilo || i >= ihi) continue;  // compile-time after unrolling
             const int r = w + NW * i;
             if (!kEvenRows && r >= kRows) break;  // wave-uniform
             const uint4 *src;
@@ -184,10 +188,13 @@ __global__ void __launch_bounds__(64 * NW, NW <= 8 ? 8 / NW : 1)
             VMCNT(0);
         }
         if (IRIS_BATCH_DIAG != 5) __builtin_amdgcn_s_barrier();
-        if (s + kAhead < total) issue(s + kAhead);
+        if (!IRIS_BATCH_SPREAD && s + kAhead < total) issue(s + kAhead);
         const uint4(*st)[64] = ring[s % kRing];
 #pragma unroll
         for (int gp = 0; gp < GP; ++gp) {
+            // IRIS_BATCH_SPREAD: the next step's DMA rows issued a few per chunk pair
+            if (IRIS_BATCH_SPREAD && s + kAhead < total)
+                issue(s + kAhead, gp * kRowsPerWave / GP, (gp + 1) * kRowsPerWave / GP);
             uint4 a4[WQ], b4[WT];
 #pragma unroll
             for (int qi = 0; qi < WQ; ++qi) a4[qi] = st[GP * (wq0 + qi) + gp][lane];
