@@ -19,29 +19,27 @@ namespace iris {
 
 // dword w of rot(b, r): bit i is b's bit at row i / 200, column (i % 200 - r)
 // mod 200 (Bits::rotated, src/bits.rs:18-29; |r| <= 15).  b: 400 dwords in LDS.
+// Word-level: the 32 output bits split into at most four runs of consecutive
+// source bits (a row boundary and the column wrap), each one funnel shift.
 __device__ __forceinline__ uint32_t rot_dword(const uint32_t *b, int r, int w) {
     uint32_t x = 0;
-    const int i0 = 32 * w;
-    int row = i0 / IRIS_COLS, col = i0 - row * IRIS_COLS;
-#pragma unroll 4
-    for (int t = 0; t < 32; ++t) {
+    int t = 0, i = 32 * w;
+    while (t < 32) {
+        const int row = i / IRIS_COLS, col = i - row * IRIS_COLS;
         int sc = col - r;
         sc += sc < 0 ? IRIS_COLS : 0;
         sc -= sc >= IRIS_COLS ? IRIS_COLS : 0;
-        const int s = row * IRIS_COLS + sc;
-        x |= ((b[s >> 5] >> (s & 31)) & 1u) << t;
-        if (++col == IRIS_COLS) {
-            col = 0;
-            ++row;
-        }
+        const int len = min(32 - t, min(IRIS_COLS - col, IRIS_COLS - sc));
+        const int src = row * IRIS_COLS + sc, d = src >> 5;
+        const uint64_t win = (uint64_t)b[d] | ((uint64_t)(d + 1 < kPlaneDwords ? b[d + 1] : 0u) << 32);
+        const uint32_t bits = (uint32_t)(win >> (src & 31)) & (len == 32 ? 0xFFFFFFFFu : ((1u << len) - 1u));
+        x |= bits << t;
+        t += len;
+        i += len;
     }
     return x;
 }
 
-// TEMPLATES: table [w*64 + 2k] = mask_k dword w, [w*64 + 2k+1] = pattern_k dword w;
-// fragments [(c*64 + k + 32h) * 4 + j/8] nibble j%8 = fp4 encode() of bit
-// frag_bit(j) of plane dword w = 2c + h (+1.0 = 0x2, -1.0 = 0xA) — the layout of
-// build_template_table / build_template_frags.  Thread (w, k), k = 31 zero.
 // The query travels by value in the kernel arguments (3200 B of the 4 KB
 // kernarg segment): creating an engine is one launch, no separate upload.
 struct TemplateArg {
