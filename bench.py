@@ -484,7 +484,9 @@ def main():
     # kernel time of one step (a batch of 1-2 queries runs as streaming passes: several launches per step)
     step_kernel_ms = kms / max(1, args.steps)
     achieved = rec_bytes * n / (avg_ms * 1e-3) / 1e9
-    traffic, traffic_src = load_traffic(args.workload, n, args.layout) if args.workload != "batch" else (None, None)
+    # batch: HBM bytes of the 1024-query launch (the DB once per XCD-shared pass + query tiles)
+    traffic, traffic_src = (load_traffic(args.workload, n, args.layout)
+                            if args.workload != "batch" or nq == 1024 else (None, None))
     ms_per_step = elapsed / args.steps * 1e3
     value = ROT * total * nq / (elapsed / args.steps)
 
@@ -530,7 +532,8 @@ def main():
                 # compute-bound: fp4 MFMA FLOPs (2 per MAC) of the den + encode products
                 "bound": "mfma", "achieved": 2 * MFMA_MACS_PER_TEMPLATE * n * nq / (step_kernel_ms * 1e-3) / 1e12,
                 "peak": 2 * FP4_DENSE_PEAK_MACS / 1e12, "unit": "TFLOP/s",
-                "frac": MFMA_MACS_PER_TEMPLATE * n * nq / (step_kernel_ms * 1e-3) / FP4_DENSE_PEAK_MACS, "traffic": None,
+                "frac": MFMA_MACS_PER_TEMPLATE * n * nq / (step_kernel_ms * 1e-3) / FP4_DENSE_PEAK_MACS,
+                "traffic": traffic,
             }),
             "kernel": {
                 "name": {("search", "tiles"): "template_mfma_kernel<MF_SEARCH> (fp4 MFMA)",

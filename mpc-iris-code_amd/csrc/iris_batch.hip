@@ -20,6 +20,7 @@
 // Per query the kernel keeps a running best (exact fraction, lowest index),
 // one partial per (query, workgroup), reduced by reduce_kernel per query.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 
 #include "iris_device.hpp"
 
@@ -96,11 +97,21 @@ constexpr bool kEvenRows = kRows % NW == 0;
 // pipeline never drains between N-groups.
 __global__ void __launch_bounds__(64 * NW, NW <= 8 ? 8 / NW : 1)
     batch_kernel(const uint4 *__restrict__ db, const uint4 *__restrict__ qtiles, uint64_t tile0, uint64_t ntiles,
-                 uint64_t first, uint64_t end, uint32_t nqg, uint32_t G, Partial *__restrict__ partials) {
+                 uint64_t first, uint64_t end, uint32_t nqg, uint32_t G, uint32_t xqg,
+                 Partial *__restrict__ partials) {
     __shared__ uint4 ring[kRing][kRows][64];  // all LDS in one object (no vmcnt(0) before ds_reads)
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const uint32_t qg = blockIdx.x % nqg, gi = blockIdx.x / nqg;
+    uint32_t qg, gi;
+    if (xqg) {  // XCD-aware: workgroup b runs on XCD b % 8; each XCD holds xqg query groups x G slices at a time
+        const uint32_t xcd = blockIdx.x & 7, local = blockIdx.x >> 3, per = xqg * G;
+        const uint32_t round = local / per, wl = local - round * per;
+        qg = (round * 8 + xcd) * xqg + wl / G;
+        gi = wl % G;
+    } else {
+        qg = blockIdx.x % nqg;
+        gi = blockIdx.x / nqg;
+    }
     const int wq0 = (w % kQW) * WQ, wsub = (w / kQW) * WT;
     const uint64_t ngroups = (ntiles + BT - 1) / BT;
     const uint32_t my_groups = gi < ngroups ? (uint32_t)((ngroups - gi + G - 1) / G) : 0;
@@ -327,6 +338,16 @@ BatchGeometry batch_geometry(LaunchRange r, uint32_t nq) {
     uint64_t G = (512 + g.nqg - 1) / g.nqg;  // ~2 workgroups per CU in total
     if (G > ngroups) G = ngroups ? ngroups : 1;
     g.G = (uint32_t)G;
+    g.xqg = 0;
+    // XCD-aware grid (IRIS_BATCH_XQG = query groups per XCD per round): the 32 CUs of an XCD
+    // run xqg query groups x 32/xqg N-slices, so their query tiles stay in that XCD's L2
+    if (const char *e = getenv("IRIS_BATCH_XQG")) {
+        const uint32_t x = (uint32_t)atoi(e);
+        if (x && 32 % x == 0 && g.nqg % (8 * x) == 0 && ngroups >= 32 / x) {
+            g.xqg = x;
+            g.G = 32 / x;
+        }
+    }
     return g;
 }
 
@@ -334,7 +355,8 @@ int launch_batch(void *stream, const void *db, const void *qtiles, LaunchRange r
                  Partial *partials, Partial *out) {
     if (r.n == 0) return 0;
     hipLaunchKernelGGL(batch_kernel, dim3(g.nqg * g.G), dim3(64 * NW), 0, (hipStream_t)stream, (const uint4 *)db,
-                       (const uint4 *)qtiles, g.tile0, g.ntiles, r.first, r.first + r.n, g.nqg, g.G, partials);
+                       (const uint4 *)qtiles, g.tile0, g.ntiles, r.first, r.first + r.n, g.nqg, g.G, g.xqg,
+                       partials);
     if (hipGetLastError() != hipSuccess) return -1;
     hipLaunchKernelGGL(batch_reduce_kernel, dim3(g.nqg * BQ), dim3(256), 0, (hipStream_t)stream, partials, g.G, out);
     return hipGetLastError() == hipSuccess ? 0 : -1;

@@ -9,7 +9,8 @@ import sys
 
 ROOT = pathlib.Path(__file__).resolve().parents[1]
 PMC = ROOT / "gpurun_out" / "pmc"
-KERNELS = {"search": ("template_mfma_kernel<1>", 10_000_000, 3200),
+KERNELS = {"search": ("template_mfma_kernel<1", 10_000_000, 3200),  # <1, 4> (and <1, 1> on small ranges)
+           "batch": ("batch_kernel", 10_000_000, 3200),  # 1024 queries: the DB once + query tiles
            "masks": ("masks_mfma_kernel", 10_000_000, 1600 + 62),
            "shares": ("shares_mfma_kernel", 10_000_000, 25600 + 62),
            "resolver": ("resolver_kernel", 10_000_000, 4 * 62),
@@ -52,7 +53,8 @@ def main(round_tag="r01"):
                 continue
             rd, wr = fetch * 1024 * 2, write * 1024
             j = {"round": int(round_tag[1:]), "workload": w, "layout": lay, "kernel": k,
-                 "command": f"rocprofv3 --pmc FETCH_SIZE|WRITE_SIZE (separate passes) -- python3 bench.py --workload {w} --steps 3 --warmup 1",
+                 "command": f"rocprofv3 --pmc FETCH_SIZE|WRITE_SIZE (separate passes) -- python3 bench.py --workload {w} "
+                            + ("--queries 1024 --steps 1 --warmup 0" if w == "batch" else "--steps 3 --warmup 1"),
                  "n_records_per_launch": n, "FETCH_SIZE_kB_raw": fetch, "WRITE_SIZE_kB_raw": write,
                  "correction": "read bytes = FETCH_SIZE*1024*2, write bytes = WRITE_SIZE*1024 (MI355X_MICROARCH.md §HBM)",
                  "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,

@@ -15,8 +15,10 @@ pass() {  # workload counter tag args...
 }
 ws=${WORKLOADS:-search masks shares resolver}
 for w in $ws; do
-    pass $w FETCH_SIZE "" --steps 3 --warmup 1 || exit 1
-    pass $w WRITE_SIZE "" --steps 3 --warmup 1 || exit 1
+    a="--steps 3 --warmup 1"
+    [ $w = batch ] && a="--queries 1024 --steps 1 --warmup 0"
+    pass $w FETCH_SIZE "" $a || exit 1
+    pass $w WRITE_SIZE "" $a || exit 1
 done
 if [ -z "$NO_LANES" ]; then
     pass search FETCH_SIZE _lanes --steps 3 --warmup 1 --layout lanes || exit 1
