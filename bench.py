@@ -551,6 +551,10 @@ def main():
                 "mfma_fp4_frac": (MFMA_MACS_PER_TEMPLATE * n * nq / (step_kernel_ms * 1e-3) / FP4_DENSE_PEAK_MACS
                                   if args.layout == "tiles" and args.workload in ("search", "batch") else None),
                 "traffic_source": traffic_src,
+                "traffic_note": ("FETCH_SIZE counts every L2 miss, Infinity-Cache hits included: the query tiles "
+                                 "(409 KB per 4 queries) are re-streamed from the 256-MB MALL for each N-group, "
+                                 "the template DB comes from HBM about once per XCD" if args.workload == "batch"
+                                 else None),
             },
             "cpu_baseline": cpu,
             "check": ({"planted_index": plant_global, "found_index": int(m.index), "rotation": int(m.rotation),
