@@ -26,7 +26,21 @@ typedef float v16f __attribute__((ext_vector_type(16)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kTile = 32;
-constexpr int kMasksTiles = 4;  // tiles per wave
+#ifndef IRIS_MASKS_T
+#define IRIS_MASKS_T 8
+#endif
+#ifndef IRIS_MASKS_BPC
+#define IRIS_MASKS_BPC 2
+#endif
+// tiles per wave: 8 for the [u16;31] output (longer groups, fewer store bursts:
+// 2.88-2.98 vs 2.98-3.03 ms per 10M in interleaved runs on two boxes, ~2 %; the first
+// run after a pause is ~7 % faster for either, the GPU is still cool); the fused resolver
+// keeps 4 (its epilogue state at 8 tiles costs registers: 5.1 vs 2.7 ms)
+constexpr int kMasksTiles = IRIS_MASKS_T;
+constexpr int kResolveTiles = 4;
+template <int MODE>
+constexpr int masks_tiles() { return MODE == 0 ? kMasksTiles : kResolveTiles; }
+constexpr int kMasksBlocksPerCu = IRIS_MASKS_BPC;  // persistent grid: workgroups per CU
 constexpr int kSharesTiles = 2;
 
 __device__ __forceinline__ uint4 nt_load(const uint4 *p) {
@@ -92,10 +106,10 @@ enum { MASKS_OUT = 0, MASKS_RESOLVE = 1 };
 // and a running (fraction, lowest index) best per lane becomes one partial per
 // workgroup — the denominators never reach memory.
 template <int MODE>
-__global__ void __launch_bounds__(256, 2)
+__global__ void __launch_bounds__(256, kMasksBlocksPerCu)
     masks_mfma_kernel(const uint4 *__restrict__ db, const uint4 *__restrict__ qfrag, uint64_t tile0, uint64_t ntiles,
                       uint64_t first, uint64_t end, uint16_t *__restrict__ out, MaskResolve rs) {
-    constexpr int T = kMasksTiles;
+    constexpr int T = masks_tiles<MODE>();
     constexpr uint32_t kSteps = kMaskChunks / 4;  // 50 steps of 4 chunks
     __shared__ uint4 sq[kMaskFragUint4];
     __shared__ __attribute__((aligned(16))) uint16_t sh_out[kWaveSlots][1024];
@@ -238,7 +252,7 @@ __global__ void __launch_bounds__(256, 2)
 int launch_masks_mfma(void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *out) {
     if (r.n == 0) return 0;
     const Tiles t = tiles_of(r, kMasksTiles);
-    const uint64_t grid = std::min<uint64_t>(t.grid, resident_blocks(2));
+    const uint64_t grid = std::min<uint64_t>(t.grid, resident_blocks(kMasksBlocksPerCu));
     hipLaunchKernelGGL(masks_mfma_kernel<MASKS_OUT>, dim3((uint32_t)grid), dim3(256), 0, (hipStream_t)stream,
                        (const uint4 *)db, (const uint4 *)qfrag, t.tile0, t.ntiles, r.first, r.first + r.n, out,
                        MaskResolve{});
@@ -246,15 +260,15 @@ int launch_masks_mfma(void *stream, const void *db, const void *qfrag, LaunchRan
 }
 
 uint32_t masks_resolve_partials(LaunchRange r) {
-    const Tiles t = tiles_of(r, kMasksTiles);
-    return (uint32_t)std::min<uint64_t>(t.grid, resident_blocks(2));
+    const Tiles t = tiles_of(r, kResolveTiles);
+    return (uint32_t)std::min<uint64_t>(t.grid, resident_blocks(kMasksBlocksPerCu));
 }
 
 int launch_masks_resolve(void *stream, const void *db, const void *qfrag, LaunchRange r,
                          const uint16_t *const *shares, uint32_t parts, double *dist_out, Partial *partials) {
     if (r.n == 0) return 0;
     if (parts == 0 || parts > 8) return -1;
-    const Tiles t = tiles_of(r, kMasksTiles);
+    const Tiles t = tiles_of(r, kResolveTiles);
     const uint64_t grid = masks_resolve_partials(r);
     MaskResolve rs{};
     rs.aligned = true;
