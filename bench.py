@@ -5,8 +5,11 @@
     torchrun --nproc-per-node N bench.py --gpus N ...
 
 A step = one search of the query against every resident template on every
-rank (the kernel + the partials reduce) plus, for N > 1, the RCCL all-gather
-of the per-shard minima and their merge.  The database is synthetic (the
+rank (the query engine build, the kernel, the partials reduce) plus, for N > 1,
+the RCCL all-gather of the per-shard minima and their merge.  Steps are
+pipelined by default (iris_template_search_async): step i+1's search is
+enqueued before step i's result is waited for and exchanged, so the host work
+and the exchange overlap the next kernel; --no-pipeline waits step by step.  The database is synthetic (the
 DESIGN.md §5 generator, uniform random pattern and mask bits as the
 reference's rng.gen::<Template>()), generated on each GPU so that shard k
 holds global templates [k*T, (k+1)*T) — inputs are resident in HBM before
@@ -54,6 +57,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--reuse-engine", action="store_true",
                     help="build the query engine once instead of once per step (default: per step, in the timed region)")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="search: wait for each step's result before enqueueing the next query "
+                         "(default: the next query's search is enqueued before this one's result is "
+                         "waited for and exchanged)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--layout", choices=["tiles", "lanes"], default="tiles",
                     help="tiles = MFMA kernels (default), lanes = VALU kernels")
@@ -440,14 +447,41 @@ def main():
             if eng is None:
                 e.close()
 
-    for _ in range(args.warmup):
-        m = step()
+    pipelined = args.workload == "search" and not args.no_pipeline
+
+    def run_steps(k):
+        """k steps; pipelined: step i+1's query engine and search are enqueued before step i's
+        result is waited for and (N > 1) all-gathered, so the exchange and the host work of a
+        step overlap the next step's kernel.  Every step's search runs to completion and every
+        result is exchanged and merged inside the call."""
+        if not pipelined:
+            m = None
+            for _ in range(k):
+                m = step()
+            return m
+
+        def finish(p):
+            m = p.wait()
+            return iris_dist.allgather_merge(m, device=xdev) if dist is not None else m
+
+        pend, m = None, None
+        for _ in range(k):
+            e = eng if eng is not None else new_engine()
+            p = e.search_async(db, index_base=lo)
+            if eng is None:
+                e.close()
+            if pend is not None:
+                m = finish(pend)
+            pend = p
+        return finish(pend) if pend is not None else m
+
+    if args.warmup:
+        m = run_steps(args.warmup)
     dev.reset_stats()
     dev.set_profiling(True)
     sync_all()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        m = step()
+    m = run_steps(args.steps)
     sync_all()
     elapsed = time.perf_counter() - t0
     dev.set_profiling(False)
@@ -524,6 +558,7 @@ def main():
                 "templates_per_gpu": n, "total_templates": total, "queries": nq, "rotations": ROT,
                 "bytes_per_template": rec_bytes, "parallelism": f"db-shard x{world}", "layout": args.layout,
                 "engine_per_step": not args.reuse_engine,
+                "pipelined": pipelined,
             },
             "roofline": ({
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -82,6 +82,7 @@ typedef struct iris_match {
 typedef struct iris_device iris_device_t;
 typedef struct iris_db iris_db_t;
 typedef struct iris_engine iris_engine_t;
+typedef struct iris_pending iris_pending_t;
 
 /* ---------------------------------------------------------------- errors */
 const char *iris_last_error(void);
@@ -223,6 +224,16 @@ int iris_template_distances(iris_engine_t *engine, const iris_db_t *db, uint64_t
  * NULL) receives the n per-template distances in DEVICE memory. */
 int iris_template_search(iris_engine_t *engine, const iris_db_t *db, uint64_t first, uint64_t n,
                          uint64_t index_base, double *dist_out_device, iris_match_t *out);
+
+/* Pipelined form of iris_template_search (no reference counterpart: the
+ * reference's calls block, src/lib.rs:42-53): enqueues the search and returns
+ * at once; iris_pending_wait blocks for THAT search only and frees the handle,
+ * so the next query's search can be enqueued (and its engine built) while the
+ * caller exchanges or consumes this result.  The engine may be destroyed
+ * before the wait; the database must stay alive and unmodified until it. */
+int iris_template_search_async(iris_engine_t *engine, const iris_db_t *db, uint64_t first, uint64_t n,
+                               uint64_t index_base, iris_pending_t **out);
+int iris_pending_wait(iris_pending_t *pending, iris_match_t *out);
 
 /* Batched queries (BASELINE configs[2]): nq query Templates searched against
  * one TILES template database in one pass; out[q] is query q's best match

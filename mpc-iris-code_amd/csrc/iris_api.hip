@@ -212,6 +212,7 @@ void device_teardown(iris_device *d) {
         for (DevBuf *b : {&d->partials, &d->result, &d->staging, &d->out_a, &d->out_b})
             if (b->p) (void)hipFree(b->p);
         if (d->host_result) (void)hipHostFree(d->host_result);
+        for (void *b : d->slot_blocks) (void)hipHostFree(b);
         for (auto &q : d->qpool) (void)hipFree(q.second);
         d->qpool.clear();
         for (auto &p : d->pending) {
@@ -656,24 +657,31 @@ int iris_template_counts(iris_engine_t *e, const iris_db_t *db, uint64_t first, 
     return 0;
 }
 
-static int search_locked(iris_engine_t *e, const iris_db_t *db, uint64_t first, uint64_t n, uint64_t index_base,
-                         double *dist_dev, iris_match_t *out) {
+// Enqueues the search of [first, first+n) and its reduce, whose winner lands in
+// `dst` (pinned host memory); nothing waits.
+static int search_enqueue(iris_engine_t *e, const iris_db_t *db, uint64_t first, uint64_t n, double *dist_dev,
+                          Partial *dst) {
     iris_device *d = e->dev;
+    if (n == 0) return 0;
     LaunchRange r{first, n};
     const bool tiles = db->k.layout == IRIS_LAYOUT_TILES;
     const uint32_t np = tiles ? mfma_search_partials(r) : search_partials(r);
     CHK(ensure(d->partials, (size_t)std::max<uint32_t>(np, 1) * sizeof(Partial)));
-    CHK(ensure_host_result(d, sizeof(Partial)));
     uint32_t written = 0;
     CHK(timed(d, "template_search", n, [&] {
         return tiles ? launch_template_mfma_search(d->stream, db->data, e->qfrag, r, dist_dev, (Partial *)d->partials.p, &written)
                      : launch_template_search(d->stream, db->data, e->qtab, r, dist_dev, (Partial *)d->partials.p, &written);
     }));
+    // the reduce writes the winner straight into pinned host memory: no copy before the wait
+    return timed(d, "reduce", written, [&] { return launch_reduce(d->stream, (Partial *)d->partials.p, written, dst); });
+}
+
+static int search_locked(iris_engine_t *e, const iris_db_t *db, uint64_t first, uint64_t n, uint64_t index_base,
+                         double *dist_dev, iris_match_t *out) {
+    iris_device *d = e->dev;
+    CHK(ensure_host_result(d, sizeof(Partial)));
+    CHK(search_enqueue(e, db, first, n, dist_dev, (Partial *)d->host_result));
     Partial res{};
-    if (n > 0) {
-        // the reduce writes the winner straight into pinned host memory: no copy before the sync
-        CHK(timed(d, "reduce", written, [&] { return launch_reduce(d->stream, (Partial *)d->partials.p, written, (Partial *)d->host_result); }));
-    }
     CHK(sync(d));
     if (n > 0) memcpy(&res, d->host_result, sizeof(Partial));
     if (out) {
@@ -750,6 +758,82 @@ int iris_template_search(iris_engine_t *e, const iris_db_t *db, uint64_t first, 
     CHK(range_ok(db, first, n));
     ARG(out, "out is NULL");
     return search_locked(e, db, first, n, index_base, dist_out_device, out);
+}
+
+static void match_from(const Partial &r, bool any, uint64_t base, iris_match_t *out) {
+    if (!any || r.den == 0) {
+        out->distance = INFINITY;
+        out->index = UINT64_MAX;
+        out->num = 0;
+        out->den = 0;
+        out->rotation = 0;
+    } else {
+        out->distance = (double)r.num / (double)r.den;
+        out->index = base + r.idx;
+        out->num = r.num;
+        out->den = r.den;
+        out->rotation = r.rot - IRIS_MAX_ROTATION;
+    }
+    out->reserved = 0;
+}
+
+struct iris_pending {
+    iris_device *dev = nullptr;
+    hipEvent_t ev = nullptr;    // recorded after the reduce (null for an empty range)
+    Partial *slot = nullptr;    // pinned host slot the reduce writes
+    uint64_t n = 0, base = 0;   // range size; index_base + first
+};
+
+int iris_template_search_async(iris_engine_t *e, const iris_db_t *db, uint64_t first, uint64_t n,
+                               uint64_t index_base, iris_pending_t **out) {
+    CHK(template_args(e, db));
+    ARG(out, "out is NULL");
+    iris_device *d = e->dev;
+    std::lock_guard<std::recursive_mutex> g(d->mu);
+    CHK(set_device(d));
+    CHK(range_ok(db, first, n));
+    iris_pending *p = new (std::nothrow) iris_pending();
+    if (!p) return fail(IRIS_E_NOMEM, "out of host memory");
+    p->dev = d;
+    p->n = n;
+    p->base = index_base + first;
+    int rc = take_result_slot(d, &p->slot);
+    if (rc == 0) rc = search_enqueue(e, db, first, n, nullptr, p->slot);
+    if (rc == 0 && n > 0) {
+        p->ev = take_event(d);
+        if (!p->ev) rc = fail(IRIS_E_HIP, "hipEventCreate failed");
+        else if (hipEventRecord(p->ev, d->stream) != hipSuccess) rc = fail(IRIS_E_HIP, "hipEventRecord failed");
+    }
+    if (rc != 0) {
+        if (p->slot) d->free_slots.push_back(p->slot);
+        if (p->ev) d->event_pool.push_back(p->ev);
+        delete p;
+        return rc;
+    }
+    device_retain(d);
+    *out = p;
+    return 0;
+}
+
+int iris_pending_wait(iris_pending_t *p, iris_match_t *out) {
+    ARG(p, "pending is NULL");
+    iris_device *d = p->dev;
+    hipError_t err = hipSuccess;
+    if (p->ev) err = hipEventSynchronize(p->ev);  // this search only: later enqueued work keeps running
+    Partial res{};
+    if (p->n > 0 && err == hipSuccess) memcpy(&res, p->slot, sizeof(Partial));
+    {
+        std::lock_guard<std::recursive_mutex> g(d->mu);
+        d->free_slots.push_back(p->slot);
+        if (p->ev) d->event_pool.push_back(p->ev);
+        fold_done(d);
+    }
+    const uint64_t n = p->n, base = p->base;
+    delete p;
+    device_release(d);
+    if (err != hipSuccess) return fail(IRIS_E_HIP, std::string("hipEventSynchronize: ") + hipGetErrorString(err));
+    if (out) match_from(res, n > 0, base, out);
+    return 0;
 }
 
 int iris_template_distances(iris_engine_t *e, const iris_db_t *db, uint64_t first, uint64_t n, double *out) {
@@ -873,22 +957,6 @@ static int resolver_finish(iris_device *d, uint32_t np, Partial *res) {
     return 0;
 }
 
-static void match_from(const Partial &r, bool any, uint64_t base, iris_match_t *out) {
-    if (!any || r.den == 0) {
-        out->distance = INFINITY;
-        out->index = UINT64_MAX;
-        out->num = 0;
-        out->den = 0;
-        out->rotation = 0;
-    } else {
-        out->distance = (double)r.num / (double)r.den;
-        out->index = base + r.idx;
-        out->num = r.num;
-        out->den = r.den;
-        out->rotation = r.rot - IRIS_MAX_ROTATION;
-    }
-    out->reserved = 0;
-}
 
 // Partial.idx values of one launch are row indices of that launch; chunked
 // host calls merge the per-chunk winners on the host in chunk order.

@@ -71,6 +71,9 @@ struct iris_device {
     // device-to-host copy between the last kernel and the stream sync)
     void *host_result = nullptr;
     size_t host_result_cap = 0;
+    // pinned result slots of asynchronous searches (iris_template_search_async)
+    std::vector<iris::Partial *> free_slots;
+    std::vector<void *> slot_blocks;
     // handles alive on this device (1 for the device handle itself + 1 per database
     // and engine handle): the device is torn down when the last one is released,
     // so handles may be destroyed in any order
@@ -136,6 +139,21 @@ inline int ensure_host_result(iris_device *d, size_t bytes) {
     return 0;
 }
 
+// A pinned host slot for one asynchronous search result (blocks of 256 slots).
+inline int take_result_slot(iris_device *d, iris::Partial **slot) {
+    if (d->free_slots.empty()) {
+        constexpr int kSlots = 256;
+        void *blk = nullptr;
+        hipError_t e = hipHostMalloc(&blk, kSlots * sizeof(iris::Partial), hipHostMallocDefault);
+        if (e != hipSuccess) return fail(IRIS_E_NOMEM, std::string("hipHostMalloc result slots: ") + hipGetErrorString(e));
+        d->slot_blocks.push_back(blk);
+        for (int i = kSlots - 1; i >= 0; --i) d->free_slots.push_back((iris::Partial *)blk + i);
+    }
+    *slot = d->free_slots.back();
+    d->free_slots.pop_back();
+    return 0;
+}
+
 inline hipEvent_t take_event(iris_device *d) {
     if (!d->event_pool.empty()) {
         hipEvent_t e = d->event_pool.back();
@@ -166,20 +184,30 @@ int timed(iris_device *d, const char *name, uint64_t items, F &&launch) {
     return 0;
 }
 
+// Folds the recorded kernel times whose end event has completed into the stats.
+inline void fold_done(iris_device *d) {
+    size_t keep = 0;
+    for (size_t i = 0; i < d->pending.size(); ++i) {
+        Pending &p = d->pending[i];
+        float ms = 0;
+        if (hipEventQuery(p.b) == hipSuccess && hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+            KStat &s = d->stats[p.name];
+            s.launches += 1;
+            s.ms += ms;
+            s.items += p.items;
+            d->event_pool.push_back(p.a);
+            d->event_pool.push_back(p.b);
+        } else {
+            d->pending[keep++] = p;
+        }
+    }
+    d->pending.resize(keep);
+}
+
 // Waits for the stream, then folds recorded kernel times into the stats.
 inline int sync(iris_device *d) {
     HIPCHK(hipStreamSynchronize(d->stream));
-    for (auto &p : d->pending) {
-        float ms = 0;
-        HIPCHK(hipEventElapsedTime(&ms, p.a, p.b));
-        KStat &s = d->stats[p.name];
-        s.launches += 1;
-        s.ms += ms;
-        s.items += p.items;
-        d->event_pool.push_back(p.a);
-        d->event_pool.push_back(p.b);
-    }
-    d->pending.clear();
+    fold_done(d);
     return 0;
 }
 

@@ -79,6 +79,8 @@ def load_library(path=None):
             "iris_device_stream": ([P, PP], ctypes.c_int),
             "iris_device_memory": ([P, ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_size_t)],
                                    ctypes.c_int),
+            "iris_template_search_async": ([P, P, u64, u64, u64, PP], ctypes.c_int),
+            "iris_pending_wait": ([P, ctypes.POINTER(Match)], ctypes.c_int),
             "iris_device_set_profiling": ([P, ctypes.c_int], ctypes.c_int),
             "iris_device_kernel_stats": ([P, ctypes.c_char_p, ctypes.POINTER(u64), ctypes.POINTER(ctypes.c_double),
                                           ctypes.POINTER(u64)], ctypes.c_int),
@@ -161,6 +163,7 @@ def exported_symbols():
         "iris_templates_read_json", "iris_templates_write_json", "iris_prepare_shares",
         "iris_db_truncate", "iris_memcpy_h2d", "iris_resolver_search_masks",
         "iris_query_table_sizes", "iris_engine_query_tables", "iris_host_query_tables", "iris_device_memory",
+        "iris_template_search_async", "iris_pending_wait",
     ]
 
 
@@ -753,6 +756,14 @@ class TemplateEngine(_Engine):
             db.append(a)
             return self.distances(db)
 
+    def search_async(self, db, first=0, n=None, index_base=0):
+        """Enqueue the fused min/argmin and return at once -> PendingSearch (wait() -> Match)."""
+        n = (len(db) - first) if n is None else n
+        h = ctypes.c_void_p()
+        _check(load_library().iris_template_search_async(self.handle, db.handle, int(first), int(n),
+                                                         int(index_base), ctypes.byref(h)))
+        return PendingSearch(h)
+
     def search(self, db, first=0, n=None, index_base=0, dist_out_device=None):
         """Fused min/argmin (src/main.rs:581-621) -> Match."""
         n = (len(db) - first) if n is None else n
@@ -760,6 +771,28 @@ class TemplateEngine(_Engine):
         _check(load_library().iris_template_search(self.handle, db.handle, int(first), int(n), int(index_base),
                                                    ctypes.c_void_p(dist_out_device or 0), ctypes.byref(m)))
         return m
+
+
+class PendingSearch:
+    """An enqueued search (TemplateEngine.search_async); wait() -> Match, once."""
+
+    def __init__(self, handle):
+        self.handle = handle
+
+    def wait(self):
+        if self.handle is None:
+            raise IrisError(-1, "PendingSearch.wait called twice")
+        m = Match()
+        h, self.handle = self.handle, None
+        _check(load_library().iris_pending_wait(h, ctypes.byref(m)))
+        return m
+
+    def __del__(self):
+        if getattr(self, "handle", None) is not None:
+            try:
+                load_library().iris_pending_wait(self.handle, None)
+            except Exception:
+                pass
 
 
 class TemplateBatchEngine(_Engine):

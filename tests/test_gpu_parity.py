@@ -366,6 +366,44 @@ def test_large_search_properties(device, layout):
             assert sample.shape == (1, 400)
 
 
+def test_search_async_pipeline(device, layout):
+    """iris_template_search_async: several searches in flight (engines destroyed right
+    after enqueueing), waited out of order, with a blocking call in between; each
+    result equals the blocking search and the oracle."""
+    n = 20_000
+    recs = oc.gen_templates(4242, 0, n)
+    rng = np.random.default_rng(8)
+    with ih.Database(device, ih.KIND_TEMPLATES, n, layout) as db:
+        db.append(recs)
+        qs = []
+        for i in range(6):
+            q = recs[int(rng.integers(0, n))].copy()
+            q[int(rng.integers(0, 400))] ^= np.uint64(1 << int(rng.integers(0, 64)))
+            qs.append(q)
+        pend = []
+        for i, q in enumerate(qs):
+            with ih.TemplateEngine(device, q) as e:
+                first, cnt = (0, n) if i % 3 else (123, n - 5000)
+                pend.append((e.search_async(db, first, cnt, index_base=7), first, cnt))
+        with ih.TemplateEngine(device, qs[0]) as e:  # a blocking call while searches are queued
+            assert len(e.distances(db, 0, 10)) == 10
+        with ih.TemplateEngine(device, qs[1]) as e:
+            empty = e.search_async(db, 5, 0).wait()
+        assert empty.distance == np.inf and empty.index == 2**64 - 1
+        order = [5, 0, 3, 1, 4, 2]
+        for i in order:
+            p, first, cnt = pend[i]
+            m = p.wait()
+            want_d, want_i = oc.argmin(oc.template_distances(qs[i], recs[first:first + cnt]))
+            assert bits_eq(m.distance, want_d) and m.index == want_i + first + 7
+            with ih.TemplateEngine(device, qs[i]) as e:
+                ms = e.search(db, first, cnt, index_base=7)
+            assert (ms.distance, ms.index, ms.num, ms.den, ms.rotation) == (m.distance, m.index, m.num, m.den,
+                                                                             m.rotation)
+        with pytest.raises(ih.IrisError):
+            pend[0][0].wait()
+
+
 def test_max_capacity_search(device):
     """A template database filling the HBM (≈85M templates, 272 GB on an MI355X): 64-bit
     tile and record offsets past 2^32 bytes and ~170k search partials.  Planted known
