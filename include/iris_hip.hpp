@@ -386,6 +386,38 @@ public:
     }
 };
 
+// An enqueued search (TemplateEngine::search_async): wait() once for its Match;
+// destroying it unwaited waits and discards the result.
+class PendingSearch {
+public:
+    explicit PendingSearch(iris_pending_t *p) : p_(p) {}
+    PendingSearch(PendingSearch &&o) noexcept : p_(o.p_) { o.p_ = nullptr; }
+    PendingSearch &operator=(PendingSearch &&o) noexcept {
+        if (this != &o) {
+            if (p_) (void)iris_pending_wait(p_, nullptr);
+            p_ = o.p_;
+            o.p_ = nullptr;
+        }
+        return *this;
+    }
+    PendingSearch(const PendingSearch &) = delete;
+    PendingSearch &operator=(const PendingSearch &) = delete;
+    ~PendingSearch() {
+        if (p_) (void)iris_pending_wait(p_, nullptr);
+    }
+    Match wait() {
+        if (!p_) throw Error(IRIS_E_ARG, "PendingSearch::wait called twice");
+        Match m{};
+        iris_pending_t *p = p_;
+        p_ = nullptr;
+        check(iris_pending_wait(p, &m));
+        return m;
+    }
+
+private:
+    iris_pending_t *p_;
+};
+
 // Template vs Template database (src/template.rs:43-64) with the resolver's argmin.
 class TemplateEngine : public detail::Engine {
 public:
@@ -396,6 +428,12 @@ public:
         Match m{};
         check(iris_template_search(h_, db.handle(), first, n, index_base, nullptr, &m));
         return m;
+    }
+    // pipelined form: returns once the search is enqueued (the engine may be destroyed before the wait)
+    PendingSearch search_async(const Database &db, uint64_t first, uint64_t n, uint64_t index_base = 0) const {
+        iris_pending_t *p = nullptr;
+        check(iris_template_search_async(h_, db.handle(), first, n, index_base, &p));
+        return PendingSearch(p);
     }
     std::vector<double> distances(const Database &db, uint64_t first, uint64_t n) const {
         std::vector<double> out(n);

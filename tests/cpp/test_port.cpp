@@ -254,6 +254,10 @@ std::vector<Case> cases() {
              tdb.append(db);
              const Match t = TemplateEngine(q).search(tdb, 0, db.size());
              CHECK(t.index == 33 && t.distance == 0.0);
+             // pipelined form: engine gone before the wait, same match
+             PendingSearch ps = TemplateEngine(q).search_async(tdb, 0, db.size());
+             const Match ta = ps.wait();
+             CHECK(ta.index == 33 && ta.distance == 0.0 && ta.rotation == 4);
          }},
     };
 }
