@@ -211,6 +211,13 @@ void device_teardown(iris_device *d) {
         (void)hipStreamSynchronize(d->stream);
         for (DevBuf *b : {&d->partials, &d->result, &d->staging, &d->out_a, &d->out_b})
             if (b->p) (void)hipFree(b->p);
+        if (d->aux) (void)hipStreamSynchronize(d->aux);
+        for (int b = 0; b < 2; ++b) {
+            if (d->apart[b].p) (void)hipFree(d->apart[b].p);
+            if (d->apart_read[b]) (void)hipEventDestroy(d->apart_read[b]);
+            if (d->apart_written[b]) (void)hipEventDestroy(d->apart_written[b]);
+        }
+        if (d->aux) (void)hipStreamDestroy(d->aux);
         if (d->host_result) (void)hipHostFree(d->host_result);
         for (void *b : d->slot_blocks) (void)hipHostFree(b);
         for (auto &q : d->qpool) (void)hipFree(q.second);
@@ -658,22 +665,44 @@ int iris_template_counts(iris_engine_t *e, const iris_db_t *db, uint64_t first, 
 }
 
 // Enqueues the search of [first, first+n) and its reduce, whose winner lands in
-// `dst` (pinned host memory); nothing waits.
+// `dst` (pinned host memory); nothing waits.  side = true (asynchronous
+// searches): the reduce runs on the side stream over one of two alternating
+// partials buffers, and `done` (if given) is recorded there after it.
 static int search_enqueue(iris_engine_t *e, const iris_db_t *db, uint64_t first, uint64_t n, double *dist_dev,
-                          Partial *dst) {
+                          Partial *dst, bool side = false, hipEvent_t done = nullptr) {
     iris_device *d = e->dev;
     if (n == 0) return 0;
     LaunchRange r{first, n};
     const bool tiles = db->k.layout == IRIS_LAYOUT_TILES;
     const uint32_t np = tiles ? mfma_search_partials(r) : search_partials(r);
-    CHK(ensure(d->partials, (size_t)std::max<uint32_t>(np, 1) * sizeof(Partial)));
+    const size_t pbytes = (size_t)std::max<uint32_t>(np, 1) * sizeof(Partial);
+    DevBuf *buf = &d->partials;
+    int b = 0;
+    if (side) {
+        if (!d->aux) HIPCHK(hipStreamCreateWithFlags(&d->aux, hipStreamNonBlocking));
+        b = d->apart_next;
+        d->apart_next ^= 1;
+        buf = &d->apart[b];
+        for (hipEvent_t *ev : {&d->apart_read[b], &d->apart_written[b]})
+            if (!*ev) HIPCHK(hipEventCreateWithFlags(ev, hipEventDisableTiming));
+        // the reduce that last read this buffer (two searches ago) precedes the overwrite
+        HIPCHK(hipStreamWaitEvent(d->stream, d->apart_read[b], 0));
+    }
+    CHK(ensure(*buf, pbytes));
+    Partial *part = (Partial *)buf->p;
     uint32_t written = 0;
     CHK(timed(d, "template_search", n, [&] {
-        return tiles ? launch_template_mfma_search(d->stream, db->data, e->qfrag, r, dist_dev, (Partial *)d->partials.p, &written)
-                     : launch_template_search(d->stream, db->data, e->qtab, r, dist_dev, (Partial *)d->partials.p, &written);
+        return tiles ? launch_template_mfma_search(d->stream, db->data, e->qfrag, r, dist_dev, part, &written)
+                     : launch_template_search(d->stream, db->data, e->qtab, r, dist_dev, part, &written);
     }));
-    // the reduce writes the winner straight into pinned host memory: no copy before the wait
-    return timed(d, "reduce", written, [&] { return launch_reduce(d->stream, (Partial *)d->partials.p, written, dst); });
+    if (!side)  // the reduce writes the winner straight into pinned host memory: no copy before the wait
+        return timed(d, "reduce", written, [&] { return launch_reduce(d->stream, part, written, dst); });
+    HIPCHK(hipEventRecord(d->apart_written[b], d->stream));
+    HIPCHK(hipStreamWaitEvent(d->aux, d->apart_written[b], 0));
+    CHK(timed(d, "reduce", written, [&] { return launch_reduce(d->aux, part, written, dst); }, d->aux));
+    HIPCHK(hipEventRecord(d->apart_read[b], d->aux));
+    if (done) HIPCHK(hipEventRecord(done, d->aux));
+    return 0;
 }
 
 static int search_locked(iris_engine_t *e, const iris_db_t *db, uint64_t first, uint64_t n, uint64_t index_base,
@@ -798,12 +827,11 @@ int iris_template_search_async(iris_engine_t *e, const iris_db_t *db, uint64_t f
     p->n = n;
     p->base = index_base + first;
     int rc = take_result_slot(d, &p->slot);
-    if (rc == 0) rc = search_enqueue(e, db, first, n, nullptr, p->slot);
     if (rc == 0 && n > 0) {
         p->ev = take_event(d);
         if (!p->ev) rc = fail(IRIS_E_HIP, "hipEventCreate failed");
-        else if (hipEventRecord(p->ev, d->stream) != hipSuccess) rc = fail(IRIS_E_HIP, "hipEventRecord failed");
     }
+    if (rc == 0) rc = search_enqueue(e, db, first, n, nullptr, p->slot, true, p->ev);
     if (rc != 0) {
         if (p->slot) d->free_slots.push_back(p->slot);
         if (p->ev) d->event_pool.push_back(p->ev);

@@ -74,6 +74,13 @@ struct iris_device {
     // pinned result slots of asynchronous searches (iris_template_search_async)
     std::vector<iris::Partial *> free_slots;
     std::vector<void *> slot_blocks;
+    // asynchronous searches reduce on a side stream, so the next search starts as soon as
+    // this one's kernel ends: partials alternate between two buffers, each guarded by the
+    // event recorded after the last reduce that read it (created on first use)
+    hipStream_t aux = nullptr;
+    DevBuf apart[2];
+    hipEvent_t apart_read[2] = {nullptr, nullptr}, apart_written[2] = {nullptr, nullptr};
+    int apart_next = 0;
     // handles alive on this device (1 for the device handle itself + 1 per database
     // and engine handle): the device is torn down when the last one is released,
     // so handles may be destroyed in any order
@@ -167,18 +174,19 @@ inline hipEvent_t take_event(iris_device *d) {
 
 // Runs `launch` on the device stream, bracketed by HIP events when profiling.
 template <class F>
-int timed(iris_device *d, const char *name, uint64_t items, F &&launch) {
+int timed(iris_device *d, const char *name, uint64_t items, F &&launch, hipStream_t stream = nullptr) {
+    if (!stream) stream = d->stream;
     hipEvent_t a = nullptr, b = nullptr;
     if (d->profiling) {
         a = take_event(d);
         b = take_event(d);
-        if (a && b) HIPCHK(hipEventRecord(a, d->stream));
+        if (a && b) HIPCHK(hipEventRecord(a, stream));
     }
     int rc = launch();
     if (rc != 0) return fail(IRIS_E_HIP, std::string("kernel launch failed: ") + name + ": " +
                                              hipGetErrorString(hipGetLastError()));
     if (d->profiling && a && b) {
-        HIPCHK(hipEventRecord(b, d->stream));
+        HIPCHK(hipEventRecord(b, stream));
         d->pending.push_back(Pending{name, a, b, items});
     }
     return 0;
@@ -207,6 +215,7 @@ inline void fold_done(iris_device *d) {
 // Waits for the stream, then folds recorded kernel times into the stats.
 inline int sync(iris_device *d) {
     HIPCHK(hipStreamSynchronize(d->stream));
+    if (d->aux) HIPCHK(hipStreamSynchronize(d->aux));
     fold_done(d);
     return 0;
 }
