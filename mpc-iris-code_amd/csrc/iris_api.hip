@@ -85,10 +85,16 @@ int run_u16_engine(iris_engine *e, const iris_db *db, uint64_t first, uint64_t n
             CHK(timed(d, "masks", m, [&] {
                 return tiles ? launch_masks_mfma(d->stream, db->data, e->qfrag, r, o) : launch_masks(d->stream, db->data, e->qtab, r, o);
             }));
-        else
+        else {
+            void *ws = nullptr;  // K-split workspace of small ranges
+            if (tiles && shares_workspace_bytes(r)) {
+                CHK(ensure(d->out_b, shares_workspace_bytes(r)));
+                ws = d->out_b.p;
+            }
             CHK(timed(d, "shares", m, [&] {
-                return tiles ? launch_shares_mfma(d->stream, db->data, e->qfrag, r, o) : launch_shares(d->stream, db->data, e->qtab, r, o);
+                return tiles ? launch_shares_mfma(d->stream, db->data, e->qfrag, r, o, ws) : launch_shares(d->stream, db->data, e->qtab, r, o);
             }));
+        }
         HIPCHK(hipMemcpyAsync(out + done * kRot, d->out_a.p, m * kRot * 2, hipMemcpyDeviceToHost, d->stream));
         CHK(sync(d));
     }
@@ -596,11 +602,17 @@ int iris_engine_batch_process_device(iris_engine_t *e, const iris_db_t *db, uint
             return tiles ? launch_masks_mfma(d->stream, db->data, e->qfrag, r, out_device)
                          : launch_masks(d->stream, db->data, e->qtab, r, out_device);
         }));
-    else
+    else {
+        void *ws = nullptr;  // K-split workspace of small ranges
+        if (tiles && shares_workspace_bytes(r)) {
+            CHK(ensure(d->out_b, shares_workspace_bytes(r)));
+            ws = d->out_b.p;
+        }
         CHK(timed(d, "shares", n, [&] {
-            return tiles ? launch_shares_mfma(d->stream, db->data, e->qfrag, r, out_device)
+            return tiles ? launch_shares_mfma(d->stream, db->data, e->qfrag, r, out_device, ws)
                          : launch_shares(d->stream, db->data, e->qtab, r, out_device);
         }));
+    }
     return sync(d);
 }
 

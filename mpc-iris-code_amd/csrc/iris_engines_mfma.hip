@@ -14,6 +14,7 @@
 //   unused 32nd A row is all ones) recombine exactly mod 2^16.
 //   |S| <= 2 * 12800 * 128^2 < 2^31.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 
 #include "iris_device.hpp"
 
@@ -105,11 +106,10 @@ enum { MASKS_OUT = 0, MASKS_RESOLVE = 1 };
 // denominators still in its accumulators (decode_distance, src/lib.rs:97-107),
 // and a running (fraction, lowest index) best per lane becomes one partial per
 // workgroup — the denominators never reach memory.
-template <int MODE>
+template <int MODE, int T = masks_tiles<MODE>()>
 __global__ void __launch_bounds__(256, kMasksBlocksPerCu)
     masks_mfma_kernel(const uint4 *__restrict__ db, const uint4 *__restrict__ qfrag, uint64_t tile0, uint64_t ntiles,
                       uint64_t first, uint64_t end, uint16_t *__restrict__ out, MaskResolve rs) {
-    constexpr int T = masks_tiles<MODE>();
     constexpr uint32_t kSteps = kMaskChunks / 4;  // 50 steps of 4 chunks
     __shared__ uint4 sq[kMaskFragUint4];
     __shared__ __attribute__((aligned(16))) uint16_t sh_out[kWaveSlots][1024];
@@ -249,18 +249,29 @@ __global__ void __launch_bounds__(256, kMasksBlocksPerCu)
     }
 }
 
+// Tiles per wave for a range of `ntiles` tiles: `big`, unless that leaves fewer waves
+// than the chip holds at two workgroups per CU — then one, for 8x / 4x / 2x the waves
+// (a participant-sized chunk of 20k records is only 625 tiles).  IRIS_TILES_PER_WAVE=1|4
+// pins the small or the big variant (tests run both).
+static int tiles_per_wave(uint64_t ntiles, int big) {
+    if (const char *f = getenv("IRIS_TILES_PER_WAVE")) return atoi(f) == 1 ? 1 : big;
+    return ntiles / big < (uint64_t)resident_blocks(2) * kWaveSlots ? 1 : big;
+}
+
 int launch_masks_mfma(void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *out) {
     if (r.n == 0) return 0;
-    const Tiles t = tiles_of(r, kMasksTiles);
+    const int tpw = tiles_per_wave(tiles_of(r, 1).ntiles, kMasksTiles);
+    const Tiles t = tiles_of(r, tpw);
     const uint64_t grid = std::min<uint64_t>(t.grid, resident_blocks(kMasksBlocksPerCu));
-    hipLaunchKernelGGL(masks_mfma_kernel<MASKS_OUT>, dim3((uint32_t)grid), dim3(256), 0, (hipStream_t)stream,
+    auto kern = tpw == 1 ? masks_mfma_kernel<MASKS_OUT, 1> : masks_mfma_kernel<MASKS_OUT>;
+    hipLaunchKernelGGL(kern, dim3((uint32_t)grid), dim3(256), 0, (hipStream_t)stream,
                        (const uint4 *)db, (const uint4 *)qfrag, t.tile0, t.ntiles, r.first, r.first + r.n, out,
                        MaskResolve{});
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 uint32_t masks_resolve_partials(LaunchRange r) {
-    const Tiles t = tiles_of(r, kResolveTiles);
+    const Tiles t = tiles_of(r, tiles_per_wave(tiles_of(r, 1).ntiles, kResolveTiles));
     return (uint32_t)std::min<uint64_t>(t.grid, resident_blocks(kMasksBlocksPerCu));
 }
 
@@ -268,7 +279,8 @@ int launch_masks_resolve(void *stream, const void *db, const void *qfrag, Launch
                          const uint16_t *const *shares, uint32_t parts, double *dist_out, Partial *partials) {
     if (r.n == 0) return 0;
     if (parts == 0 || parts > 8) return -1;
-    const Tiles t = tiles_of(r, kResolveTiles);
+    const int tpw = tiles_per_wave(tiles_of(r, 1).ntiles, kResolveTiles);
+    const Tiles t = tiles_of(r, tpw);
     const uint64_t grid = masks_resolve_partials(r);
     MaskResolve rs{};
     rs.aligned = true;
@@ -279,7 +291,8 @@ int launch_masks_resolve(void *stream, const void *db, const void *qfrag, Launch
     rs.parts = parts;
     rs.dist_out = dist_out;
     rs.partials = partials;
-    hipLaunchKernelGGL(masks_mfma_kernel<MASKS_RESOLVE>, dim3((uint32_t)grid), dim3(256), 0, (hipStream_t)stream,
+    auto kern = tpw == 1 ? masks_mfma_kernel<MASKS_RESOLVE, 1> : masks_mfma_kernel<MASKS_RESOLVE>;
+    hipLaunchKernelGGL(kern, dim3((uint32_t)grid), dim3(256), 0, (hipStream_t)stream,
                        (const uint4 *)db, (const uint4 *)qfrag, t.tile0, t.ntiles, r.first, r.first + r.n,
                        (uint16_t *)nullptr, rs);
     return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -293,13 +306,22 @@ __device__ __forceinline__ v16i mfma_i8(const uint4 &a, const uint4 &b, const v1
     return __builtin_amdgcn_mfma_i32_32x32x32_i8(av, bv, c, 0, 0, 0);
 }
 
+// split > 1 (small ranges): wave w computes K-slice w % split of tile group
+// w / split and writes its partial rows to out + slice * slice_stride; the
+// partial dot products add up mod 2^16 (shares_combine_kernel).  Slice 0 carries
+// the query-sum bias terms; the 16384 * K_slice terms vanish (K_slice = 64 * steps).
+template <int T = kSharesTiles>
 __global__ void __launch_bounds__(256, 2)
     shares_mfma_kernel(const uint4 *__restrict__ db, const uint4 *__restrict__ qfrag, const int2 *__restrict__ qsum,
-                       uint64_t tile0, uint64_t ntiles, uint64_t first, uint64_t end, uint16_t *__restrict__ out) {
-    constexpr int T = kSharesTiles;
-    constexpr int kSteps = kShareChunks / 2;  // 200 steps of 2 chunks
+                       uint64_t tile0, uint64_t ntiles, uint64_t first, uint64_t end, uint16_t *__restrict__ out,
+                       uint32_t split, uint64_t slice_stride) {
     const int lane = threadIdx.x & 63;
-    const uint64_t wave = (uint64_t)blockIdx.x * kWaveSlots + (threadIdx.x >> 6);
+    const uint64_t wave0 = (uint64_t)blockIdx.x * kWaveSlots + (threadIdx.x >> 6);
+    const uint32_t slice = (uint32_t)(wave0 % split);
+    const uint64_t wave = wave0 / split;
+    const int kSteps = kShareChunks / 2 / (int)split;  // steps of 2 chunks in this wave's K-slice
+    const int g0 = (int)slice * kSteps;
+    out += slice * slice_stride;
     const uint64_t tw = wave * T;
     if (tw >= ntiles) return;
     v16i s1[T], s2[T];
@@ -322,7 +344,7 @@ __global__ void __launch_bounds__(256, 2)
         uint4 qlo[2], qhi[2];
     };
     auto load = [&](Stage &st, int g) {
-        g = g < kSteps ? g : kSteps - 1;
+        g = g0 + (g < kSteps ? g : kSteps - 1);
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
             const int c = 2 * g + i;
@@ -359,7 +381,7 @@ __global__ void __launch_bounds__(256, 2)
         load(sb, g + 4);
         compute(sc);
     }
-    // 200 = 66 * 3 + 2
+    // kSteps = 3q + {0, 1, 2} (200 = 66 * 3 + 2)
     if (g < kSteps) compute(sa);
     if (g + 1 < kSteps) compute(sb);
 
@@ -374,7 +396,7 @@ __global__ void __launch_bounds__(256, 2)
         const int ehi = __shfl(s2[t][15], src) - elo;
         store_tile_rows(out, lds, (tile0 + tw + t) * kTile, first, end, tw + t < ntiles, lane, [&](int r) {
             const int k = (r & 3) + 8 * (r >> 2) + 4 * h;
-            const int2 qs = qsum[k < kRot ? k : 0];  // (sum q'_lo, sum q'_hi) of row k
+            const int2 qs = slice == 0 ? qsum[k < kRot ? k : 0] : make_int2(0, 0);  // (sum q'_lo, sum q'_hi) of row k
             // the 16384 * K terms vanish mod 2^16 (K = 12800)
             const uint32_t lo = (uint32_t)s1[t][r] + 128u * (uint32_t)elo + 128u * (uint32_t)qs.x;
             const uint32_t cross = (uint32_t)s2[t][r] + 128u * (uint32_t)ehi + 128u * (uint32_t)qs.x +
@@ -384,13 +406,62 @@ __global__ void __launch_bounds__(256, 2)
     }
 }
 
-int launch_shares_mfma(void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *out) {
+// K-slices for a range (1 = no split): enough one-tile waves to fill the chip, a
+// divisor of the 200 steps, at most 10.
+static uint32_t shares_split(LaunchRange r) {
+    const uint64_t ntiles = tiles_of(r, 1).ntiles;
+    if (tiles_per_wave(ntiles, kSharesTiles) != 1 || getenv("IRIS_TILES_PER_WAVE")) return 1;
+    const uint64_t waves = (uint64_t)resident_blocks(2) * kWaveSlots;
+    for (uint32_t s : {1u, 2u, 4u, 5u, 8u, 10u})
+        if (ntiles * s >= waves) return s;
+    return 10;
+}
+
+size_t shares_workspace_bytes(LaunchRange r) {
+    const uint32_t s = r.n ? shares_split(r) : 1;
+    return s > 1 ? (size_t)s * ((r.n * kRot + 7) / 8 * 8) * 2 : 0;  // 16-B aligned slices
+}
+
+// sum of `split` partial [n][31] u16 slices, mod 2^16
+__global__ void __launch_bounds__(256) shares_combine_kernel(const uint16_t *__restrict__ ws, uint64_t count,
+                                                             uint64_t stride, uint32_t split,
+                                                             uint16_t *__restrict__ out) {
+    typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (8 * i + 8 <= count && (((uintptr_t)out & 15) == 0)) {
+        u16x8 v = *(const u16x8 *)(ws + 8 * i);
+        for (uint32_t s = 1; s < split; ++s) v += *(const u16x8 *)(ws + s * stride + 8 * i);
+        *(u16x8 *)(out + 8 * i) = v;
+    } else {
+        for (uint64_t e = 8 * i; e < count && e < 8 * i + 8; ++e) {
+            uint16_t v = 0;
+            for (uint32_t s = 0; s < split; ++s) v = (uint16_t)(v + ws[s * stride + e]);
+            out[e] = v;
+        }
+    }
+}
+
+// ws: shares_workspace_bytes(r) bytes of device memory (16-B aligned), or null when that is 0
+int launch_shares_mfma(void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *out, void *ws) {
     if (r.n == 0) return 0;
-    const Tiles t = tiles_of(r, kSharesTiles);
+    const int tpw = tiles_per_wave(tiles_of(r, 1).ntiles, kSharesTiles);
+    const uint32_t split = ws ? shares_split(r) : 1;
+    const Tiles t = tiles_of(r, tpw);
     const int2 *qsum = (const int2 *)((const uint4 *)qfrag + kShareFragUint4);
-    hipLaunchKernelGGL(shares_mfma_kernel, dim3((uint32_t)t.grid), dim3(256), 0, (hipStream_t)stream,
-                       (const uint4 *)db, (const uint4 *)qfrag, qsum, t.tile0, t.ntiles, r.first, r.first + r.n, out);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
+    const uint64_t waves = (t.ntiles + tpw - 1) / tpw * split;
+    const uint64_t grid = (waves + kWaveSlots - 1) / kWaveSlots;
+    const uint64_t count = r.n * kRot, stride = (count + 7) / 8 * 8;
+    auto kern = tpw == 1 ? shares_mfma_kernel<1> : shares_mfma_kernel<>;
+    hipLaunchKernelGGL(kern, dim3((uint32_t)grid), dim3(256), 0, (hipStream_t)stream,
+                       (const uint4 *)db, (const uint4 *)qfrag, qsum, t.tile0, t.ntiles, r.first, r.first + r.n,
+                       split > 1 ? (uint16_t *)ws : out, split, split > 1 ? stride : 0);
+    if (hipGetLastError() != hipSuccess) return -1;
+    if (split > 1) {
+        hipLaunchKernelGGL(shares_combine_kernel, dim3((uint32_t)((count + 8 * 256 - 1) / (8 * 256))), dim3(256), 0,
+                           (hipStream_t)stream, (const uint16_t *)ws, count, stride, split, out);
+        if (hipGetLastError() != hipSuccess) return -1;
+    }
+    return 0;
 }
 
 // ------------------------------------------------------------------ TILES plumbing (masks, shares)

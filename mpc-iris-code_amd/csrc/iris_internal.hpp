@@ -221,7 +221,8 @@ int launch_batch(void *stream, const void *db, const void *qtiles, LaunchRange r
                  Partial *partials, Partial *out);
 int launch_resolver(void *stream, const uint16_t *const *shares, uint32_t parts, const uint16_t *denoms, uint64_t n,
                     double *dist_out, Partial *partials);
-int launch_shares_mfma(void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *out);
+size_t shares_workspace_bytes(LaunchRange r);  // > 0: launch_shares_mfma splits K over slices
+int launch_shares_mfma(void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *out, void *ws);
 int launch_template_search(void *stream, const void *db, const void *qtab, LaunchRange r, double *dist_out,
                            Partial *partials, uint32_t *n_partials);
 int launch_reduce(void *stream, Partial *partials, uint32_t n_partials, Partial *out);  // consumes partials

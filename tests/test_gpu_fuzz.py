@@ -50,7 +50,12 @@ def test_fuzz_templates(device, monkeypatch, tiles_per_wave):
             assert m.index == (idx + 5 + first if idx != 2**64 - 1 else idx), (total, first, n, layout)
 
 
-def test_fuzz_masks_and_shares(device):
+@pytest.mark.parametrize("tiles_per_wave", ["auto", "1", "4"])
+def test_fuzz_masks_and_shares(device, monkeypatch, tiles_per_wave):
+    # small ranges run one tile per wave (shares: split over K-slices) by default; "1" pins
+    # one tile per wave without the K-split, "4" the large-range variants
+    if tiles_per_wave != "auto":
+        monkeypatch.setenv("IRIS_TILES_PER_WAVE", tiles_per_wave)
     masks = oc.gen_templates(102, 0, 600)[:, 200:].copy()
     shares = np.random.default_rng(103).integers(0, 2**16, (300, 12800), dtype=np.uint16)
     for i, (total, first, n, layout) in enumerate(_draws(2, 300)):
