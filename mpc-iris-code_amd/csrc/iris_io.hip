@@ -19,7 +19,9 @@
 // src/json_stream.rs:53-60.
 #include <errno.h>
 #include <fcntl.h>
+#include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -120,14 +122,85 @@ int iris_db_load_file(iris_db_t *db, const char *path, uint64_t first, uint64_t 
 
     const uint64_t ch = std::max<uint64_t>(1, kIoChunkBytes / k.rec_bytes);
     const size_t chb = ch * k.rec_bytes;
-    Pinned host[2];
-    Event done[2];
-    for (int b = 0; b < 2; ++b) {
-        HIPCHK(hipHostMalloc(&host[b].p, chb, hipHostMallocDefault));
-        HIPCHK(hipEventCreateWithFlags(&done[b].e, hipEventDisableTiming));
-    }
     CHK(ensure(d->staging, 2 * chb));
     const uint64_t base = db->len;
+    Event done[2];
+    for (int b = 0; b < 2; ++b) HIPCHK(hipEventCreateWithFlags(&done[b].e, hipEventDisableTiming));
+    // Fast path: DMA straight out of the page cache.  The file is mapped and each
+    // chunk's pages are registered with the device (hipHostRegister, read-only) while
+    // the previous chunk copies; no host-side copy (measured 56 GB/s against 41 GB/s
+    // for pread into pinned buffers, tools/ubench_file_dma.cpp).  Falls back to the
+    // pread path if the mapping cannot be registered.
+    {
+        // Chunks end on page boundaries so that no page is registered twice: chunk sizes are
+        // multiples of `unit` records (unit * rec_bytes is a multiple of the page), after a
+        // first chunk that runs up to the first page-aligned record boundary.
+        const size_t page = (size_t)sysconf(_SC_PAGESIZE);
+        size_t g = page, r = k.rec_bytes;
+        while (r) { const size_t t = g % r; g = r; r = t; }  // gcd(page, rec_bytes)
+        const uint64_t unit = page / g;
+        const uint64_t pch = std::max<uint64_t>(unit, ch / unit * unit);
+        const uint64_t lead = (first + unit - 1) / unit * unit - first;  // records before an aligned boundary
+        const bool force_pread = getenv("IRIS_LOAD_PREAD") != nullptr;  // test hook: the fallback path
+        void *map = pch <= ch && !force_pread ? ::mmap(nullptr, (size_t)size, PROT_READ, MAP_SHARED, f.fd, 0)
+                                              : MAP_FAILED;
+        if (map != MAP_FAILED) {
+            // hipHostUnregister waits for the device, so windows stay registered (their
+            // registration overlapping the previous window's copy) and are released in
+            // batches of up to 4 GB
+            constexpr size_t kPinBatch = 4ull << 30;
+            std::vector<char *> reg;
+            size_t pinned = 0;
+            bool ok = true;
+            int rc = 0;
+            auto release = [&] {
+                if (reg.empty()) return hipSuccess;
+                const hipError_t e = hipStreamSynchronize(d->stream);
+                for (char *r : reg) (void)hipHostUnregister(r);
+                reg.clear();
+                pinned = 0;
+                return e;
+            };
+            uint64_t off = 0;
+            for (int i = 0; off < n; ++i) {
+                const int b = i & 1;
+                const uint64_t m = std::min<uint64_t>(i == 0 && lead ? lead : pch, n - off);
+                const size_t s0 = (size_t)(first + off) * k.rec_bytes, s1 = s0 + (size_t)m * k.rec_bytes;
+                char *a0 = (char *)map + s0 / page * page;
+                const size_t alen = std::min((s1 + page - 1) / page * page, (size_t)size) - s0 / page * page;
+                if (pinned + alen > kPinBatch && release() != hipSuccess) {
+                    rc = fail(IRIS_E_HIP, "load: stream synchronize");
+                    break;
+                }
+                if (hipHostRegister(a0, alen, hipHostRegisterReadOnly) != hipSuccess) {
+                    (void)hipGetLastError();
+                    ok = false;  // e.g. a file system whose pages cannot be pinned
+                    break;
+                }
+                reg.push_back(a0);
+                pinned += alen;
+                char *dst = (char *)d->staging.p + (size_t)b * chb;
+                const hipError_t e = hipMemcpyAsync(dst, (char *)map + s0, s1 - s0, hipMemcpyHostToDevice, d->stream);
+                if (e != hipSuccess) { rc = fail(IRIS_E_HIP, std::string("load: copy: ") + hipGetErrorString(e)); break; }
+                rc = timed(d, "pack", m, [&] { return launch_pack(d->stream, k, dst, db->data, base + off, m); });
+                if (rc != 0) break;
+                off += m;
+            }
+            const int src = sync(d);
+            (void)release();
+            ::munmap(map, (size_t)size);
+            if (rc != 0) return rc;
+            if (src != 0) return src;
+            if (ok) {
+                db->len = base + n;
+                if (loaded) *loaded = n;
+                return 0;
+            }
+            // not registrable: redo the whole range through pinned buffers below
+        }
+    }
+    Pinned host[2];
+    for (int b = 0; b < 2; ++b) HIPCHK(hipHostMalloc(&host[b].p, chb, hipHostMallocDefault));
     uint64_t off = 0;
     for (int i = 0; off < n; ++i, off += ch) {
         const int b = i & 1;

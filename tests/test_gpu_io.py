@@ -64,7 +64,28 @@ def test_capacity_checked(device, tmp_path):
         assert db.load_file(path, count=cap) == cap
 
 
-def test_multi_chunk_masks_file(device, tmp_path):
+@pytest.fixture(params=["mmap", "pread"])
+def load_path(request, monkeypatch):
+    """The loader's two paths: DMA from the registered page-cache mapping (default)
+    and pread into pinned buffers (the fallback, pinned by IRIS_LOAD_PREAD)."""
+    if request.param == "pread":
+        monkeypatch.setenv("IRIS_LOAD_PREAD", "1")
+    return request.param
+
+
+def test_multi_chunk_unaligned_templates(device, tmp_path, load_path):
+    """A 96-MB template file loaded from an unaligned first record: a short leading chunk up
+    to a page-aligned record boundary, then full chunks, then a ragged last one."""
+    n, first = 30_000, 13
+    recs = oc.gen_templates(91, 0, n)
+    path = tmp_path / "t.bin"
+    recs.tofile(path)
+    with ih.Database(device, ih.KIND_TEMPLATES, n) as db:
+        assert db.load_file(path, first=first) == n - first
+        assert (db.read(0, n - first) == recs[first:]).all()
+
+
+def test_multi_chunk_masks_file(device, tmp_path, load_path):
     """50 000 masks = 80 MB: more than one 64 MB pinned buffer, so the double
     buffering and chunk offsets are exercised; then the engine runs on it."""
     n = 50_000
@@ -74,8 +95,8 @@ def test_multi_chunk_masks_file(device, tmp_path):
     q = oc.gen_templates(78, 0, 1)[0]
     with ih.Database(device, ih.KIND_MASKS, n) as db, ih.MasksEngine(device, q[200:]) as eng:
         assert db.load_file(path) == n
-        idx = np.array([0, 1, 41942, 41943, 41944, n - 1])  # around the first chunk boundary
-        assert (db.read(0, n)[idx] == recs[idx]).all()
+        idx = np.array([0, 1, 41919, 41920, 41942, 41943, 41944, n - 1])  # around the chunk boundaries
+        assert (db.read(0, n) == recs).all()
         out = np.empty((n, ROT), np.uint16)
         eng.batch_process(out, db)
         assert (out[idx] == oc.masks_batch(q[200:], recs[idx])).all()
