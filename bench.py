@@ -37,6 +37,9 @@ import iris_hip as ih  # noqa: E402
 METRIC = "template comparisons/sec (query×rotations×DB) + % HBM roofline, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
 HBM_MEASURED_GBS = 6290.0    # MI355X_MICROARCH.md: float4 copy
+# best pure 16-B read stream over 32 GB on this part (tools/ubench_stream.hip,
+# profiles/r01_ubench_read_stream*.txt: 6.54-6.80 TB/s across boxes and runs)
+HBM_READ_CEILING_GBS = 6800.0
 # integer VALU issue ceiling for v_bcnt/v_bitop3 (16 lanes/clk/SIMD measured, tools/ubench_ops.hip)
 VALU_INT_PEAK_OPS = 256 * 4 * 16 * 2.4e9
 FP4_DENSE_PEAK_MACS = 10e15 / 2            # MI355X_MICROARCH.md: ~10 PF dense fp4
@@ -581,6 +584,7 @@ def main():
                 "avg_ms": avg_ms, "launches": launches,
                 "reduce_avg_ms": rms / max(1, launches),
                 "frac_of_measured_hbm": achieved / HBM_MEASURED_GBS,
+                "frac_of_read_ceiling": achieved / HBM_READ_CEILING_GBS,
                 "valu_int_frac": (VALU_OPS_PER_TEMPLATE * n / (avg_ms * 1e-3) / VALU_INT_PEAK_OPS
                                   if args.layout == "lanes" and args.workload == "search" else None),
                 "mfma_fp4_frac": (MFMA_MACS_PER_TEMPLATE * n * nq / (step_kernel_ms * 1e-3) / FP4_DENSE_PEAK_MACS
