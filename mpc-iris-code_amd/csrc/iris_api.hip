@@ -922,7 +922,8 @@ int iris_template_batch_engine_new(iris_device_t *d, const iris_template_t *quer
         *out = e;
         return 0;
     }
-    const uint32_t nqp = (nq + 3) / 4 * 4;  // padded to the kernel's query groups (zero tiles: no candidate)
+    const uint32_t qgs = batch_query_group();
+    const uint32_t nqp = (nq + qgs - 1) / qgs * qgs;  // padded to the kernel's query groups (zero tiles: no candidate)
     const size_t tile_bytes = (size_t)16 * kPlaneGroups * 64;
     CHK(engine_from_query(d, IRIS_KIND_TEMPLATES, queries, (size_t)nq * sizeof(iris_template_t), 0,
                           (size_t)nqp * tile_bytes, out, [&](void *stream, const void *q, uint32_t *, uint32_t *frag) {
@@ -952,7 +953,7 @@ int iris_template_batch_search(iris_engine_t *e, const iris_db_t *db, uint64_t f
     }
     LaunchRange r{first, n};
     const BatchGeometry geo = batch_geometry(r, e->nq);
-    const uint32_t nqp = geo.nqg * 4;
+    const uint32_t nqp = geo.nqg * batch_query_group();
     std::vector<Partial> res(nqp);
     if (n > 0) {
         CHK(ensure(d->partials, (size_t)nqp * geo.G * sizeof(Partial)));
@@ -1198,7 +1199,7 @@ int iris_query_table_sizes(int kind, uint32_t nq, size_t *tab_bytes, size_t *fra
     case IRIS_KIND_TEMPLATES:
         ARG(nq == 0 || nq > kBatchStreamMax, "nq must be 0 (single query) or a tiled batch (> 3 queries)");
         *tab_bytes = nq ? 0 : (size_t)kPlaneDwords * kTemplateTabStride * 4;
-        *frag_bytes = nq ? (size_t)(nq + 3) / 4 * 4 * 16 * kPlaneGroups * 64 : kTemplateFragDwords * 4;
+        *frag_bytes = nq ? (size_t)(nq + batch_query_group() - 1) / batch_query_group() * batch_query_group() * 16 * kPlaneGroups * 64 : kTemplateFragDwords * 4;
         return 0;
     case IRIS_KIND_MASKS:
         *tab_bytes = (size_t)kPlaneDwords * kSlotTabStride * 4;

@@ -29,7 +29,10 @@ namespace iris {
 typedef int v8i __attribute__((ext_vector_type(8)));
 typedef float v16f __attribute__((ext_vector_type(16)));
 
-constexpr int BQ = 4;                     // queries per workgroup
+#ifndef IRIS_BATCH_BQ
+#define IRIS_BATCH_BQ 4
+#endif
+constexpr int BQ = IRIS_BATCH_BQ;         // queries per workgroup (query group)
 #ifndef IRIS_BATCH_NW
 #define IRIS_BATCH_NW 8
 #endif
@@ -327,6 +330,8 @@ __global__ void __launch_bounds__(256) batch_reduce_kernel(const Partial *__rest
         out[q] = b;
     }
 }
+
+uint32_t batch_query_group() { return BQ; }
 
 BatchGeometry batch_geometry(LaunchRange r, uint32_t nq) {
     BatchGeometry g;

@@ -217,6 +217,7 @@ struct BatchGeometry {
     uint32_t xqg;     // > 0: XCD-aware grid, xqg query groups per XCD at a time (iris_batch.hip)
 };
 BatchGeometry batch_geometry(LaunchRange r, uint32_t nq);
+uint32_t batch_query_group();  // queries per batch_kernel query group (padding unit)
 int launch_batch(void *stream, const void *db, const void *qtiles, LaunchRange r, const BatchGeometry &g,
                  Partial *partials, Partial *out);
 int launch_resolver(void *stream, const uint16_t *const *shares, uint32_t parts, const uint16_t *denoms, uint64_t n,
