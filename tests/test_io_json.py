@@ -74,3 +74,35 @@ def test_missing_file(tmp_path):
     with pytest.raises(ih.IrisError) as ei:
         ih.read_templates_json(tmp_path / "absent.json")
     assert ei.value.code == -6
+
+
+def test_mutated_files_never_crash(tmp_path):
+    """Truncations and byte mutations of a valid file: the reader either returns records
+    that Python's decoder also accepts or raises IrisError — never crashes or reads past
+    the buffer (this test also runs against the host-ASan build of the library)."""
+    t = oc.gen_templates(5, 0, 3)
+    good = tmp_path / "g.json"
+    ih.write_templates_json(good, t)
+    base = good.read_bytes()
+    rng = np.random.default_rng(12)
+    path = tmp_path / "m.json"
+    cuts = [0, 1, 2, 15, len(base) // 2, len(base) - 2, len(base) - 1]
+    variants = [base[:c] for c in cuts]
+    alphabet = b'[]{}",: \n0123456789abcdefABCDEFxyz\\'
+    for _ in range(120):
+        b = bytearray(base)
+        for _ in range(int(rng.integers(1, 4))):
+            b[int(rng.integers(0, len(b)))] = alphabet[int(rng.integers(0, len(alphabet)))]
+        variants.append(bytes(b))
+    for v in variants:
+        path.write_bytes(v)
+        try:
+            got = ih.read_templates_json(path)
+        except ih.IrisError as e:
+            assert e.code in (-7, -6), e
+            continue
+        try:
+            want = _py_decode(path)
+        except (ValueError, KeyError, TypeError):
+            continue  # the reader is more lenient than json.load on e.g. trailing bytes
+        assert got.shape[0] == want.shape[0] and (got == want).all()
