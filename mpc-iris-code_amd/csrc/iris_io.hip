@@ -136,9 +136,13 @@ int iris_db_load_file(iris_db_t *db, const char *path, uint64_t first, uint64_t 
         // multiples of `unit` records (unit * rec_bytes is a multiple of the page), after a
         // first chunk that runs up to the first page-aligned record boundary.
         const size_t page = (size_t)sysconf(_SC_PAGESIZE);
-        size_t g = page, r = k.rec_bytes;
-        while (r) { const size_t t = g % r; g = r; r = t; }  // gcd(page, rec_bytes)
-        const uint64_t unit = page / g;
+        size_t gcd = page, rem = k.rec_bytes;
+        while (rem) {
+            const size_t t = gcd % rem;
+            gcd = rem;
+            rem = t;
+        }
+        const uint64_t unit = page / gcd;
         const uint64_t pch = std::max<uint64_t>(unit, ch / unit * unit);
         const uint64_t lead = (first + unit - 1) / unit * unit - first;  // records before an aligned boundary
         const bool force_pread = getenv("IRIS_LOAD_PREAD") != nullptr;  // test hook: the fallback path
@@ -156,7 +160,7 @@ int iris_db_load_file(iris_db_t *db, const char *path, uint64_t first, uint64_t 
             auto release = [&] {
                 if (reg.empty()) return hipSuccess;
                 const hipError_t e = hipStreamSynchronize(d->stream);
-                for (char *r : reg) (void)hipHostUnregister(r);
+                for (char *w : reg) (void)hipHostUnregister(w);
                 reg.clear();
                 pinned = 0;
                 return e;
