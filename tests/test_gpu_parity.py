@@ -435,6 +435,33 @@ def test_max_capacity_search(device):
             assert bits_eq(m.distance, want)
 
 
+def test_max_capacity_masks(device):
+    """A masks database filling the HBM beside its full [n][31] output (~150M masks, 240 GB
+    + 9 GB): the whole range into device memory, then sampled rows at both ends and across
+    the 2^32-record-byte boundaries against the oracle, and a host-output sub-range at the
+    end of the database."""
+    free, _ = device.memory()
+    n = min(150_000_000, (free - (12 << 30)) // (1600 + 62))
+    assert n > 60_000_000, f"only {free / 1e9:.0f} GB free"
+    seed = 4711
+    q = oc.gen_templates(99, 0, 1)[0][200:]
+    with ih.Database(device, ih.KIND_MASKS, n) as db, ih.MasksEngine(device, q) as eng:
+        db.generate(n, seed)
+        out = device.alloc(n * ROT * 2)
+        try:
+            eng.batch_process_device(db, out)
+            for lo in (0, (1 << 32) // 1600 - 500, n // 2, n - 1000):
+                rows = np.empty((1000, ROT), np.uint16)
+                device.d2h(rows, out + lo * ROT * 2)
+                want = oc.masks_batch(q, oc.gen_templates(seed, lo, 1000)[:, 200:])
+                assert (rows == want).all(), lo
+        finally:
+            device.free(out)
+        tail = np.empty((777, ROT), np.uint16)
+        eng.batch_process(tail, db, first=n - 777, n=777)
+        assert (tail == oc.masks_batch(q, oc.gen_templates(seed, n - 777, 777)[:, 200:])).all()
+
+
 # ---------------------------------------------------------------- resolver (src/main.rs:597-621)
 
 
