@@ -64,6 +64,9 @@ def parse():
                     help="search: wait for each step's result before enqueueing the next query "
                          "(default: the next query's search is enqueued before this one's result is "
                          "waited for and exchanged)")
+    ap.add_argument("--prewarm-s", type=float, default=1.0,
+                    help="seconds of untimed steps before the warmup steps (the GPU reaches its steady "
+                         "streaming rate after ~0.5-1 s of load)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--layout", choices=["tiles", "lanes"], default="tiles",
                     help="tiles = MFMA kernels (default), lanes = VALU kernels")
@@ -478,6 +481,15 @@ def main():
             pend = p
         return finish(pend) if pend is not None else m
 
+    # pre-warm: the GPU needs ~0.5-1 s of sustained streaming before the search reaches its
+    # steady rate (tools/engine_variance.py: the first ~100 searches of a process run up to 4 %
+    # slower, then settle); untimed, like the warmup steps, and reported under "setup"
+    t_pre = time.perf_counter()
+    prewarm_steps = 0
+    while time.perf_counter() - t_pre < args.prewarm_s:
+        m = run_steps(1)
+        prewarm_steps += 1
+    prewarm_s = time.perf_counter() - t_pre
     if args.warmup:
         m = run_steps(args.warmup)
     dev.reset_stats()
@@ -599,7 +611,7 @@ def main():
             "check": ({"planted_index": plant_global, "found_index": int(m.index), "rotation": int(m.rotation),
                        "distance": m.distance, "ok": bool(ok)} if args.workload in ("search", "batch")
                       else {"sampled_outputs_checked": 64, "ok": bool(ok)}),
-            "setup": {"generate_s": gen_s},
+            "setup": {"generate_s": gen_s, "prewarm_s": prewarm_s, "prewarm_steps": prewarm_steps},
         }
         print(json.dumps(line))
     if out_dev is not None:
