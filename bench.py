@@ -434,19 +434,19 @@ def main():
         else:
             dev.synchronize()
 
-    def step():
+    def step(exchange=True):
         e = eng if eng is not None else new_engine()
         try:
             if args.workload == "batch":
                 ms = e.search(db, index_base=lo)
-                if dist is not None:
+                if dist is not None and exchange:
                     ms = iris_dist.allgather_merge_many(ms, device=xdev)
                 return ms
             if args.workload != "search":
                 e.batch_process_device(db, out_dev)  # [n][31] u16 left in HBM
                 return None
             m = e.search(db, index_base=lo)
-            if dist is not None:
+            if dist is not None and exchange:
                 m = iris_dist.allgather_merge(m, device=xdev)
             return m
         finally:
@@ -484,10 +484,11 @@ def main():
     # pre-warm: the GPU needs ~0.5-1 s of sustained streaming before the search reaches its
     # steady rate (tools/engine_variance.py: the first ~100 searches of a process run up to 4 %
     # slower, then settle); untimed, like the warmup steps, and reported under "setup"
+    # local searches only: ranks run different numbers of them, so no collective may be inside
     t_pre = time.perf_counter()
     prewarm_steps = 0
     while time.perf_counter() - t_pre < args.prewarm_s:
-        m = run_steps(1)
+        step(exchange=False)
         prewarm_steps += 1
     prewarm_s = time.perf_counter() - t_pre
     if args.warmup:
