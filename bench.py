@@ -271,6 +271,9 @@ def run_aux(args, dev):
         kname, unit = "prepare", "templates/s"
         rec_bytes = 3200 + P * 25600  # template in, P shares out (the prepare kernel)
         workload = f"prepare: EncodedBits::share({P}) of encode(t) + masks, ChaCha20 counter mode (src/main.rs:333-361)"
+    t_pre = time.perf_counter()  # untimed pre-warm, as in main()
+    while time.perf_counter() - t_pre < args.prewarm_s:
+        step()
     for _ in range(args.warmup):
         m = step()
     dev.reset_stats()
