@@ -37,9 +37,10 @@ import iris_hip as ih  # noqa: E402
 METRIC = "template comparisons/sec (query×rotations×DB) + % HBM roofline, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
 HBM_MEASURED_GBS = 6290.0    # MI355X_MICROARCH.md: float4 copy
-# best pure 16-B read stream over 32 GB on this part (tools/ubench_stream.hip,
-# profiles/r01_ubench_read_stream*.txt: 6.54-6.80 TB/s across boxes and runs)
-HBM_READ_CEILING_GBS = 6800.0
+# best pure 16-B read stream over 32 GB on this part after a 1.5-s warm-up
+# (tools/ubench_stream.hip, profiles/r01_ubench_read_stream_warm.txt: 7.02 TB/s at 12 waves
+# per CU, 6.78 TB/s at the search kernel's 8)
+HBM_READ_CEILING_GBS = 7016.0
 # integer VALU issue ceiling for v_bcnt/v_bitop3 (16 lanes/clk/SIMD measured, tools/ubench_ops.hip)
 VALU_INT_PEAK_OPS = 256 * 4 * 16 * 2.4e9
 FP4_DENSE_PEAK_MACS = 10e15 / 2            # MI355X_MICROARCH.md: ~10 PF dense fp4

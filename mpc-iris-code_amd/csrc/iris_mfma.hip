@@ -32,7 +32,14 @@ typedef float v16f __attribute__((ext_vector_type(16)));
 
 constexpr int kTileRecs = 32;
 constexpr int kTileUint4 = kPlaneGroups * 64;  // 6400 uint4 = 102400 B per tile
-constexpr int kMfmaTiles = 4;                  // tiles per wave (128 templates)
+#ifndef IRIS_MFMA_TILES
+#define IRIS_MFMA_TILES 4
+#endif
+#ifndef IRIS_MFMA_WGS
+#define IRIS_MFMA_WGS 2
+#endif
+constexpr int kMfmaTiles = IRIS_MFMA_TILES;    // tiles per wave (4: 128 templates)
+constexpr int kMfmaWgs = IRIS_MFMA_WGS;        // workgroups per CU the register budget allows
 
 __device__ __forceinline__ v16f mfma_fp4(const v8i &a, const v8i &b, const v16f &c) {
     // cbsz = blgp = 4: both operands e2m1; scales 127 = 2^0 (e8m0)
@@ -71,7 +78,7 @@ __device__ __forceinline__ uint4 stream_load(const uint4 *p) {
 enum { MF_COUNTS = 0, MF_SEARCH = 1 };
 
 template <int MODE, int T = kMfmaTiles>
-__global__ void __launch_bounds__(256, 2)
+__global__ void __launch_bounds__(256, kMfmaWgs)
     template_mfma_kernel(const uint4 *__restrict__ db, const uint4 *__restrict__ qfrag, uint64_t tile0,
                          uint64_t ntiles, uint64_t first, uint64_t end, uint16_t *__restrict__ num_out,
                          uint16_t *__restrict__ den_out, double *__restrict__ dist_out,
