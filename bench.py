@@ -236,7 +236,7 @@ def run_aux(args, dev):
 
         kname, unit = "pack", "templates/s"
         rec_bytes = 2 * 3200  # the transpose kernel: reference layout in, TILES out
-        workload = "raw template file (page cache) -> pinned double-buffered H2D -> TILES transpose (src/main.rs:386-400)"
+        workload = "raw template file (page cache) -> DMA from registered page-cache windows -> TILES transpose (src/main.rs:386-400)"
     elif args.workload in ("host-shares", "host-masks"):
         shares_wl = args.workload == "host-shares"
         n = min(args.n_per_gpu, 200_000 if shares_wl else 2_000_000)  # 5.1 GB / 3.2 GB of host records

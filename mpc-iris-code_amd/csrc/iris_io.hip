@@ -8,10 +8,11 @@
 //   *.masks      concatenated Bits        (1600 B, u64 limbs)
 //   *.share-i    concatenated EncodedBits (25600 B, u16 elements)
 //   templates    concatenated Template    (3200 B, pattern then mask)
-// Loading streams the file through two pinned host buffers: reader threads
-// fill one buffer (pread) while the device copies the other and transposes
-// it into the TILES layout, so the load runs at the slower of file read and
-// PCIe rather than their sum.
+// Loading DMAs the file straight out of the page cache (its mapped pages are
+// registered with the device chunk by chunk) into a device staging slot that
+// the pack kernel transposes into the TILES layout; if the pages cannot be
+// registered, reader threads fill two pinned buffers (pread) while the device
+// copies the other, so the load runs at the slower of file read and PCIe.
 //
 // JSON: a top-level array of {"pattern": hex, "mask": hex} objects — serde's
 // form of Template with Bits as the lowercase hex of its 1600 LE bytes
