@@ -255,7 +255,8 @@ def run_aux(args, dev):
         kname, unit = ("shares" if shares_wl else "masks"), "records/s"
         rec_bytes = host.shape[1] * host.itemsize
         workload = (f"{'DistanceEngine' if shares_wl else 'MasksEngine'}::batch_process(out, db: &[T]) over a host "
-                    "slice (src/lib.rs:42-52, 69-79): pinned 2-slot pipeline, PCIe-inclusive")
+                    "slice (src/lib.rs:42-52, 69-79): H2D of the pageable slice (runtime-staged) + TILES pack per "
+                    "256-MB chunk, then the engine kernel; PCIe-inclusive")
     else:
         n = min(args.n_per_gpu, 1_000_000)  # 3 share DBs of 1M = 77 GB
         tdb = ih.Database(dev, ih.KIND_TEMPLATES, n)
