@@ -84,6 +84,8 @@ def parse():
                          "load = raw template file (page-cached) -> resident TILES database; "
                          "host-shares / host-masks = batch_process over host slices (the reference signature)")
     ap.add_argument("--parties", type=int, default=3, help="parties (workloads resolver, prepare)")
+    ap.add_argument("--rounds", type=int, default=12, choices=[8, 12, 20],
+                    help="ChaCha rounds for --workload prepare (12 = the reference's thread_rng, rand 0.8.5)")
     return ap.parse_args()
 
 
@@ -268,11 +270,12 @@ def run_aux(args, dev):
         def step():
             for db in sdbs + [mdb]:
                 db.truncate(0)
-            ih.prepare_shares(tdb, sdbs, mdb, key=key)
+            ih.prepare_shares(tdb, sdbs, mdb, key=key, rounds=args.rounds)
 
         kname, unit = "prepare", "templates/s"
         rec_bytes = 3200 + P * 25600  # template in, P shares out (the prepare kernel)
-        workload = f"prepare: EncodedBits::share({P}) of encode(t) + masks, ChaCha20 counter mode (src/main.rs:333-361)"
+        workload = (f"prepare: EncodedBits::share({P}) of encode(t) + masks, ChaCha{args.rounds} counter mode "
+                    "(src/main.rs:333-361)")
     t_pre = time.perf_counter()  # untimed pre-warm, as in main()
     while time.perf_counter() - t_pre < args.prewarm_s:
         step()
@@ -331,7 +334,7 @@ def run_aux(args, dev):
         "scaling": "weak", "vs_baseline": None,
         "dtype": {"resolver": "u16 (wrapping share sums) -> u32 cross-multiplied fractions",
                   "resolve-masks": "fp4 e2m1 MFMA -> f32 denominators, u16 share sums",
-                  "prepare": "u32 (ChaCha20 keystream) -> u16 shares",
+                  "prepare": "u32 (ChaCha keystream) -> u16 shares",
                   "load": "u8 (record bytes)",
                   "host-shares": "i8 MFMA -> i32 (u16 shares as biased byte planes)",
                   "host-masks": "fp4 e2m1 MFMA -> f32 (0/1 products)"}[args.workload],

@@ -174,15 +174,17 @@ int iris_templates_write_json(const char *path, const iris_template_t *templates
  * encode(template) (src/encoded_bits.rs:23-38, src/lib.rs:16-26): parties-1
  * uniformly random shares and a last one = encode - sum(rest) mod 2^16 —
  * and, if masks is not NULL, the template's mask to the masks database.
- * Randomness: ChaCha20 in counter mode under the caller's 256-bit key and
- * 64-bit nonce (key from a CSPRNG such as getrandom; the reference uses
- * rand's thread_rng): share j < parties-1 of global template index
+ * Randomness: ChaCha with `rounds` = 8, 12 or 20 (Bernstein's 64-bit-nonce
+ * form) in counter mode under the caller's 256-bit key and 64-bit nonce (key
+ * from a CSPRNG such as getrandom).  The reference uses rand 0.8.5's
+ * thread_rng, a reseeded ChaCha12 (rand_chacha 0.3.1): 12 is its round count
+ * and the recommended value.  Share j < parties-1 of global template index
  * g = index_base + first + i, elements 32b..32b+31 = the 32 LE u16 of
  * keystream block (g*(parties-1) + j)*400 + b.  Deterministic given
  * (key, nonce, g), so shards prepared on different GPUs never reuse a block. */
 int iris_prepare_shares(const iris_db_t *templates, uint64_t first, uint64_t n, uint64_t index_base,
-                        const uint8_t key[32], uint64_t nonce, uint32_t parties, iris_db_t *const *shares,
-                        iris_db_t *masks);
+                        const uint8_t key[32], uint64_t nonce, uint32_t rounds, uint32_t parties,
+                        iris_db_t *const *shares, iris_db_t *masks);
 
 /* ---------------------------------------------------------------- engines
  * MasksEngine::new(&Bits)            src/lib.rs:60-67

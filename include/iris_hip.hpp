@@ -497,11 +497,11 @@ inline Match resolver_search(const std::vector<std::vector<Rotations>> &shares, 
 // `prepare` (src/main.rs:333-361) on the device: shares of encode(templates[first..first+n))
 inline void prepare_shares(const Database &templates, uint64_t first, uint64_t n, const std::array<uint8_t, 32> &key,
                            const std::vector<Database *> &shares, Database *masks = nullptr, uint64_t nonce = 0,
-                           uint64_t index_base = 0) {
+                           uint64_t index_base = 0, uint32_t rounds = 12) {
     std::vector<iris_db_t *> h;
     for (Database *d : shares) h.push_back(d->handle());
-    check(iris_prepare_shares(templates.handle(), first, n, index_base, key.data(), nonce, (uint32_t)h.size(), h.data(),
-                              masks ? masks->handle() : nullptr));
+    check(iris_prepare_shares(templates.handle(), first, n, index_base, key.data(), nonce, rounds, (uint32_t)h.size(),
+                              h.data(), masks ? masks->handle() : nullptr));
 }
 
 }  // namespace mpc_iris_code

@@ -177,14 +177,16 @@ int launch_query_template(void *stream, const void *q, uint32_t *tab, uint32_t *
 int launch_query_masks(void *stream, const void *qmask, uint32_t *tab, uint32_t *frag);
 int launch_query_shares(void *stream, const void *q, uint32_t *tab, uint32_t *frag);
 int launch_query_tiles(void *stream, const void *queries, uint32_t nq, uint32_t nqp, uint32_t *tiles);
+// rounds: ChaCha8 / 12 / 20 (anything else: -1)
 int launch_prepare_shares(void *stream, const void *templates, uint64_t m, uint64_t g0, const uint8_t key[32],
-                          uint64_t nonce, uint32_t parties, void *shares);
+                          uint64_t nonce, uint32_t rounds, uint32_t parties, void *shares);
 constexpr int kMaxPrepParties = 64;
 int launch_prepare_shares_tiles(void *stream, const void *templates, uint64_t m, uint64_t g0, const uint8_t key[32],
-                                uint64_t nonce, uint32_t parties, void *const *dbs, const uint64_t *t_first);
+                                uint64_t nonce, uint32_t rounds, uint32_t parties, void *const *dbs,
+                                const uint64_t *t_first);
 int launch_prepare_direct(void *stream, const void *tdb, uint64_t t_first, uint64_t m, uint64_t g0,
-                          const uint8_t key[32], uint64_t nonce, uint32_t parties, void *const *dbs,
-                          const uint64_t *s_first, void *masks, uint64_t m_first);
+                          const uint8_t key[32], uint64_t nonce, uint32_t rounds, uint32_t parties,
+                          void *const *dbs, const uint64_t *s_first, void *masks, uint64_t m_first);
 int launch_unpack(void *stream, const KindInfo &k, const void *db, void *staging, uint64_t t_first, uint64_t n);
 int launch_generate(void *stream, const KindInfo &k, void *db, uint64_t t_first, uint64_t n, uint64_t seed,
                     uint64_t global_index0);

@@ -434,9 +434,10 @@ int iris_templates_write_json(const char *path, const iris_template_t *t, uint64
 // ------------------------------------------------------------------ share preparation
 
 extern "C" int iris_prepare_shares(const iris_db_t *templates, uint64_t first, uint64_t n, uint64_t index_base,
-                                   const uint8_t key[32], uint64_t nonce, uint32_t parties,
+                                   const uint8_t key[32], uint64_t nonce, uint32_t rounds, uint32_t parties,
                                    iris_db_t *const *shares, iris_db_t *masks) {
     ARG(templates && key && shares, "NULL argument");
+    ARG(rounds == 8 || rounds == 12 || rounds == 20, "rounds must be 8, 12 or 20 (ChaCha8/12/20)");
     ARG(parties >= 1 && parties <= 64, "parties must be 1..64 (EncodedBits::share asserts n > 0)");
     ARG(templates->k.kind == IRIS_KIND_TEMPLATES, "iris_prepare_shares needs a template database");
     iris_device *d = templates->dev;
@@ -465,7 +466,7 @@ extern "C" int iris_prepare_shares(const iris_db_t *templates, uint64_t first, u
             sf[j] = shares[j]->len;
         }
         CHK(timed(d, "prepare", n, [&] {
-            return launch_prepare_direct(d->stream, templates->data, first, n, index_base + first, key, nonce, parties,
+            return launch_prepare_direct(d->stream, templates->data, first, n, index_base + first, key, nonce, rounds, parties,
                                          dbp.data(), sf.data(), masks ? masks->data : nullptr, masks ? masks->len : 0);
         }));
         CHK(sync(d));
@@ -499,12 +500,12 @@ extern "C" int iris_prepare_shares(const iris_db_t *templates, uint64_t first, u
         if (direct) {
             for (uint32_t j = 0; j < parties; ++j) tf[j] = base[j] + off;
             CHK(timed(d, "prepare", m, [&] {
-                return launch_prepare_shares_tiles(d->stream, st_t, m, index_base + first + off, key, nonce, parties,
+                return launch_prepare_shares_tiles(d->stream, st_t, m, index_base + first + off, key, nonce, rounds, parties,
                                                    dbp.data(), tf.data());
             }));
         } else {
             CHK(timed(d, "prepare", m, [&] {
-                return launch_prepare_shares(d->stream, st_t, m, index_base + first + off, key, nonce, parties, st_s);
+                return launch_prepare_shares(d->stream, st_t, m, index_base + first + off, key, nonce, rounds, parties, st_s);
             }));
             for (uint32_t j = 0; j < parties; ++j)
                 CHK(timed(d, "pack", m, [&] {

@@ -4,15 +4,19 @@
 // encode(template) (EncodedBits::share, src/encoded_bits.rs:23-38): count-1
 // uniformly random EncodedBits and a last share = encode - sum(rest), mod 2^16.
 //
-// Randomness: ChaCha20 (D. J. Bernstein's original: 64-bit nonce, 64-bit
-// block counter) keyed by the caller's 256-bit key, in counter mode, so every
-// (template, share, 64-byte block) is an independent thread of work:
+// Randomness: ChaCha (D. J. Bernstein's original: 64-bit nonce, 64-bit block
+// counter) with 8, 12 or 20 rounds, keyed by the caller's 256-bit key, in
+// counter mode, so every (template, share, 64-byte block) is an independent
+// thread of work:
 //   block counter = (g * (parties-1) + j) * 400 + b   (g = global template index)
 //   share j, elements 32b .. 32b+31 = the block's 32 little-endian u16.
-// The reference draws from rand's thread_rng (a ChaCha-based CSPRNG seeded
-// from the OS); its stream is unseeded and not reproducible, so parity here is
-// against the oracle's restatement of this derivation (oracle/iris_oracle.c,
-// pinned by the RFC 8439 ChaCha20 vectors) plus the share-sum identity.
+// The reference draws from rand 0.8.5's thread_rng (src/encoded_bits.rs:27),
+// whose core is rand_chacha 0.3.1's ChaCha12 (same block function, 12 rounds;
+// Cargo.lock) reseeded from the OS; the default here is therefore 12 rounds.
+// Its stream is unseeded and not reproducible, so parity here is against the
+// oracle's restatement of this derivation (oracle/iris_oracle.c, pinned by the
+// RFC 8439 ChaCha20 vectors and the published ChaCha8/12 zero-key vectors)
+// plus the share-sum identity.
 //
 // One thread per (template, block b): element block b of encode(t) needs
 // pattern and mask dword b only (element i = bit i, LE limbs), so the thread
@@ -40,8 +44,10 @@ __device__ __forceinline__ uint32_t rotl(uint32_t x, int r) { return __builtin_r
     c += d;                 \
     b = rotl(b ^ c, 7);
 
-__device__ __forceinline__ void chacha20_block(const ChachaKey &key, uint64_t nonce, uint64_t counter,
-                                               uint32_t out[16]) {
+// DR double rounds: 4 = ChaCha8, 6 = ChaCha12, 10 = ChaCha20
+template <int DR>
+__device__ __forceinline__ void chacha_block(const ChachaKey &key, uint64_t nonce, uint64_t counter,
+                                             uint32_t out[16]) {
     const uint32_t in[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u, key.k[0], key.k[1],
                              key.k[2],    key.k[3],    key.k[4],    key.k[5],    key.k[6], key.k[7],
                              (uint32_t)counter, (uint32_t)(counter >> 32), (uint32_t)nonce,
@@ -50,7 +56,7 @@ __device__ __forceinline__ void chacha20_block(const ChachaKey &key, uint64_t no
 #pragma unroll
     for (int i = 0; i < 16; ++i) x[i] = in[i];
 #pragma unroll 2
-    for (int r = 0; r < 10; ++r) {
+    for (int r = 0; r < DR; ++r) {
         CC_QR(x[0], x[4], x[8], x[12]);
         CC_QR(x[1], x[5], x[9], x[13]);
         CC_QR(x[2], x[6], x[10], x[14]);
@@ -75,6 +81,7 @@ __device__ __forceinline__ uint32_t pk_sub_u16(uint32_t a, uint32_t b) {
 
 // templates: m reference-layout records (pattern dwords 0..399, mask 400..799)
 // shares: [parties][m][12800] u16
+template <int DR>
 __global__ void __launch_bounds__(256) prepare_shares_kernel(const uint32_t *__restrict__ templates, uint64_t m,
                                                              uint64_t g0, ChachaKey key, uint64_t nonce,
                                                              uint32_t parties, uint16_t *__restrict__ shares) {
@@ -97,7 +104,7 @@ __global__ void __launch_bounds__(256) prepare_shares_kernel(const uint32_t *__r
         const uint64_t g = g0 + i;
         for (uint32_t j = 0; j + 1 < parties; ++j) {
             uint32_t r[16];
-            chacha20_block(key, nonce, (g * (parties - 1) + j) * kBlocks + (uint64_t)b, r);
+            chacha_block<DR>(key, nonce, (g * (parties - 1) + j) * kBlocks + (uint64_t)b, r);
             uint4 *dst = (uint4 *)(shares + ((uint64_t)j * m + i) * IRIS_BITS + 32 * b);
 #pragma unroll
             for (int q = 0; q < 4; ++q) dst[q] = make_uint4(r[4 * q], r[4 * q + 1], r[4 * q + 2], r[4 * q + 3]);
@@ -132,6 +139,7 @@ __device__ __forceinline__ void store_share_block(uint4 *db, uint64_t t, int b, 
     base[(2 * b + 1) * 64 + 32] = hi;
 }
 
+template <int DR>
 __global__ void __launch_bounds__(256) prepare_shares_tiles_kernel(const uint32_t *__restrict__ templates, uint64_t m,
                                                                    uint64_t g0, ChachaKey key, uint64_t nonce,
                                                                    uint32_t parties, ShareDsts dst) {
@@ -151,7 +159,7 @@ __global__ void __launch_bounds__(256) prepare_shares_tiles_kernel(const uint32_
         }
         for (uint32_t j = 0; j + 1 < parties; ++j) {
             uint32_t r[16];
-            chacha20_block(key, nonce, (g * (parties - 1) + j) * kBlocks + (uint64_t)b, r);
+            chacha_block<DR>(key, nonce, (g * (parties - 1) + j) * kBlocks + (uint64_t)b, r);
             store_share_block(dst.db[j], dst.t_first[j] + i, b, r);
 #pragma unroll
             for (int q = 0; q < 16; ++q) last[q] = pk_sub_u16(last[q], r[q]);
@@ -165,6 +173,7 @@ __global__ void __launch_bounds__(256) prepare_shares_tiles_kernel(const uint32_
 // optional masks written straight into TILES databases — one launch, no
 // staging.  The masks dword b of record t is component (b & 6) / 2 of the
 // 16-byte word (b / 8, half b & 1) of its tile (pack_masks_tiles' layout).
+template <int DR>
 __global__ void __launch_bounds__(256) prepare_direct_kernel(const uint4 *__restrict__ tdb, uint64_t t_first,
                                                              uint64_t m, uint64_t g0, ChachaKey key, uint64_t nonce,
                                                              uint32_t parties, ShareDsts dst, uint4 *masks,
@@ -197,7 +206,7 @@ __global__ void __launch_bounds__(256) prepare_direct_kernel(const uint4 *__rest
         }
         for (uint32_t j = 0; j + 1 < parties; ++j) {
             uint32_t r[16];
-            chacha20_block(key, nonce, (g * (parties - 1) + j) * kBlocks + (uint64_t)b, r);
+            chacha_block<DR>(key, nonce, (g * (parties - 1) + j) * kBlocks + (uint64_t)b, r);
             store_share_block(dst.db[j], dst.t_first[j] + i, b, r);
 #pragma unroll
             for (int q = 0; q < 16; ++q) last[q] = pk_sub_u16(last[q], r[q]);
@@ -206,54 +215,66 @@ __global__ void __launch_bounds__(256) prepare_direct_kernel(const uint4 *__rest
     }
 }
 
-int launch_prepare_direct(void *stream, const void *tdb, uint64_t t_first, uint64_t m, uint64_t g0,
-                          const uint8_t key[32], uint64_t nonce, uint32_t parties, void *const *dbs,
-                          const uint64_t *s_first, void *masks, uint64_t m_first) {
-    if (m == 0) return 0;
-    if (parties == 0 || parties > (uint32_t)kMaxPrepParties) return -1;
+static ChachaKey load_key(const uint8_t key[32]) {
     ChachaKey k;
     for (int i = 0; i < 8; ++i)
         k.k[i] = (uint32_t)key[4 * i] | ((uint32_t)key[4 * i + 1] << 8) | ((uint32_t)key[4 * i + 2] << 16) |
                  ((uint32_t)key[4 * i + 3] << 24);
+    return k;
+}
+
+// the kernel instance for a round count (8, 12, 20); nullptr for any other
+template <typename K>
+static K by_rounds(uint32_t rounds, K k8, K k12, K k20) {
+    return rounds == 8 ? k8 : rounds == 12 ? k12 : rounds == 20 ? k20 : nullptr;
+}
+
+int launch_prepare_direct(void *stream, const void *tdb, uint64_t t_first, uint64_t m, uint64_t g0,
+                          const uint8_t key[32], uint64_t nonce, uint32_t rounds, uint32_t parties,
+                          void *const *dbs, const uint64_t *s_first, void *masks, uint64_t m_first) {
+    if (m == 0) return 0;
+    if (parties == 0 || parties > (uint32_t)kMaxPrepParties) return -1;
+    const ChachaKey k = load_key(key);
     ShareDsts d{};
     for (uint32_t j = 0; j < parties; ++j) {
         d.db[j] = (uint4 *)dbs[j];
         d.t_first[j] = s_first[j];
     }
-    hipLaunchKernelGGL(prepare_direct_kernel, dim3((uint32_t)((m + 63) / 64)), dim3(256), 0, (hipStream_t)stream,
+    const auto kern = by_rounds(rounds, prepare_direct_kernel<4>, prepare_direct_kernel<6>, prepare_direct_kernel<10>);
+    if (!kern) return -1;
+    hipLaunchKernelGGL(kern, dim3((uint32_t)((m + 63) / 64)), dim3(256), 0, (hipStream_t)stream,
                        (const uint4 *)tdb, t_first, m, g0, k, nonce, parties, d, (uint4 *)masks, m_first);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int launch_prepare_shares_tiles(void *stream, const void *templates, uint64_t m, uint64_t g0, const uint8_t key[32],
-                                uint64_t nonce, uint32_t parties, void *const *dbs, const uint64_t *t_first) {
+                                uint64_t nonce, uint32_t rounds, uint32_t parties, void *const *dbs, const uint64_t *t_first) {
     if (m == 0) return 0;
     if (parties == 0 || parties > (uint32_t)kMaxPrepParties) return -1;
-    ChachaKey k;
-    for (int i = 0; i < 8; ++i)
-        k.k[i] = (uint32_t)key[4 * i] | ((uint32_t)key[4 * i + 1] << 8) | ((uint32_t)key[4 * i + 2] << 16) |
-                 ((uint32_t)key[4 * i + 3] << 24);
+    const ChachaKey k = load_key(key);
     ShareDsts d{};
     for (uint32_t j = 0; j < parties; ++j) {
         d.db[j] = (uint4 *)dbs[j];
         d.t_first[j] = t_first[j];
     }
-    hipLaunchKernelGGL(prepare_shares_tiles_kernel, dim3((uint32_t)((m + 63) / 64)), dim3(256), 0, (hipStream_t)stream,
+    const auto kern = by_rounds(rounds, prepare_shares_tiles_kernel<4>, prepare_shares_tiles_kernel<6>,
+                                 prepare_shares_tiles_kernel<10>);
+    if (!kern) return -1;
+    hipLaunchKernelGGL(kern, dim3((uint32_t)((m + 63) / 64)), dim3(256), 0, (hipStream_t)stream,
                        (const uint32_t *)templates, m, g0, k, nonce, parties, d);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int launch_prepare_shares(void *stream, const void *templates, uint64_t m, uint64_t g0, const uint8_t key[32],
-                          uint64_t nonce, uint32_t parties, void *shares) {
+                          uint64_t nonce, uint32_t rounds, uint32_t parties, void *shares) {
     if (m == 0) return 0;
-    ChachaKey k;
-    for (int i = 0; i < 8; ++i)
-        k.k[i] = (uint32_t)key[4 * i] | ((uint32_t)key[4 * i + 1] << 8) | ((uint32_t)key[4 * i + 2] << 16) |
-                 ((uint32_t)key[4 * i + 3] << 24);
+    const ChachaKey k = load_key(key);
     const uint64_t total = m * kBlocks;
     uint64_t grid = (total + 255) / 256;
     if (grid > 256ull * 64) grid = 256ull * 64;
-    hipLaunchKernelGGL(prepare_shares_kernel, dim3((uint32_t)grid), dim3(256), 0, (hipStream_t)stream,
+    const auto kern = by_rounds(rounds, prepare_shares_kernel<4>, prepare_shares_kernel<6>, prepare_shares_kernel<10>);
+    if (!kern) return -1;
+    hipLaunchKernelGGL(kern, dim3((uint32_t)grid), dim3(256), 0, (hipStream_t)stream,
                        (const uint32_t *)templates, m, g0, k, nonce, parties, (uint16_t *)shares);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -108,7 +108,7 @@ def load_library(path=None):
             "iris_templates_write_json": ([ctypes.c_char_p, P, u64], ctypes.c_int),
             "iris_resolver_search_masks": ([P, P, u64, u64, P, ctypes.c_uint32, u64, P, ctypes.POINTER(Match)],
                                            ctypes.c_int),
-            "iris_prepare_shares": ([P, u64, u64, u64, P, u64, ctypes.c_uint32, P, P], ctypes.c_int),
+            "iris_prepare_shares": ([P, u64, u64, u64, P, u64, ctypes.c_uint32, ctypes.c_uint32, P, P], ctypes.c_int),
             "iris_masks_engine_new": ([P, P, PP], ctypes.c_int),
             "iris_distance_engine_new": ([P, P, PP], ctypes.c_int),
             "iris_template_engine_new": ([P, P, PP], ctypes.c_int),
@@ -203,10 +203,11 @@ def write_templates_json(path, templates):
     _check(load_library().iris_templates_write_json(os.fsencode(path), _ptr(a), a.shape[0]))
 
 
-def prepare_shares(templates, shares, masks=None, key=None, nonce=0, first=0, n=None, index_base=0):
+def prepare_shares(templates, shares, masks=None, key=None, nonce=0, first=0, n=None, index_base=0, rounds=12):
     """`prepare` on the device (src/main.rs:333-361): appends EncodedBits::share(len(shares))
     of encode(templates[first:first+n]) to the share Databases and, optionally, the masks to
-    a masks Database.  key: 32 bytes (default: os.urandom, a CSPRNG).  Returns the key."""
+    a masks Database.  key: 32 bytes (default: os.urandom, a CSPRNG).  rounds: ChaCha8/12/20;
+    12 is the reference's generator (rand 0.8.5 thread_rng = ChaCha12).  Returns the key."""
     if key is None:
         key = os.urandom(32)
     key = bytes(key)
@@ -217,7 +218,7 @@ def prepare_shares(templates, shares, masks=None, key=None, nonce=0, first=0, n=
     kbuf = (ctypes.c_uint8 * 32).from_buffer_copy(key)
     arr = (ctypes.c_void_p * len(shares))(*[s.handle for s in shares])
     _check(load_library().iris_prepare_shares(templates.handle, int(first), int(n), int(index_base), kbuf,
-                                              int(nonce), len(shares), arr,
+                                              int(nonce), int(rounds), len(shares), arr,
                                               masks.handle if masks is not None else None))
     return key
 

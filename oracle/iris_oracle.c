@@ -388,7 +388,7 @@ static uint32_t orc_rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)
         c += d; b ^= c; b = orc_rotl32(b, 7);  \
     } while (0)
 
-void orc_chacha20_block(const uint8_t key[32], uint64_t nonce, uint64_t counter, uint8_t out[64]) {
+void orc_chacha_block(const uint8_t key[32], uint64_t nonce, uint64_t counter, uint32_t rounds, uint8_t out[64]) {
     uint32_t in[16], x[16];
     in[0] = 0x61707865u; /* "expand 32-byte k" */
     in[1] = 0x3320646eu;
@@ -402,7 +402,7 @@ void orc_chacha20_block(const uint8_t key[32], uint64_t nonce, uint64_t counter,
     in[14] = (uint32_t)nonce;
     in[15] = (uint32_t)(nonce >> 32);
     memcpy(x, in, sizeof x);
-    for (int r = 0; r < 10; ++r) {
+    for (uint32_t r = 0; r < rounds / 2; ++r) { /* double rounds: column then diagonal */
         ORC_QR(x[0], x[4], x[8], x[12]);
         ORC_QR(x[1], x[5], x[9], x[13]);
         ORC_QR(x[2], x[6], x[10], x[14]);
@@ -422,7 +422,7 @@ void orc_chacha20_block(const uint8_t key[32], uint64_t nonce, uint64_t counter,
 }
 
 void orc_prepare_shares(const orc_template *t, uint64_t n, uint64_t index_base, const uint8_t key[32],
-                        uint64_t nonce, uint32_t parties, uint16_t *shares, uint64_t *masks) {
+                        uint64_t nonce, uint32_t rounds, uint32_t parties, uint16_t *shares, uint64_t *masks) {
     uint16_t enc[ORC_BITS];
     uint8_t blk[64];
     for (uint64_t i = 0; i < n; ++i) {
@@ -433,7 +433,7 @@ void orc_prepare_shares(const orc_template *t, uint64_t n, uint64_t index_base, 
         for (uint32_t j = 0; j + 1 < parties; ++j) {
             uint16_t *sh = shares + ((uint64_t)j * n + i) * ORC_BITS;
             for (int b = 0; b < ORC_BITS / 32; ++b) {
-                orc_chacha20_block(key, nonce, (g * (parties - 1) + j) * (ORC_BITS / 32) + (uint64_t)b, blk);
+                orc_chacha_block(key, nonce, (g * (parties - 1) + j) * (ORC_BITS / 32) + (uint64_t)b, rounds, blk);
                 for (int e = 0; e < 32; ++e) {
                     const uint16_t v = (uint16_t)(blk[2 * e] | (blk[2 * e + 1] << 8));
                     sh[32 * b + e] = v;

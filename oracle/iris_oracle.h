@@ -68,18 +68,20 @@ void orc_gen_templates(uint64_t seed, uint64_t t0, uint64_t n, orc_template *out
 void orc_gen_masks(uint64_t seed, uint64_t t0, uint64_t n, uint64_t *out);
 void orc_gen_shares(uint64_t seed, uint64_t t0, uint64_t n, uint16_t *out);
 
-/* share preparation.  ChaCha20 block function, D. J.
- * Bernstein's original parameterisation (64-bit block counter in state words
- * 12-13, 64-bit nonce in words 14-15); RFC 8439 §2.3 is the same function
- * with the 128 bits split 32/96, so its test vectors apply. */
-void orc_chacha20_block(const uint8_t key[32], uint64_t nonce, uint64_t counter, uint8_t out[64]);
+/* share preparation.  ChaCha block function with
+ * `rounds` (8, 12, 20) rounds, D. J. Bernstein's original parameterisation
+ * (64-bit block counter in state words 12-13, 64-bit nonce in words 14-15),
+ * which is also rand_chacha 0.3.1's (the reference's thread_rng core is its
+ * ChaCha12, rand 0.8.5); RFC 8439 §2.3 is the 20-round function with the 128
+ * bits split 32/96, so its test vectors apply. */
+void orc_chacha_block(const uint8_t key[32], uint64_t nonce, uint64_t counter, uint32_t rounds, uint8_t out[64]);
 /* EncodedBits::share (src/encoded_bits.rs:23-38) of encode(t[i]) for
- * template index g = index_base + i: shares j < parties-1 are the ChaCha20
- * keystream blocks counter = (g * (parties-1) + j) * 400 + b, b = 0..399
+ * template index g = index_base + i: shares j < parties-1 are the ChaCha
+ * (`rounds`) keystream blocks counter = (g * (parties-1) + j) * 400 + b, b = 0..399
  * (element 32b + e = little-endian u16 e of block b); the last share is
  * encode(t) minus their sum (mod 2^16).  shares: [parties][n][12800];
  * masks (may be NULL): [n][200], the `.masks` records (src/main.rs:333-342). */
 void orc_prepare_shares(const orc_template *t, uint64_t n, uint64_t index_base, const uint8_t key[32],
-                        uint64_t nonce, uint32_t parties, uint16_t *shares, uint64_t *masks);
+                        uint64_t nonce, uint32_t rounds, uint32_t parties, uint16_t *shares, uint64_t *masks);
 
 #endif

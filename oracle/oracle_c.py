@@ -55,8 +55,8 @@ def load(path=None):
     lib.orc_gen_templates.argtypes = [u64, u64, u64, P]
     lib.orc_gen_masks.argtypes = [u64, u64, u64, P]
     lib.orc_gen_shares.argtypes = [u64, u64, u64, P]
-    lib.orc_chacha20_block.argtypes = [P, u64, u64, P]
-    lib.orc_prepare_shares.argtypes = [P, u64, u64, P, u64, ctypes.c_uint32, P, P]
+    lib.orc_chacha_block.argtypes = [P, u64, u64, ctypes.c_uint32, P]
+    lib.orc_prepare_shares.argtypes = [P, u64, u64, P, u64, ctypes.c_uint32, ctypes.c_uint32, P, P]
     if path is None:
         _lib = lib
     return lib
@@ -185,17 +185,17 @@ def gen_shares(seed, t0, n):
     return out
 
 
-def chacha20_block(key, nonce, counter):
-    """64 keystream bytes (DJB ChaCha20: 64-bit nonce, 64-bit block counter)."""
+def chacha_block(key, nonce, counter, rounds=20):
+    """64 keystream bytes (DJB ChaCha, 8/12/20 rounds: 64-bit nonce, 64-bit block counter)."""
     k = np.frombuffer(bytes(key), np.uint8).copy()
     assert k.size == 32
     out = np.zeros(64, np.uint8)
-    load().orc_chacha20_block(_p(k), int(nonce), int(counter), _p(out))
+    load().orc_chacha_block(_p(k), int(nonce), int(counter), int(rounds), _p(out))
     return out.tobytes()
 
 
-def prepare_shares(templates, key, nonce=0, parties=3, index_base=0):
-    """EncodedBits::share of encode(t) with the ChaCha20 stream of orc_prepare_shares:
+def prepare_shares(templates, key, nonce=0, parties=3, index_base=0, rounds=12):
+    """EncodedBits::share of encode(t) with the ChaCha stream of orc_prepare_shares:
     returns (shares [parties][n][12800] u16, masks [n][200] u64)."""
     t = np.ascontiguousarray(np.asarray(templates, np.uint64).reshape(-1, 400))
     n = t.shape[0]
@@ -203,5 +203,6 @@ def prepare_shares(templates, key, nonce=0, parties=3, index_base=0):
     assert k.size == 32
     shares = np.zeros((parties, n, 12800), np.uint16)
     masks = np.zeros((n, 200), np.uint64)
-    load().orc_prepare_shares(_p(t), n, int(index_base), _p(k), int(nonce), int(parties), _p(shares), _p(masks))
+    load().orc_prepare_shares(_p(t), n, int(index_base), _p(k), int(nonce), int(rounds), int(parties), _p(shares),
+                              _p(masks))
     return shares, masks

@@ -194,8 +194,9 @@ def _rotl32(x, r):
     return ((x << np.uint32(r)) | (x >> np.uint32(32 - r))).astype(np.uint32)
 
 
-def chacha20_blocks(key, nonce, counters):
-    """Vectorised ChaCha20 blocks (DJB: 64-bit nonce, 64-bit counter) -> uint8 [len(counters), 64]."""
+def chacha_blocks(key, nonce, counters, rounds=20):
+    """Vectorised ChaCha blocks (DJB: 64-bit nonce, 64-bit counter; 8/12/20 rounds; rand_chacha
+    0.3.1's layout) -> uint8 [len(counters), 64]."""
     k = np.frombuffer(bytes(key), "<u4")
     c = np.asarray(counters, np.uint64)
     n = c.size
@@ -214,16 +215,17 @@ def chacha20_blocks(key, nonce, counters):
         x[a] += x[b]; x[d] = _rotl32(x[d] ^ x[a], 8)
         x[cc] += x[d]; x[b] = _rotl32(x[b] ^ x[cc], 7)
 
-    for _ in range(10):
+    for _ in range(rounds // 2):
         qr(0, 4, 8, 12); qr(1, 5, 9, 13); qr(2, 6, 10, 14); qr(3, 7, 11, 15)
         qr(0, 5, 10, 15); qr(1, 6, 11, 12); qr(2, 7, 8, 13); qr(3, 4, 9, 14)
     out = (x + st).astype("<u4").T.copy()
     return out.view(np.uint8).reshape(n, 64)
 
 
-def prepare_shares(templates, key, nonce=0, parties=3, index_base=0):
-    """EncodedBits::share (src/encoded_bits.rs:23-38) with the counter-mode ChaCha20
-    derivation of oracle/iris_oracle.h: shares [parties][n][12800], masks [n][200]."""
+def prepare_shares(templates, key, nonce=0, parties=3, index_base=0, rounds=12):
+    """EncodedBits::share (src/encoded_bits.rs:23-38) with the counter-mode ChaCha
+    derivation of oracle/iris_oracle.h (12 rounds: rand 0.8.5's thread_rng core):
+    shares [parties][n][12800], masks [n][200]."""
     t = np.asarray(templates, np.uint64).reshape(-1, 400)
     n = t.shape[0]
     shares = np.zeros((parties, n, 12800), np.uint16)
@@ -232,7 +234,7 @@ def prepare_shares(templates, key, nonce=0, parties=3, index_base=0):
         last = encode(t[i, :200], t[i, 200:]).astype(np.uint16)
         for j in range(parties - 1):
             ctr = (g * (parties - 1) + j) * 400 + np.arange(400, dtype=np.uint64)
-            sh = chacha20_blocks(key, nonce, ctr).view("<u2").reshape(12800)
+            sh = chacha_blocks(key, nonce, ctr, rounds).view("<u2").reshape(12800)
             shares[j, i] = sh
             last = (last - sh).astype(np.uint16)
         shares[parties - 1, i] = last

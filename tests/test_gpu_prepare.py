@@ -1,6 +1,6 @@
 """Share preparation on the device (the reference's
 `prepare`, src/main.rs:333-361, EncodedBits::share src/encoded_bits.rs:23-38):
-bit-exact against the oracle's restatement of the ChaCha20 counter-mode
+bit-exact against the oracle's restatement of the ChaCha (8/12/20-round) counter-mode
 derivation, and the prepared shares drive the MPC flow to the plaintext answer."""
 import numpy as np
 import pytest
@@ -14,17 +14,18 @@ KEY = bytes(range(7, 39))
 
 
 @pytest.mark.parametrize("layout", [ih.LAYOUT_TILES, ih.LAYOUT_LANES], ids=["tiles", "lanes"])
-@pytest.mark.parametrize("parties", [1, 2, 3])
-def test_prepare_matches_oracle(device, layout, parties):
+@pytest.mark.parametrize("parties,rounds", [(1, 12), (2, 12), (3, 12), (3, 20), (2, 8)])
+def test_prepare_matches_oracle(device, layout, parties, rounds):
     n = 70
     t = oc.gen_templates(31, 0, n)
-    want_s, want_m = oc.prepare_shares(t[5:5 + 60], KEY, nonce=11, parties=parties, index_base=1000 + 5)
+    want_s, want_m = oc.prepare_shares(t[5:5 + 60], KEY, nonce=11, parties=parties, index_base=1000 + 5,
+                                       rounds=rounds)
     with ih.Database(device, ih.KIND_TEMPLATES, n, layout) as tdb:
         tdb.append(t)
         sdbs = [ih.Database(device, ih.KIND_SHARES, 64, layout) for _ in range(parties)]
         with ih.Database(device, ih.KIND_MASKS, 64, layout) as mdb:
             mdb.append(t[:1, 200:])  # appends after existing records
-            ih.prepare_shares(tdb, sdbs, mdb, key=KEY, nonce=11, first=5, n=60, index_base=1000)
+            ih.prepare_shares(tdb, sdbs, mdb, key=KEY, nonce=11, first=5, n=60, index_base=1000, rounds=rounds)
             assert len(mdb) == 61 and (mdb.read(1, 60) == want_m).all()
         for j, db in enumerate(sdbs):
             assert len(db) == 60
@@ -104,4 +105,6 @@ def test_prepare_argument_errors(device):
             ih.prepare_shares(tdb, [m])            # wrong kind
         with pytest.raises(ih.IrisError):
             ih.prepare_shares(tdb, [s], first=5, n=10)  # outside the template range
+        with pytest.raises(ih.IrisError):
+            ih.prepare_shares(tdb, [s], rounds=10)      # not ChaCha8/12/20
         assert len(s) == 0
