@@ -395,8 +395,13 @@ int iris_db_create_ex(iris_device_t *d, int kind, uint64_t capacity, int layout,
     if (!db) return fail(IRIS_E_NOMEM, "out of host memory");
     db->dev = d;
     db->k = kind_info(kind, layout);
-    db->cap = (capacity + db->k.block - 1) / db->k.block * db->k.block;
-    const size_t bytes = std::max<uint64_t>(1, db->cap / db->k.block) * block_bytes(db->k);
+    const uint64_t blocks = std::max<uint64_t>(1, capacity / db->k.block + (capacity % db->k.block != 0));
+    size_t bytes = 0;
+    if (__builtin_mul_overflow(blocks, (uint64_t)block_bytes(db->k), &bytes)) {
+        delete db;
+        return fail(IRIS_E_NOMEM, "database capacity overflows the address space");
+    }
+    db->cap = capacity == 0 ? 0 : blocks * db->k.block;
     hipError_t e = hipMalloc(&db->data, bytes);
     if (e != hipSuccess) {
         delete db;

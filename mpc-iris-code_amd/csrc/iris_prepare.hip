@@ -130,7 +130,8 @@ struct ShareDsts {
 
 // Share rows leave with nontemporal stores: 19.4 vs 20.2 ms per 1M templates (ChaCha12, 3
 // parties, interleaved runs on one box).  Loading the next block's template pair ahead of
-// the stores (vmcnt counts stores too on gfx9) measured no change.
+// the stores (vmcnt counts stores too on gfx9) measured no change; write-through policies
+// (sc1, sc0 sc1, nt sc1) were 0.5-2 % slower than nt.
 #ifndef IRIS_PREP_NT
 #define IRIS_PREP_NT 1
 #endif

@@ -97,6 +97,15 @@ def test_append_write_read_roundtrip(device, layout):
             db.write(151, recs[:1])
 
 
+@pytest.mark.parametrize("kind", [ih.KIND_MASKS, ih.KIND_SHARES, ih.KIND_TEMPLATES])
+def test_db_capacity_overflow_rejected(device, kind):
+    """A capacity whose byte size overflows 64 bits fails cleanly instead of allocating a
+    wrapped-around size."""
+    for cap in (2**64 - 1, 2**62):
+        with pytest.raises(ih.IrisError):
+            ih.Database(device, kind, cap)
+
+
 # ---------------------------------------------------------------- Template path
 
 
