@@ -36,7 +36,7 @@ import iris_hip as ih  # noqa: E402
 
 METRIC = "template comparisons/sec (query×rotations×DB) + % HBM roofline, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
-HBM_MEASURED_GBS = 6290.0    # MI355X_MICROARCH.md: float4 copy
+HBM_GUIDE_COPY_GBS = 6290.0  # MI355X_MICROARCH.md: float4 copy (read + write), not a read ceiling
 # best pure 16-B read stream over 32 GB on this part after a 1.5-s warm-up
 # (tools/ubench_stream.hip, profiles/r01_ubench_read_stream_warm.txt: 7.02 TB/s at 12 waves
 # per CU, 6.78 TB/s at the search kernel's 8)
@@ -604,7 +604,7 @@ def main():
                          ("batch", "tiles"): "batch_kernel (fp4 MFMA, LDS-tiled GEMM)"}[(args.workload, args.layout)],
                 "avg_ms": avg_ms, "launches": launches,
                 "reduce_avg_ms": rms / max(1, launches),
-                "frac_of_measured_hbm": achieved / HBM_MEASURED_GBS,
+                "frac_of_guide_copy_bw": achieved / HBM_GUIDE_COPY_GBS,
                 "frac_of_read_ceiling": achieved / HBM_READ_CEILING_GBS,
                 "valu_int_frac": (VALU_OPS_PER_TEMPLATE * n / (avg_ms * 1e-3) / VALU_INT_PEAK_OPS
                                   if args.layout == "lanes" and args.workload == "search" else None),
