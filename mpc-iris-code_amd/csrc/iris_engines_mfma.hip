@@ -82,6 +82,9 @@ __device__ __forceinline__ void mask_chunk(uint32_t x, const v8i &a, v16f &acc) 
     acc = mfma_fp4(a, b, acc);
 }
 
+#ifndef IRIS_RESOLVE_NT
+#define IRIS_RESOLVE_NT 1
+#endif
 // Fused resolver operands (MASKS_RESOLVE): the participants' [n][31] u16
 // outputs, row i = record first + i (src/main.rs:597-607).
 struct MaskResolve {
@@ -139,8 +142,12 @@ __global__ void __launch_bounds__(256, kMasksBlocksPerCu)
         if (full) {  // wave-uniform: 124 16-B words per share array
             typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
             for (int i = lane; i < 32 * kRot / 8; i += 64) {
-                u16x8 v = *(const u16x8 *)(rs.shares[0] + e0 + 8 * i);
-                for (uint32_t p = 1; p < rs.parts; ++p) v += *(const u16x8 *)(rs.shares[p] + e0 + 8 * i);
+                // read once: nontemporal, like the masks stream
+                u16x8 v = IRIS_RESOLVE_NT ? __builtin_nontemporal_load((const u16x8 *)(rs.shares[0] + e0 + 8 * i))
+                                          : *(const u16x8 *)(rs.shares[0] + e0 + 8 * i);
+                for (uint32_t p = 1; p < rs.parts; ++p)
+                    v += IRIS_RESOLVE_NT ? __builtin_nontemporal_load((const u16x8 *)(rs.shares[p] + e0 + 8 * i))
+                                         : *(const u16x8 *)(rs.shares[p] + e0 + 8 * i);
                 *(u16x8 *)&lds[8 * i] = v;
             }
         } else {
