@@ -4,6 +4,12 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--n-per-gpu T]
     torchrun --nproc-per-node N bench.py --gpus N ...
 
+`python bench.py --gpus N` with N > 1 and no launcher starts the N ranks itself
+(torch.distributed.run as a child process, before this process touches a GPU)
+and exits with their status; every rank checks that the process group really
+has N ranks (and, on RCCL, that it owns a GPU of its own) and exits non-zero
+otherwise, so a scaling run can never print a one-GPU line for N GPUs.
+
 A step = one search of the query against every resident template on every
 rank (the query engine build, the kernel, the partials reduce) plus, for N > 1,
 the RCCL all-gather of the per-shard minima and their merge.  Steps are
@@ -13,14 +19,15 @@ and the exchange overlap the next kernel; --no-pipeline waits step by step.  The
 DESIGN.md §5 generator, uniform random pattern and mask bits as the
 reference's rng.gen::<Template>()), generated on each GPU so that shard k
 holds global templates [k*T, (k+1)*T) — inputs are resident in HBM before
-the timed region.  A rotated, lightly perturbed copy of the query is planted
-at a known global index; every step's result is checked against it.
+the timed region.  Rotated, lightly perturbed copies of the query (of four
+queries in four query groups for --workload batch) are planted at known global
+indices; every run checks they are found (exit 3 otherwise).
 """
 import argparse
-import ctypes
 import json
 import os
 import pathlib
+import socket
 import subprocess
 import sys
 import tempfile
@@ -32,7 +39,7 @@ ROOT = pathlib.Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 sys.path.insert(0, str(ROOT / "mpc-iris-code_amd"))
 
-import iris_hip as ih  # noqa: E402
+import iris_hip as ih  # noqa: E402  (loads libiris_hip.so; no HIP call until a Device is opened)
 
 METRIC = "template comparisons/sec (query×rotations×DB) + % HBM roofline, 1/2/4/8 GPU"
 HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: 8.0 TB/s spec
@@ -49,6 +56,8 @@ BYTES_PER_TEMPLATE = 3200    # pattern + mask planes, read once per query
 VALU_OPS_PER_TEMPLATE = 400 * 31 * 4   # words x rotations x (and, bitop3, 2x bcnt)
 ROT = 31
 SEED = 20251015
+GPU_WORKLOADS = ("search", "masks", "shares", "batch")
+AUX_WORKLOADS = ("resolver", "resolve-masks", "prepare", "load", "host-shares", "host-masks", "criterion")
 
 
 def parse():
@@ -72,9 +81,7 @@ def parse():
     ap.add_argument("--layout", choices=["tiles", "lanes"], default="tiles",
                     help="tiles = MFMA kernels (default), lanes = VALU kernels")
     ap.add_argument("--queries", type=int, default=1024, help="queries per batch (workload batch)")
-    ap.add_argument("--workload", choices=["search", "masks", "shares", "batch", "resolver", "resolve-masks", "prepare",
-                                           "load", "host-shares", "host-masks"],
-                    default="search",
+    ap.add_argument("--workload", choices=list(GPU_WORKLOADS + AUX_WORKLOADS), default="search",
                     help="search = Template masked Hamming + argmin (configs[1], default); "
                          "masks = MasksEngine denominators; shares = DistanceEngine u16 share dot (configs[3]); "
                          "batch = --queries queries x 31 rotations x N templates in one pass (configs[2]); "
@@ -82,18 +89,47 @@ def parse():
                          "resolve-masks = the same with the denominators computed on the fly from a masks DB; "
                          "prepare = GPU share preparation of n templates into --parties share DBs + masks; "
                          "load = raw template file (page-cached) -> resident TILES database; "
-                         "host-shares / host-masks = batch_process over host slices (the reference signature)")
+                         "host-shares / host-masks = batch_process over host slices (the reference signature); "
+                         "criterion = configs[0]: 1 query x 31 x 10k search plus the arch dot shapes of "
+                         "src/arch/mod.rs:22-72, beside the CPU criterion loop")
     ap.add_argument("--parties", type=int, default=3, help="parties (workloads resolver, prepare)")
     ap.add_argument("--rounds", type=int, default=12, choices=[8, 12, 20],
                     help="ChaCha rounds for --workload prepare (12 = the reference's thread_rng, rand 0.8.5)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher rehearsal without a GPU: start / join the ranks, check the world size, "
+                         "exchange and merge a synthetic per-rank result over gloo, print the line (value null)")
     return ap.parse_args()
 
 
-def planted_record(query, rotation):
+def planted_record(query, rotation, flips=0x00FF00FF00FF00FF):
     p = ih.Bits(query[:200]).rotated(rotation).limbs.copy()
     m = ih.Bits(query[200:]).rotated(rotation).limbs
-    p[7] ^= np.uint64(0x00FF00FF00FF00FF)  # 32 flipped bits
+    p[7] ^= np.uint64(flips)  # 32 flipped bits
     return np.concatenate([p, m])
+
+
+def plant_sites(total, count):
+    """`count` distinct global indices inside [0, total) for planted answers (the first is
+    3/4 of the way in, so with 2+ ranks it lies in a later rank's shard)."""
+    if total <= 0:
+        return []
+    base = total * 3 // 4 + min(12345, total // 8)
+    step = max(1, total // 7)
+    sites = []
+    for k in range(count):
+        s = (base + k * step) % total
+        while s in sites:
+            s = (s + 1) % total
+        sites.append(s)
+        if len(sites) == total:
+            break
+    return sites
+
+
+def batch_plant_queries(nq):
+    """Queries that get a planted answer in the batch run: four query groups apart
+    (group = 4 consecutive queries, iris_batch.hip BQ), including the first and last."""
+    return sorted({nq // 2, 0, nq - 1, nq // 4 + 1} & set(range(nq)))
 
 
 def gen_records(dev, kind, n, seed):
@@ -130,43 +166,162 @@ def check_resolver(shares, denoms):
     return (float(d[idx]), idx) if np.isfinite(d[idx]) else (float("inf"), 2**64 - 1)
 
 
-def cpu_baseline(seconds):
-    """The oracle's engine-style CPU path (test infrastructure), compiled for
-    this host, timed on a bounded sample of the same workload."""
-    from oracle import oracle_c as oc
+# ---------------------------------------------------------------------------- CPU baseline
 
-    threads = min(16, os.cpu_count() or 1)
-    path = pathlib.Path(tempfile.gettempdir()) / f"liboracle_native_{os.getpid()}.so"
-    try:
-        oc.build(path, march="native")
-        lib = str(path)
-    except Exception:
-        lib = None  # fall back to the prebuilt x86-64-v3 oracle
-    oc_lib = oc.load(lib) if lib else oc.load()
-    query = oc.gen_templates(SEED + 1, 0, 1)[0]
 
-    n = 1_000_000  # 3.2 GB of templates: far beyond the CPU caches, streamed from DRAM each pass
-    db = oc.gen_templates(SEED, 0, n)
-    out = np.empty(n, np.float64)
-    d = np.zeros(1, np.float64)
-    i = np.zeros(1, np.uint64)
-    passes, t = 0, 0.0
-    while t < seconds and passes < 1000:
-        t0 = time.perf_counter()
-        oc_lib.orc_template_distances_batch(oc._p(query), oc._p(db), n, oc._p(out), threads)
-        oc_lib.orc_argmin(oc._p(out), n, oc._p(d), oc._p(i))  # resolver aggregation, src/main.rs:616-621
-        t += time.perf_counter() - t0
-        passes += 1
-    del db
+def cpu_info():
+    """Where the CPU leg runs: the CPUs this process may use (its affinity mask, which is
+    what the leg's thread count is), the machine's count and the cgroup's CPU quota."""
     try:
         model = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
     except Exception:
         model = "unknown"
-    return {
-        "value": ROT * n * passes / t, "unit": "template comparisons/s", "cores": threads, "kind": "port",
-        "sample": f"{passes} passes over {n} templates x 31 rotations, 1 query, distances + argmin, {t:.2f} s, "
-                  f"{threads} threads on {model}, gcc -O3 -march=native oracle/iris_oracle.c",
-    }
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        quota = None if q == "max" else int(q) / int(per)
+    except Exception:
+        pass
+    return {"model": model, "nproc": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
+            "cgroup_cpu_quota": quota}
+
+
+def _time_passes(fn, seconds, max_passes=1000):
+    passes, t = 0, 0.0
+    while (t < seconds or passes == 0) and passes < max_passes:
+        t0 = time.perf_counter()
+        fn()
+        t += time.perf_counter() - t0
+        passes += 1
+    return passes, t
+
+
+def cpu_baseline(args):
+    """The oracle's CPU restatement of the reference path for this workload (test
+    infrastructure: oracle/), compiled -O3 -march=native for this host and run on every
+    CPU the process may use, timed on a bounded sample (~--cpu-seconds) of the same
+    workload.  Rates are per the workload's unit, so they compare with `value`."""
+    from oracle import oracle_c as oc
+
+    info = cpu_info()
+    # every CPU the process may run on: its affinity mask, unless the cgroup's CPU quota grants
+    # less CPU time than that (on the GPU box: 256 CPUs in the mask, a 16-CPU quota; 256
+    # threads under that quota measured 2.9e8 comparisons/s against 4.0e8 with 16,
+    # profiles/r02_bench_search_cpu256.jsonl), in which case one thread per quota CPU
+    threads = info["affinity_cpus"]
+    if info["cgroup_cpu_quota"]:
+        threads = max(1, min(threads, int(-(-info["cgroup_cpu_quota"] // 1))))
+    path = pathlib.Path(tempfile.gettempdir()) / f"liboracle_native_{os.getpid()}.so"
+    try:
+        oc.build(path, march="native")
+        oc_lib = oc.load(str(path))
+        flags = "gcc -O3 -march=native"
+    except Exception:
+        oc_lib = oc.load()  # the prebuilt x86-64-v3 oracle
+        flags = "gcc -O3 -march=x86-64-v3"
+    finally:
+        path.unlink(missing_ok=True)
+    oc._lib = oc_lib  # the oracle_c helpers below use this build
+    wl = args.workload
+    secs = args.cpu_seconds
+    extra = {}
+    if wl in ("search", "batch"):
+        n = 1_000_000  # 3.2 GB of templates: far beyond the CPU caches, streamed from DRAM each pass
+        nq = 1 if wl == "search" else 4
+        db = oc.gen_templates(SEED, 0, n)
+        qs = oc.gen_templates(SEED + 1, 0, nq)
+        out = np.empty(n, np.float64)
+        d, i = np.zeros(1, np.float64), np.zeros(1, np.uint64)
+
+        def run():
+            for q in qs:  # per query: Template::distance per pair + the resolver's argmin
+                oc_lib.orc_template_distances_batch(oc._p(q), oc._p(db), n, oc._p(out), threads)
+                oc_lib.orc_argmin(oc._p(out), n, oc._p(d), oc._p(i))
+
+        passes, t = _time_passes(run, secs)
+        value, unit = ROT * n * nq * passes / t, "template comparisons/s"
+        sample = (f"{passes} passes of {nq} quer{'y' if nq == 1 else 'ies'} x 31 rotations x {n} templates "
+                  "(Template::distance per pair + argmin, src/template.rs:43-64, src/main.rs:616-621)")
+    elif wl in ("masks", "host-masks"):
+        n = 2_000_000  # 3.2 GB of masks
+        db = oc.gen_masks(SEED, 0, n)
+        q = oc.gen_masks(SEED + 1, 0, 1)[0]
+        out = np.empty((n, ROT), np.uint16)
+        passes, t = _time_passes(lambda: oc_lib.orc_masks_batch(oc._p(q), oc._p(db), n, oc._p(out), threads), secs)
+        value, unit = n * passes / t, "records/s"
+        extra["comparisons_per_s"] = ROT * value
+        sample = f"{passes} passes of MasksEngine::batch_process over {n} masks (src/lib.rs:69-79)"
+    elif wl in ("shares", "host-shares"):
+        n = 100_000  # 2.56 GB of shares (the 10M-share DB does not fit host RAM): extrapolated per record
+        db = oc.gen_shares(SEED, 0, n)
+        q = oc.encode(oc.gen_templates(SEED + 1, 0, 1)[0])
+        out = np.empty((n, ROT), np.uint16)
+        passes, t = _time_passes(lambda: oc_lib.orc_distance_batch(oc._p(q), oc._p(db), n, oc._p(out), threads),
+                                 secs)
+        value = n * passes / t
+        unit = "records/s" if wl == "host-shares" else "template comparisons/s"
+        if wl == "shares":
+            value *= ROT
+        sample = (f"{passes} passes of DistanceEngine::batch_process (dot_u16, src/lib.rs:42-52, "
+                  f"src/arch/generic.rs:11-16) over {n} shares, per-record rate extrapolated")
+    elif wl in ("resolver", "resolve-masks"):
+        n = 2_000_000
+        rng = np.random.default_rng(SEED)
+        shares = rng.integers(0, 65536, (args.parties, n, ROT), dtype=np.uint16)
+        denoms = rng.integers(0, 12801, (n, ROT), dtype=np.uint16)
+        out = np.empty(n, np.float64)
+        d, i = np.zeros(1, np.float64), np.zeros(1, np.uint64)
+
+        def run():
+            oc_lib.orc_resolver_combine(oc._p(shares), args.parties, oc._p(denoms), n, oc._p(out))
+            oc_lib.orc_argmin(oc._p(out), n, oc._p(d), oc._p(i))
+
+        passes, t = _time_passes(run, secs)
+        threads = 1  # the combine loop is the reference's sequential scan
+        value, unit = n * passes / t, "records/s"
+        sample = f"{passes} passes of the share sum + decode + argmin (src/main.rs:597-621) over {n} entries"
+        if wl == "resolve-masks":
+            sample += " (the masks engine's denominators are not included)"
+    elif wl == "prepare":
+        n = 2000
+        tmpl = oc.gen_templates(SEED, 0, n)
+        passes, t = _time_passes(lambda: oc.prepare_shares(tmpl, bytes(range(32)), parties=args.parties,
+                                                           rounds=args.rounds), secs)
+        threads = 1
+        value, unit = n * passes / t, "templates/s"
+        sample = f"{passes} passes of encode + EncodedBits::share({args.parties}) (ChaCha{args.rounds}) over {n} templates"
+    elif wl == "criterion":
+        threads = 1  # criterion runs the loop on one thread (src/arch/mod.rs:34-41)
+        shapes = {}
+        rng = np.random.default_rng(SEED)
+        for name, shp in (("dot_bool", [(1, 1), (1, 1000), (31, 1000), (1, 100_000)]),
+                          ("dot_u16", [(1, 1), (1, 1000), (31, 1000), (1, 100_000), (31, 100_000)])):
+            for a, b in shp:
+                if name == "dot_bool":
+                    av = rng.integers(0, 2**63, (a, 200), dtype=np.uint64)
+                    bv = rng.integers(0, 2**63, (b, 200), dtype=np.uint64)
+                    fn = lambda: oc.dot_bool_pairs(av, bv)  # noqa: E731
+                else:
+                    av = rng.integers(0, 65536, (a, 12800), dtype=np.uint16)
+                    bv = rng.integers(0, 65536, (b, 12800), dtype=np.uint16)
+                    fn = lambda: oc.dot_u16_pairs(av, bv)  # noqa: E731
+                p, tt = _time_passes(fn, min(2.0, secs / 9))
+                shapes[f"{name}/{a * b}"] = a * b * p / tt
+        n = 10_000
+        db = oc.gen_templates(SEED, 0, n)
+        q = oc.gen_templates(SEED + 1, 0, 1)[0]
+        out = np.empty(n, np.float64)
+        passes, t = _time_passes(lambda: oc_lib.orc_template_distances_batch(oc._p(q), oc._p(db), n, oc._p(out), 1),
+                                 min(2.0, secs / 5))
+        value, unit = ROT * n * passes / t, "template comparisons/s"
+        extra["criterion_elements_per_s"] = shapes
+        sample = (f"configs[0]: {passes} passes of 1 query x 31 x {n} templates (Template::distance), one thread; "
+                  "criterion shapes of src/arch/mod.rs:29,53 timed with the same loop order")
+    else:  # load: a PCIe/page-cache path with no CPU compute counterpart (the reference mmaps)
+        return None
+    return {"value": value, "unit": unit, "cores": threads, "threads": threads, "kind": "port",
+            "sample": f"{sample}, {t:.2f} s, {threads} thread(s) on {info['model']}, {flags} oracle/iris_oracle.c",
+            "host": info, **extra}
 
 
 def load_traffic(workload, n_per_launch, layout):
@@ -186,12 +341,117 @@ def load_traffic(workload, n_per_launch, layout):
     return None, None
 
 
+# ---------------------------------------------------------------------------- launching
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args):
+    """`python bench.py --gpus N` (N > 1) without a launcher: run the N ranks under
+    torch.distributed.run as a CHILD process (nothing in this process has touched a GPU;
+    no exec) and return their exit status.  Refuses (rc 2) when the RCCL backend is asked
+    for more GPUs than are visible."""
+    backend = "gloo" if args.dry_run else os.environ.get("IRIS_DIST_BACKEND", "nccl")
+    if backend == "nccl":
+        import torch
+
+        have = torch.cuda.device_count()  # counts devices without initialising HIP
+        if have < args.gpus:
+            print(f"error: --gpus {args.gpus} needs {args.gpus} visible GPUs for one RCCL rank each; "
+                  f"{have} visible", file=sys.stderr)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(pathlib.Path(__file__).resolve()),
+           *sys.argv[1:]]
+    env = dict(os.environ, IRIS_BENCH_LAUNCHER="bench.py")
+    return subprocess.call(cmd, env=env)
+
+
+def init_ranks(args):
+    """Process-group setup for a multi-rank run.  Returns (dist module or None, world, rank,
+    device ordinal, backend, exchange device)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"error: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
+    # "nccl" is RCCL on ROCm (the exchange runs over xGMI); IRIS_DIST_BACKEND=gloo
+    # rehearses the same flow with CPU exchange tensors (e.g. 2 ranks on 1 GPU).
+    backend = "gloo" if args.dry_run else os.environ.get("IRIS_DIST_BACKEND", "nccl")
+    # IRIS_FORCE_DIST=1 runs the process-group path even for one rank (a one-GPU rehearsal of
+    # the RCCL exchange, barriers and max-over-ranks timing)
+    if world == 1 and os.environ.get("IRIS_FORCE_DIST") != "1":
+        return None, 1, 0, 0, None, "cpu"
+    import torch
+    import torch.distributed as dist
+
+    ordinal = local
+    if not args.dry_run:
+        have = torch.cuda.device_count()
+        if backend == "nccl" and local >= have:
+            raise SystemExit(f"error: rank {rank} (local {local}) has no GPU of its own: {have} visible")
+        ordinal = local % max(1, have)
+        torch.cuda.set_device(ordinal)
+    dist.init_process_group(backend, rank=rank, world_size=world)
+    if dist.get_world_size() != args.gpus:
+        raise SystemExit(f"error: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
+    xdev = f"cuda:{ordinal}" if backend == "nccl" else "cpu"
+    return dist, world, rank, ordinal, backend, xdev
+
+
+def launcher_name():
+    if os.environ.get("IRIS_BENCH_LAUNCHER"):
+        return "bench.py (torch.distributed.run child)"
+    return "torch.distributed.run" if "WORLD_SIZE" in os.environ else "none"
+
+
+def dry_run(args, dist, world, rank, backend):
+    """No GPU: each rank contributes a synthetic shard result (equal distances, so the
+    lowest global index — rank 0's — must win the merge, src/main.rs:616-621)."""
+    import iris_dist
+
+    n = args.n_per_gpu or 10_000_000
+    t0 = time.perf_counter()
+    local = ih.Match(0.25, rank * n + 7, 10, 40, -3, 0)
+    merged = iris_dist.allgather_merge(local, device="cpu") if dist is not None else local
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ok = merged.index == 7 and merged.distance == 0.25
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "template comparisons/s", "n_gpus": world,
+                          "ranks_seen": world, "backend": backend, "launcher": launcher_name(), "dry_run": True,
+                          "steps": 0, "warmup": 0, "ms_per_step": elapsed * 1e3, "higher_is_better": True,
+                          "scaling": "weak", "vs_baseline": None, "dtype": None, "data": "none (dry run)",
+                          "config": {"workload": "launcher rehearsal", "templates_per_gpu": n},
+                          "check": {"merged_index": int(merged.index), "ok": bool(ok)}}))
+    if dist is not None:
+        dist.destroy_process_group()
+    if not ok:
+        sys.exit(3)
+
+
+# ---------------------------------------------------------------------------- single-GPU lines
+
+
 def run_aux(args, dev):
     """Single-GPU lines for the §8(f) workloads beside the hot path: the fused
-    resolver (share sum + decode + argmin) and GPU share preparation."""
+    resolver (share sum + decode + argmin), GPU share preparation, file loading,
+    the host-slice engine calls and configs[0]'s criterion shapes."""
     P = args.parties
     rng = np.random.default_rng(SEED)
     ptrs = []
+    extra = {}
     if args.workload == "resolver":
         n = args.n_per_gpu
         shares = rng.integers(0, 65536, (P, n, ROT), dtype=np.uint16)
@@ -259,6 +519,36 @@ def run_aux(args, dev):
         workload = (f"{'DistanceEngine' if shares_wl else 'MasksEngine'}::batch_process(out, db: &[T]) over a host "
                     "slice (src/lib.rs:42-52, 69-79): H2D of the pageable slice (runtime-staged) + TILES pack per "
                     "256-MB chunk, then the engine kernel; PCIe-inclusive")
+    elif args.workload == "criterion":
+        # configs[0]: 1 query x 31 x 10k templates (resident), plus the arch shapes below
+        n = min(args.n_per_gpu, 10_000)
+        tdb = ih.Database(dev, ih.KIND_TEMPLATES, n)
+        tdb.generate(n, SEED)
+        query = gen_records(dev, ih.KIND_TEMPLATES, 1, SEED + 1)[0]
+        plant = plant_sites(n, 1)[0]
+        tdb.write(plant, planted_record(query, 9)[None, :])
+        eng = ih.TemplateEngine(dev, query)
+
+        def step():
+            return eng.search(tdb)
+
+        kname, unit = "template_search", "template comparisons/s"
+        rec_bytes = 3200
+        workload = ("configs[0]: 1 query x 31 rotations x 10k templates (cache-resident: plumbing, no roofline "
+                    "claim) + the criterion shapes of src/arch/mod.rs:22-72 through iris_dot_*_batch (host arrays)")
+        shapes = {}
+        for name, fn, shp, words, dt in (
+                ("dot_bool", ih.dot_bool_batch, [(1, 1), (1, 1000), (31, 1000), (1, 100_000)], 200, np.uint64),
+                ("dot_u16", ih.dot_u16_batch, [(1, 1), (1, 1000), (31, 1000), (1, 100_000), (31, 100_000)], 12800,
+                 np.uint16)):
+            for a, b in shp:
+                av = rng.integers(0, np.iinfo(dt).max, (a, words), dtype=dt)
+                bv = rng.integers(0, np.iinfo(dt).max, (b, words), dtype=dt)
+                fn(av, bv, dev)
+                p, tt = _time_passes(lambda: fn(av, bv, dev), 0.3, 200)
+                shapes[f"{name}/{a * b}"] = a * b * p / tt
+        extra["criterion_elements_per_s"] = shapes
+        extra["criterion_note"] = "all-pairs calls with host arrays in and out (PCIe and launch included)"
     else:
         n = min(args.n_per_gpu, 1_000_000)  # 3 share DBs of 1M = 77 GB
         tdb = ih.Database(dev, ih.KIND_TEMPLATES, n)
@@ -313,6 +603,9 @@ def run_aux(args, dev):
         ok = m == n and all((tdb.read(i, 1) == src.read(i, 1)).all() for i in sample)
         fpath.unlink()
         check = {"sampled_templates_vs_source": len(sample), "ok": bool(ok)}
+    elif args.workload == "criterion":
+        ok = m.index == plant and m.rotation == 9
+        check = {"planted_index": plant, "found_index": int(m.index), "rotation": int(m.rotation), "ok": bool(ok)}
     else:  # EncodedBits::share identity: the shares sum to encode(template); masks copied
         sample = [0, n // 3, n - 1]
         ok = True
@@ -322,14 +615,23 @@ def run_aux(args, dev):
             ok &= bool((total == ih.encode(ih.Template.from_array(t)).values).all())
             ok &= bool((mdb.read(i, 1)[0] == t[200:]).all())
         check = {"sampled_templates_share_identity": len(sample), "ok": bool(ok)}
+    cpu = None
+    if not args.no_cpu_baseline:
+        try:
+            cpu = cpu_baseline(args)
+        except Exception as ex:  # reported, never fatal
+            cpu = {"value": None, "error": str(ex)}
+    per_unit = ROT if args.workload == "criterion" else 1
     line = {
         "metric": {"resolver": "resolver records/s (share sum + decode + argmin)",
                    "resolve-masks": "resolver records/s (masks engine + share sum + decode + argmin, fused)",
                    "prepare": "templates prepared/s (shares + masks)",
                    "load": "templates loaded/s (file -> resident database, PCIe-inclusive)",
                    "host-shares": "share records/s through batch_process over host slices (PCIe-inclusive)",
-                   "host-masks": "mask records/s through batch_process over host slices (PCIe-inclusive)"}[args.workload],
-        "value": n * args.steps / elapsed, "unit": unit, "n_gpus": 1, "steps": args.steps,
+                   "host-masks": "mask records/s through batch_process over host slices (PCIe-inclusive)",
+                   "criterion": METRIC}[args.workload],
+        "value": per_unit * n * args.steps / elapsed, "unit": unit, "n_gpus": 1, "ranks_seen": 1, "backend": None,
+        "launcher": launcher_name(), "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None,
         "dtype": {"resolver": "u16 (wrapping share sums) -> u32 cross-multiplied fractions",
@@ -337,20 +639,24 @@ def run_aux(args, dev):
                   "prepare": "u32 (ChaCha keystream) -> u16 shares",
                   "load": "u8 (record bytes)",
                   "host-shares": "i8 MFMA -> i32 (u16 shares as biased byte planes)",
-                  "host-masks": "fp4 e2m1 MFMA -> f32 (0/1 products)"}[args.workload],
+                  "host-masks": "fp4 e2m1 MFMA -> f32 (0/1 products)",
+                  "criterion": "fp4 e2m1 MFMA -> f32 (0/+-1 products)"}[args.workload],
         "data": "synthetic (uniform random u16 / on-device generated templates)",
         "config": {"workload": workload, "records_per_gpu": n, "parties": P},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
                      "traffic": load_traffic(args.workload, n, "tiles")[0]
+                     if args.workload in ("resolver", "resolve-masks") else None,
+                     "traffic_source": "committed PMC bytes per record (profiles/), scaled to this launch"
                      if args.workload in ("resolver", "resolve-masks") else None},
         "kernel": {"name": kname, "avg_ms": kms / max(1, launches), "launches": launches,
                    "bytes_per_record": rec_bytes},
         "file_GBps": (n * 3200 * args.steps / elapsed / 1e9) if args.workload == "load" else None,
         "host_input_GBps": (n * rec_bytes * args.steps / elapsed / 1e9)
         if args.workload in ("host-shares", "host-masks") else None,
-        "cpu_baseline": None,
+        "cpu_baseline": cpu,
         "check": check,
+        **extra,
     }
     print(json.dumps(line))
     for p in ptrs:
@@ -362,27 +668,15 @@ def run_aux(args, dev):
 
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
-    dist = None
-    # "nccl" is RCCL on ROCm (the exchange runs over xGMI); IRIS_DIST_BACKEND=gloo
-    # rehearses the same flow with CPU exchange tensors (e.g. 2 ranks on 1 GPU).
-    backend = os.environ.get("IRIS_DIST_BACKEND", "nccl")
-    ordinal = local
-    # IRIS_FORCE_DIST=1 runs the process-group path even for one rank (a one-GPU rehearsal of
-    # the RCCL exchange, barriers and max-over-ranks timing)
-    if world > 1 or os.environ.get("IRIS_FORCE_DIST") == "1":
-        import torch
-        import torch.distributed as dist
-
-        ordinal = local % max(1, torch.cuda.device_count())
-        torch.cuda.set_device(ordinal)
-        dist.init_process_group(backend, rank=rank, world_size=world)
+    if args.gpus < 1:
+        raise SystemExit("error: --gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
+    dist, world, rank, ordinal, backend, xdev = init_ranks(args)
+    if args.dry_run:
+        return dry_run(args, dist, world, rank, backend)
+    if dist is not None:
         import iris_dist
-    xdev = f"cuda:{ordinal}" if backend == "nccl" else "cpu"
 
     if args.n_per_gpu is None:  # configs[1] at N=1; configs[4] (100M over 8 GPUs) at N=8
         args.n_per_gpu = 12_500_000 if (args.workload == "search" and world > 1) else 10_000_000
@@ -390,9 +684,9 @@ def main():
     lo = rank * n
     total = n * world
     dev = ih.Device(ordinal)
-    if args.workload in ("resolver", "resolve-masks", "prepare", "load", "host-shares", "host-masks"):
+    if args.workload in AUX_WORKLOADS:
         if world > 1:
-            raise SystemExit("workloads resolver / prepare are single-GPU lines (run without torchrun)")
+            raise SystemExit(f"workload {args.workload} is a single-GPU line (run without --gpus / torchrun)")
         return run_aux(args, dev)
     layout = ih.LAYOUT_TILES if args.layout == "tiles" else ih.LAYOUT_LANES
     kind = {"search": ih.KIND_TEMPLATES, "batch": ih.KIND_TEMPLATES, "masks": ih.KIND_MASKS,
@@ -403,16 +697,22 @@ def main():
     gen_s = time.time() - t0
 
     query = gen_records(dev, ih.KIND_TEMPLATES, 1, SEED + 1)[0]
-    plant_global = total * 3 // 4 + 12345
-    plant_rot = 9
     out_dev = None
     nq = args.queries if args.workload == "batch" else 1
-    if args.workload in ("search", "batch"):
-        if lo <= plant_global < lo + n:
-            db.write(plant_global - lo, planted_record(query, plant_rot)[None, :])
-    if args.workload == "batch":
+    # planted known answers: (query index, global index, rotation)
+    plants = []
+    if args.workload == "search":
+        plants = [(0, plant_sites(total, 1)[0], 9)]
+    elif args.workload == "batch":
         batch_q = gen_records(dev, ih.KIND_TEMPLATES, nq, SEED + 2)
-        batch_q[nq // 2] = query  # its best match is the planted record
+        batch_q[nq // 2] = query
+        pq = batch_plant_queries(nq)
+        rots = [9, -15, 15, 0, -7]
+        plants = [(q, site, rots[k % len(rots)]) for k, (q, site) in enumerate(zip(pq, plant_sites(total, len(pq))))]
+    for q, site, r in plants:
+        if lo <= site < lo + n:
+            src = query if args.workload == "search" else batch_q[q]
+            db.write(site - lo, planted_record(src, r)[None, :])
     if args.workload in ("masks", "shares"):
         out_dev = dev.alloc(n * ROT * 2)
     share_query = ih.encode(ih.Template.from_array(query)) if args.workload == "shares" else None
@@ -519,12 +819,17 @@ def main():
     kname = {"search": "template_search", "batch": "template_batch", "masks": "masks", "shares": "shares"}[args.workload]
     rec_bytes = {"search": BYTES_PER_TEMPLATE, "batch": BYTES_PER_TEMPLATE, "masks": 1600,
                  "shares": 25600}[args.workload]
-    if args.workload == "search":
-        ok = m.index == plant_global and m.rotation == plant_rot
-    elif args.workload == "batch":
-        mq = m[nq // 2]
-        ok = mq.index == plant_global and mq.rotation == plant_rot
-        m = mq
+    if args.workload in ("search", "batch"):
+        results = [m] if args.workload == "search" else m
+        found = [{"query": q, "planted_index": site, "found_index": int(results[q].index),
+                  "rotation": int(results[q].rotation), "planted_rotation": r,
+                  "distance": results[q].distance} for q, site, r in plants]
+        ok = all(f["found_index"] == f["planted_index"] and f["rotation"] == f["planted_rotation"] for f in found)
+        check = ({**found[0], "ok": bool(ok)} if args.workload == "search"
+                 else {"planted_queries": found, "query_groups": sorted({f["query"] // 4 for f in found}),
+                       "ok": bool(ok)})
+        if args.workload == "batch":
+            m = results[plants[0][0]]
     else:  # spot-check 64 outputs
         sample = np.random.default_rng(0).choice(n, 64, replace=False)
         full = np.empty((n, ROT), np.uint16)
@@ -533,6 +838,7 @@ def main():
         want = (check_masks_rows(query[200:], recs) if args.workload == "masks"
                 else check_shares_rows(ih.encode(ih.Template.from_array(query)).values, recs))
         ok = bool((full[sample] == want).all())
+        check = {"sampled_outputs_checked": 64, "ok": bool(ok)}
         del full
     launches, kms, items = dev.kernel_stats(kname)
     if launches == 0 and args.workload == "batch":  # a one-query batch runs the single-query search
@@ -550,9 +856,9 @@ def main():
 
     if rank == 0:
         cpu = None
-        if world == 1 and not args.no_cpu_baseline and args.workload == "search":
+        if world == 1 and not args.no_cpu_baseline:
             try:
-                cpu = cpu_baseline(args.cpu_seconds)
+                cpu = cpu_baseline(args)
             except Exception as ex:  # reported, never fatal
                 cpu = {"value": None, "error": str(ex)}
         line = {
@@ -560,6 +866,9 @@ def main():
             "value": value,
             "unit": "template comparisons/s",
             "n_gpus": world,
+            "ranks_seen": dist.get_world_size() if dist is not None else 1,
+            "backend": backend,
+            "launcher": launcher_name(),
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
@@ -587,12 +896,16 @@ def main():
             "roofline": ({
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                "traffic_source": ("committed PMC bytes per record (profiles/" + traffic_src + "), scaled to this launch")
+                if traffic_src else None,
             } if args.workload != "batch" else {
                 # compute-bound: fp4 MFMA FLOPs (2 per MAC) of the den + encode products
                 "bound": "mfma", "achieved": 2 * MFMA_MACS_PER_TEMPLATE * n * nq / (step_kernel_ms * 1e-3) / 1e12,
                 "peak": 2 * FP4_DENSE_PEAK_MACS / 1e12, "unit": "TFLOP/s",
                 "frac": MFMA_MACS_PER_TEMPLATE * n * nq / (step_kernel_ms * 1e-3) / FP4_DENSE_PEAK_MACS,
                 "traffic": traffic,
+                "traffic_source": ("committed PMC bytes per launch (profiles/" + traffic_src + ")")
+                if traffic_src else None,
             }),
             "kernel": {
                 "name": {("search", "tiles"): "template_mfma_kernel<MF_SEARCH> (fp4 MFMA)",
@@ -610,16 +923,13 @@ def main():
                                   if args.layout == "lanes" and args.workload == "search" else None),
                 "mfma_fp4_frac": (MFMA_MACS_PER_TEMPLATE * n * nq / (step_kernel_ms * 1e-3) / FP4_DENSE_PEAK_MACS
                                   if args.layout == "tiles" and args.workload in ("search", "batch") else None),
-                "traffic_source": traffic_src,
                 "traffic_note": ("FETCH_SIZE counts every L2 miss, Infinity-Cache hits included: the query tiles "
-                                 "(409 KB per 4 queries) are re-streamed from the 256-MB MALL for each N-group, "
+                                 "are re-streamed from the 256-MB MALL for each N-group, "
                                  "the template DB comes from HBM about once per XCD" if args.workload == "batch"
                                  else None),
             },
             "cpu_baseline": cpu,
-            "check": ({"planted_index": plant_global, "found_index": int(m.index), "rotation": int(m.rotation),
-                       "distance": m.distance, "ok": bool(ok)} if args.workload in ("search", "batch")
-                      else {"sampled_outputs_checked": 64, "ok": bool(ok)}),
+            "check": check,
             "setup": {"generate_s": gen_s, "prewarm_s": prewarm_s, "prewarm_steps": prewarm_steps},
         }
         print(json.dumps(line))
@@ -632,7 +942,7 @@ def main():
     if dist is not None:
         dist.destroy_process_group()
     if not ok:
-        print(f"result check failed: {m}", file=sys.stderr)
+        print(f"result check failed: {check}", file=sys.stderr)
         sys.exit(3)
 
 

@@ -1,0 +1,261 @@
+//! Safe layer over `libiris_hip.so` (MI355X / gfx950 kernels behind the C ABI of
+//! `include/iris_hip.h`), written as a module of the reference crate: drop
+//! `src/iris_hip/` next to `src/arch/hip.rs` and enable the `hip` feature
+//! (INTEGRATION.md lists the three lines that change in the crate).
+//!
+//! Ownership follows the C ABI: host buffers belong to the caller and are never
+//! retained after a call returns; device memory belongs to the handles here and is
+//! released on `Drop`.  Every handle keeps the `Device` it was created on alive.
+//! Errors are `Result<_, Error>`; the reference-signature wrappers in `engines`
+//! panic where the reference panics (`assert_eq!(out.len(), db.len())`,
+//! src/lib.rs:43,70) and on device errors, since the reference API has no
+//! `Result` to return.
+
+pub mod engines;
+pub mod ffi;
+
+use std::{
+    ffi::{CStr, CString},
+    fmt,
+    os::raw::c_int,
+    path::Path,
+    ptr,
+    sync::{Arc, OnceLock},
+};
+
+use crate::{Bits, EncodedBits, Template};
+
+/// A failed ABI call: the status code and `iris_last_error()`.
+#[derive(Debug, Clone, PartialEq, Eq)]
+pub struct Error {
+    pub code: i32,
+    pub message: String,
+}
+
+impl fmt::Display for Error {
+    fn fmt(&self, f: &mut fmt::Formatter<'_>) -> fmt::Result {
+        write!(f, "iris_hip error {}: {}", self.code, self.message)
+    }
+}
+
+impl std::error::Error for Error {}
+
+pub type Result<T> = std::result::Result<T, Error>;
+
+/// Turns an ABI status into a `Result`, reading the thread's last error message.
+pub fn check(rc: c_int) -> Result<()> {
+    if rc == ffi::IRIS_OK {
+        return Ok(());
+    }
+    let message = unsafe {
+        let p = ffi::iris_last_error();
+        if p.is_null() {
+            String::new()
+        } else {
+            CStr::from_ptr(p).to_string_lossy().into_owned()
+        }
+    };
+    Err(Error { code: rc, message })
+}
+
+struct DeviceInner(*mut ffi::IrisDevice);
+
+// The library serialises calls per device internally (include/iris_hip.h, "Handles are
+// thread-safe"), as the reference engines are `Sync` and shared by rayon workers.
+unsafe impl Send for DeviceInner {}
+unsafe impl Sync for DeviceInner {}
+
+impl Drop for DeviceInner {
+    fn drop(&mut self) {
+        unsafe {
+            ffi::iris_device_close(self.0);
+        }
+    }
+}
+
+/// One gfx950 device and its stream; cheap to clone (shared handle).
+#[derive(Clone)]
+pub struct Device(Arc<DeviceInner>);
+
+impl Device {
+    pub fn open(ordinal: i32) -> Result<Self> {
+        let mut raw = ptr::null_mut();
+        check(unsafe { ffi::iris_device_open(ordinal, &mut raw) })?;
+        Ok(Device(Arc::new(DeviceInner(raw))))
+    }
+
+    pub fn count() -> Result<i32> {
+        let mut n: c_int = 0;
+        check(unsafe { ffi::iris_device_count(&mut n) })?;
+        Ok(n)
+    }
+
+    pub fn raw(&self) -> *mut ffi::IrisDevice {
+        self.0 .0
+    }
+
+    pub fn synchronize(&self) -> Result<()> {
+        check(unsafe { ffi::iris_device_synchronize(self.raw()) })
+    }
+
+    /// (free, total) device memory in bytes.
+    pub fn memory(&self) -> Result<(usize, usize)> {
+        let (mut free, mut total) = (0usize, 0usize);
+        check(unsafe { ffi::iris_device_memory(self.raw(), &mut free, &mut total) })?;
+        Ok((free, total))
+    }
+}
+
+static DEFAULT_DEVICE: OnceLock<Device> = OnceLock::new();
+
+/// The process-wide device behind the reference-signature entry points
+/// (`arch::dot_bool`, `DistanceEngine::new`, ...), which take no device argument:
+/// ordinal `IRIS_HIP_DEVICE` (default 0), opened on first use.  Panics if no
+/// gfx950 device can be opened — there is no CPU fallback behind this backend.
+pub fn default_device() -> &'static Device {
+    DEFAULT_DEVICE.get_or_init(|| {
+        let ordinal = std::env::var("IRIS_HIP_DEVICE").ok().and_then(|s| s.parse().ok()).unwrap_or(0);
+        Device::open(ordinal).unwrap_or_else(|e| panic!("iris_hip: cannot open device {ordinal}: {e}"))
+    })
+}
+
+/// Record types a device database can hold: the reference's POD value types, whose
+/// bytes are exactly the C ABI's record layouts (bytemuck views, src/bits.rs:13-15,
+/// src/encoded_bits.rs:13-15, src/template.rs:11-29).
+///
+/// # Safety
+/// `Self` must be `#[repr(C)]`/`#[repr(transparent)]` with the size of the kind's record.
+pub unsafe trait Record: Copy {
+    const KIND: c_int;
+}
+
+unsafe impl Record for Bits {
+    const KIND: c_int = ffi::IRIS_KIND_MASKS;
+}
+unsafe impl Record for EncodedBits {
+    const KIND: c_int = ffi::IRIS_KIND_SHARES;
+}
+unsafe impl Record for Template {
+    const KIND: c_int = ffi::IRIS_KIND_TEMPLATES;
+}
+
+/// A device-resident database of one record kind (the GPU's replacement for the
+/// mmap'd share / masks files, src/main.rs:389,458).
+pub struct Database {
+    raw: *mut ffi::IrisDb,
+    kind: c_int,
+    device: Device,
+}
+
+unsafe impl Send for Database {}
+unsafe impl Sync for Database {}
+
+impl Database {
+    pub fn new<T: Record>(device: &Device, capacity: u64) -> Result<Self> {
+        let mut raw = ptr::null_mut();
+        check(unsafe { ffi::iris_db_create(device.raw(), T::KIND, capacity, &mut raw) })?;
+        Ok(Database { raw, kind: T::KIND, device: device.clone() })
+    }
+
+    pub fn raw(&self) -> *mut ffi::IrisDb {
+        self.raw
+    }
+
+    pub fn kind(&self) -> c_int {
+        self.kind
+    }
+
+    pub fn device(&self) -> &Device {
+        &self.device
+    }
+
+    pub fn len(&self) -> u64 {
+        let mut n = 0u64;
+        check(unsafe { ffi::iris_db_len(self.raw, &mut n) }).map(|_| n).unwrap_or(0)
+    }
+
+    pub fn is_empty(&self) -> bool {
+        self.len() == 0
+    }
+
+    fn expect_kind<T: Record>(&self) -> Result<()> {
+        if T::KIND != self.kind {
+            return Err(Error { code: ffi::IRIS_E_ARG, message: "record kind does not match the database".into() });
+        }
+        Ok(())
+    }
+
+    pub fn append<T: Record>(&mut self, records: &[T]) -> Result<()> {
+        self.expect_kind::<T>()?;
+        check(unsafe { ffi::iris_db_append(self.raw, records.as_ptr().cast(), records.len() as u64) })
+    }
+
+    pub fn write<T: Record>(&mut self, index: u64, records: &[T]) -> Result<()> {
+        self.expect_kind::<T>()?;
+        check(unsafe { ffi::iris_db_write(self.raw, index, records.as_ptr().cast(), records.len() as u64) })
+    }
+
+    pub fn read<T: Record>(&self, first: u64, out: &mut [T]) -> Result<()> {
+        self.expect_kind::<T>()?;
+        check(unsafe { ffi::iris_db_read(self.raw, first, out.len() as u64, out.as_mut_ptr().cast()) })
+    }
+
+    /// Appends records [first, first + count) of a raw record file (`.masks`,
+    /// `.share-i`, raw templates; `count = u64::MAX`: to the end).  A file that is not
+    /// a whole number of records is rejected like the reference's `try_cast_slice`.
+    pub fn load_file(&mut self, path: &Path, first: u64, count: u64) -> Result<u64> {
+        let c = path_cstring(path)?;
+        let mut loaded = 0u64;
+        check(unsafe { ffi::iris_db_load_file(self.raw, c.as_ptr(), first, count, &mut loaded) })?;
+        Ok(loaded)
+    }
+
+    pub fn save_file(&self, path: &Path, first: u64, n: u64) -> Result<()> {
+        let c = path_cstring(path)?;
+        check(unsafe { ffi::iris_db_save_file(self.raw, c.as_ptr(), first, n) })
+    }
+}
+
+impl Drop for Database {
+    fn drop(&mut self) {
+        unsafe {
+            ffi::iris_db_destroy(self.raw);
+        }
+    }
+}
+
+fn path_cstring(path: &Path) -> Result<CString> {
+    use std::os::unix::ffi::OsStrExt;
+    CString::new(path.as_os_str().as_bytes())
+        .map_err(|_| Error { code: ffi::IRIS_E_ARG, message: "path contains a NUL byte".into() })
+}
+
+/// `(min_distance, min_index)` as the reference's resolver reports them
+/// (src/main.rs:581-582, 616-621): `usize::MAX` and +inf when nothing matched.
+pub fn match_to_pair(m: &ffi::IrisMatch) -> (f64, usize) {
+    let index = if m.index == u64::MAX { usize::MAX } else { m.index as usize };
+    (m.distance, index)
+}
+
+/// The resolver's aggregation (src/main.rs:597-621) over host arrays: wrapping sum
+/// of every participant's `[u16; 31]`, `decode_distance`, first strict minimum.
+pub fn resolver_search(shares: &[&[[u16; 31]]], denominators: &[[u16; 31]]) -> (f64, usize) {
+    for s in shares {
+        assert_eq!(s.len(), denominators.len());
+    }
+    let ptrs: Vec<*const u16> = shares.iter().map(|s| s.as_ptr().cast::<u16>()).collect();
+    let mut m = ffi::IrisMatch::default();
+    check(unsafe {
+        ffi::iris_resolver_search_host(
+            default_device().raw(),
+            ptrs.as_ptr(),
+            ptrs.len() as u32,
+            denominators.as_ptr().cast(),
+            denominators.len() as u64,
+            0,
+            &mut m,
+        )
+    })
+    .unwrap_or_else(|e| panic!("resolver_search: {e}"));
+    match_to_pair(&m)
+}

@@ -115,6 +115,18 @@ uint16_t orc_dot_u16(const uint16_t a[ORC_BITS], const uint16_t b[ORC_BITS]) {
     return (uint16_t)s;
 }
 
+/* The criterion harness (src/arch/mod.rs:22-72): for b in db { for a in queries { f(a, b) } },
+ * one thread, as criterion runs it. */
+void orc_dot_bool_pairs(const uint64_t *a, uint64_t na, const uint64_t *b, uint64_t nb, uint16_t *out) {
+    for (uint64_t j = 0; j < nb; ++j)
+        for (uint64_t i = 0; i < na; ++i) out[j * na + i] = orc_dot_bool(a + i * ORC_LIMBS, b + j * ORC_LIMBS);
+}
+
+void orc_dot_u16_pairs(const uint16_t *a, uint64_t na, const uint16_t *b, uint64_t nb, uint16_t *out) {
+    for (uint64_t j = 0; j < nb; ++j)
+        for (uint64_t i = 0; i < na; ++i) out[j * na + i] = orc_dot_u16(a + i * ORC_BITS, b + j * ORC_BITS);
+}
+
 /* ------------------------------------------------------------ threading */
 
 typedef void (*range_fn)(void *ctx, uint64_t lo, uint64_t hi);

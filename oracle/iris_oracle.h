@@ -40,6 +40,10 @@ void orc_encode(const orc_template *t, uint16_t out[ORC_BITS]);
 /* arch kernels */
 uint16_t orc_dot_bool(const uint64_t a[ORC_LIMBS], const uint64_t b[ORC_LIMBS]);
 uint16_t orc_dot_u16(const uint16_t a[ORC_BITS], const uint16_t b[ORC_BITS]);
+/* the criterion harness loop (src/arch/mod.rs:34-41, 62-69): for b in db { for a in queries },
+ * single-threaded; out[j*na + i] = dot(a[i], b[j]) */
+void orc_dot_bool_pairs(const uint64_t *a, uint64_t na, const uint64_t *b, uint64_t nb, uint16_t *out);
+void orc_dot_u16_pairs(const uint16_t *a, uint64_t na, const uint16_t *b, uint64_t nb, uint16_t *out);
 
 /* engines (batch_process); out is [n][31] */
 void orc_masks_batch(const uint64_t query[ORC_LIMBS], const uint64_t *db, uint64_t n, uint16_t *out, int threads);

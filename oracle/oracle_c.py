@@ -42,6 +42,8 @@ def load(path=None):
     lib.orc_dot_bool.restype = ctypes.c_uint16
     lib.orc_dot_u16.argtypes = [P, P]
     lib.orc_dot_u16.restype = ctypes.c_uint16
+    lib.orc_dot_bool_pairs.argtypes = [P, u64, P, u64, P]
+    lib.orc_dot_u16_pairs.argtypes = [P, u64, P, u64, P]
     lib.orc_masks_batch.argtypes = [P, P, u64, P, i32]
     lib.orc_distance_batch.argtypes = [P, P, u64, P, i32]
     lib.orc_template_distance.argtypes = [P, P]
@@ -102,6 +104,24 @@ def dot_bool(a, b):
 
 def dot_u16(a, b):
     return int(load().orc_dot_u16(_p(np.ascontiguousarray(a, np.uint16)), _p(np.ascontiguousarray(b, np.uint16))))
+
+
+def dot_bool_pairs(a, b):
+    """out[j, i] = dot_bool(a[i], b[j]), the criterion loop order (src/arch/mod.rs:34-41)."""
+    a = np.ascontiguousarray(a, np.uint64).reshape(-1, LIMBS)
+    b = np.ascontiguousarray(b, np.uint64).reshape(-1, LIMBS)
+    out = np.empty((b.shape[0], a.shape[0]), np.uint16)
+    load().orc_dot_bool_pairs(_p(a), a.shape[0], _p(b), b.shape[0], _p(out))
+    return out
+
+
+def dot_u16_pairs(a, b):
+    """out[j, i] = dot_u16(a[i], b[j]) (src/arch/mod.rs:62-69)."""
+    a = np.ascontiguousarray(a, np.uint16).reshape(-1, BITS)
+    b = np.ascontiguousarray(b, np.uint16).reshape(-1, BITS)
+    out = np.empty((b.shape[0], a.shape[0]), np.uint16)
+    load().orc_dot_u16_pairs(_p(a), a.shape[0], _p(b), b.shape[0], _p(out))
+    return out
 
 
 def masks_batch(query_mask, db, threads=None):

@@ -24,7 +24,7 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, n, seed, q, result_path):
+def _worker(rank, world, port, n, seed, q, plants, result_path):
     sys.path.insert(0, str(ROOT))
     sys.path.insert(0, str(ROOT / "mpc-iris-code_amd"))
     import iris_dist
@@ -35,6 +35,9 @@ def _worker(rank, world, port, n, seed, q, result_path):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     lo, hi = iris_dist.shard_range(n, rank, world)
     db = oc.gen_templates(seed, lo, hi - lo)
+    for dst, src in plants:  # copies of record src planted at global index dst
+        if lo <= dst < hi:
+            db[dst - lo] = oc.gen_templates(seed, src, 1)[0]
     d = oc.template_distances(q, db, threads=1)
     best, idx = oc.argmin(d)
     if idx != 2**64 - 1:
@@ -66,11 +69,22 @@ def test_gloo_shard_merge(tmp_path, world):
     full = oc.gen_templates(seed, 0, n)
     q = full[1234].copy()
     q[:200] ^= np.uint64(1)  # near-duplicate of 1234
-    # plant a second, equal-distance copy later so the tie-break crosses shards
+    # plant a second, equal-distance copy of 1234 in the LAST shard, so the global minimum
+    # is tied across shards and only the lowest-index rule (src/main.rs:616-621, strict <
+    # in a sequential scan) applied by iris_match_merge picks 1234
+    plants = [(2500, 1234)]
+    full[2500] = full[1234]
+    d_full = oc.template_distances(q, full)
+    spans = [iris_dist.shard_range(n, r, world) for r in range(world)]
+    assert spans[0][0] <= 1234 < spans[0][1] and spans[-1][0] <= 2500 < spans[-1][1]
+    shard_min = [oc.argmin(d_full[lo:hi]) for lo, hi in spans]
+    assert shard_min[0][0] == shard_min[-1][0]  # a real cross-shard tie
+    assert shard_min[-1][1] + spans[-1][0] == 2500
     result = tmp_path / "r.npy"
-    mp.spawn(_worker, args=(world, _free_port(), n, seed, q, str(result)), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), n, seed, q, plants, str(result)), nprocs=world, join=True)
     got = np.load(result)
-    want_d, want_i = oc.argmin(oc.template_distances(q, full))
+    want_d, want_i = oc.argmin(d_full)
+    assert want_i == 1234
     assert got[0] == want_d and int(got[1]) == want_i
     assert got[4] == got[0] and got[5] == got[1]              # batched merge == single merge
     assert got[6] == np.inf and got[7] == float(2**64 - 1)     # no candidate on any rank

@@ -38,7 +38,37 @@ def test_bench_two_ranks(workload):
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["check"]["ok"]
     assert d["config"]["total_templates"] == 400000
-    assert d["check"]["planted_index"] >= 200000  # the answer lives in rank 1's shard
+    assert d["ranks_seen"] == 2 and d["backend"] == "gloo"
+    found = [d["check"]] if workload == "search" else d["check"]["planted_queries"]
+    assert found[0]["planted_index"] >= 200000  # the first answer lives in rank 1's shard
+    if workload == "batch":
+        assert len(found) == 4 and len(d["check"]["query_groups"]) >= 2
+
+
+def test_bench_self_launch_two_ranks():
+    """`python bench.py --gpus 2` with no launcher starts both ranks itself (here on the one
+    GPU, gloo exchange) and prints one line with n_gpus 2."""
+    env = dict(os.environ, IRIS_DIST_BACKEND="gloo")
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1", "--n-per-gpu",
+           "200000", "--no-cpu-baseline", "--prewarm-s", "0.2"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["ranks_seen"] == 2 and d["check"]["ok"]
+    assert d["launcher"].startswith("bench.py")
+
+
+def test_bench_more_gpus_than_visible_fails():
+    """`python bench.py --gpus 8` on a one-GPU box (RCCL backend) refuses instead of
+    printing a one-GPU line."""
+    env = dict(os.environ)
+    env.pop("IRIS_DIST_BACKEND", None)
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "8", "--steps", "1"], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode != 0
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
 
 
 def test_rccl_exchange_single_rank():
