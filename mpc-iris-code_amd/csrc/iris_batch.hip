@@ -331,6 +331,270 @@ __global__ void __launch_bounds__(256) batch_reduce_kernel(const Partial *__rest
     }
 }
 
+// ---------------------------------------------------------------------------- batch_lds_kernel
+//
+// The same GEMM (M = 32 rows per query, N = templates, K = 12800 bits, den + encode
+// products) with the operand traffic re-balanced for the VALU:
+//
+//   workgroup (8 waves) = 4 queries (shared by all 8 waves) x 8 template tiles (one per wave)
+//   K-step              = GP chunk pairs
+//
+// - A (the 4 queries' rotation tiles) is loaded once per workgroup and K-step (2 rows of
+//   1 KB per wave, plain global loads a step ahead), expanded ONCE into the MFMA-ready fp4
+//   den / encode fragments and written to a 2-stage LDS ring; every wave reads all four
+//   queries' fragments from it (ds_read_b128, lane-linear 1-KB rows: conflict-free).
+//   batch_kernel instead re-expands every A fragment in each of the 4 waves that use it.
+// - B (templates): each wave owns one tile per N-group and loads it straight into
+//   registers (global_load_dwordx4, 1 KB per wave and chunk pair, one K-step ahead) —
+//   no LDS-DMA (whose issue cost, ~60 cycles per 1-KB piece beside MFMAs, was ~17 % of
+//   batch_kernel) — and expands it itself (10 VALU per 64-bit chunk).
+// - VALU per MFMA: 20 (B) + 12 (this wave's share of the A expansion) per 16 MFMAs,
+//   against 88 in batch_kernel; one s_barrier per K-step.
+// The grid holds one workgroup per CU; all query groups walk the same N-groups, so a
+// template tile comes from HBM about once per XCD and from L2 after that.
+#ifndef IRIS_BATCH2_GP
+#define IRIS_BATCH2_GP 4
+#endif
+// Diagnostic builds (tools/, never the shipped library; results wrong by design):
+// IRIS_BATCH2_DIAG = 1 no s_barrier, 2 no LDS fragment reads (the B operands stand in),
+// 3 no B loads after the first step, 4 no A loads / expansion after the first step,
+// 5 no MFMAs (a VALU fold keeps the operands live)
+#ifndef IRIS_BATCH2_DIAG
+#define IRIS_BATCH2_DIAG 0
+#endif
+// 1: block b + 1's fragment reads issued between block b's MFMAs; 0: each block reads its own
+#ifndef IRIS_BATCH2_ROLL
+#define IRIS_BATCH2_ROLL 1
+#endif
+namespace lds2 {
+constexpr int kBQ = 4;                   // queries per workgroup (must equal batch_kernel's: padding)
+constexpr int kGP = IRIS_BATCH2_GP;      // chunk pairs per K-step
+constexpr int kSteps = kPlaneGroups / kGP;
+constexpr int kArows = kBQ * kGP;        // compact A rows (1 KB) per K-step
+constexpr int kTilesPerGroup = 8;        // template tiles per N-group (NW waves x WT tiles)
+static_assert(kPlaneGroups % kGP == 0, "K-step must tile the 100 chunk pairs");
+static_assert(kBQ == IRIS_BATCH_BQ, "query groups must pad like batch_kernel's");
+}  // namespace lds2
+
+// NW waves x WT tiles per wave = 8 tiles per N-group: NW = 8, WT = 1 (two waves per SIMD,
+// 128 accumulator registers) or NW = 4, WT = 2 (one wave per SIMD, 256 accumulators).
+template <int NW, int WT>
+__global__ void __launch_bounds__(64 * NW, 1)
+    batch_lds_kernel(const uint4 *__restrict__ db, const uint4 *__restrict__ qtiles, uint64_t tile0, uint64_t ntiles,
+                     uint64_t first, uint64_t end, uint32_t nqg, uint32_t G, Partial *__restrict__ partials) {
+    using namespace lds2;
+    static_assert(NW * WT == kTilesPerGroup && kArows % NW == 0, "geometry");
+    constexpr int kAper = kArows / NW;  // compact A rows per wave and K-step
+    // [stage][chunk pair][query][den h0, enc h0, den h1, enc h1][lane]: 2 x kGP x 16 KB
+    __shared__ uint4 afrag[2][kGP][kBQ][4][64];
+
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint32_t qg = blockIdx.x % nqg, gi = blockIdx.x / nqg;
+    const uint64_t ngroups = (ntiles + kTilesPerGroup - 1) / kTilesPerGroup;
+    const uint32_t my_groups = gi < ngroups ? (uint32_t)((ngroups - gi + G - 1) / G) : 0;
+    const uint32_t total = my_groups * kSteps;
+
+    // this wave's compact A rows of a K-step: r = w + NW i -> query r % kBQ, chunk pair r / kBQ
+    const uint4 *abase = qtiles + (uint64_t)(qg * kBQ) * kTileU4 + lane;
+    auto load_a = [&](uint32_t s, uint4 (&aq)[kAper]) {
+        const uint32_t k = s % kSteps;
+#pragma unroll
+        for (int i = 0; i < kAper; ++i) {
+            const int r = w + NW * i;
+            aq[i] = abase[(uint64_t)(r % kBQ) * kTileU4 + (k * kGP + r / kBQ) * 64];
+        }
+    };
+    auto b_row = [&](uint32_t s, int t) {  // tile t of this wave, chunk pair 0 of K-step s
+        const uint32_t j = s / kSteps, k = s - j * kSteps;
+        const uint64_t trel = (gi + (uint64_t)j * G) * kTilesPerGroup + w * WT + t;
+        return db + (tile0 + (trel < ntiles ? trel : ntiles - 1)) * (uint64_t)kTileU4 + (k * kGP) * 64 + lane;
+    };
+    // compact A row -> fp4 den / encode fragments of both chunks (the expansion of batch_kernel)
+    auto store_a = [&](uint32_t s, const uint4 (&aq)[kAper]) {
+#pragma unroll
+        for (int i = 0; i < kAper; ++i) {
+            const int r = w + NW * i, qi = r % kBQ, gp = r / kBQ;
+            uint4(*dst)[64] = afrag[s & 1][gp][qi];
+#pragma unroll
+            for (int h2 = 0; h2 < 2; ++h2) {
+                const uint32_t ax = h2 ? aq[i].z : aq[i].x, ay = h2 ? aq[i].w : aq[i].y;
+                dst[2 * h2][lane] = make_uint4(ax & 0x22222222u, (ax & 0x11111111u) << 2, ay & 0x22222222u,
+                                               (ay & 0x11111111u) << 2);
+                dst[2 * h2 + 1][lane] = make_uint4(ax & 0xAAAAAAAAu, (ax << 1) & 0xAAAAAAAAu, ay & 0xAAAAAAAAu,
+                                                   (ay << 1) & 0xAAAAAAAAu);
+            }
+        }
+    };
+    auto barrier = [] {
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's fragment writes landed; loads stay in flight
+        if (IRIS_BATCH2_DIAG != 1) __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    };
+    auto mma = [](const v8i &a, const v8i &b, const v16f &c) {
+#if IRIS_BATCH2_DIAG == 5
+        v16f r = c;
+        r[0] += __builtin_bit_cast(float, (a[0] ^ b[1]) & 1);
+        return r;
+#else
+        return mfma4(a, b, c);
+#endif
+    };
+
+    // running best per query, lane-distributed: lane qi (< kBQ) holds query qi's
+    Partial best = partial_none();
+    v16f den[kBQ][WT], sacc[kBQ][WT];
+    auto zero = [&] {
+#pragma unroll
+        for (int qi = 0; qi < kBQ; ++qi)
+#pragma unroll
+            for (int t = 0; t < WT; ++t)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    den[qi][t][i] = 0.f;
+                    sacc[qi][t][i] = 0.f;
+                }
+    };
+    zero();
+    if (NW == 8 && w >= NW / 2) __builtin_amdgcn_s_setprio(1);  // the younger half (see batch_kernel)
+
+    // B rolls through bq: chunk pair g of step s + 1 is loaded into bq[t][g] as soon as step s
+    // has expanded both of its chunks — one K-step of latency cover
+    uint4 bq[WT][kGP];
+    if (total) {
+        uint4 aq[kAper];
+        load_a(0, aq);
+#pragma unroll
+        for (int t = 0; t < WT; ++t) {
+            const uint4 *src = b_row(0, t);
+#pragma unroll
+            for (int g = 0; g < kGP; ++g) bq[t][g] = src[g * 64];
+        }
+        store_a(0, aq);
+        barrier();
+    }
+#pragma unroll 1
+    for (uint32_t s = 0; s < total; ++s) {
+        // A(s + 1) is loaded first, so waiting for it leaves step s + 1's B loads in flight;
+        // branch-free: the last step re-loads its own rows (harmless) instead of skipping
+        const uint32_t s1 = s + 1 < total ? s + 1 : s;
+        uint4 aq[kAper];
+        if (IRIS_BATCH2_DIAG != 4 || s == 0) load_a(s1, aq);
+        const uint4(*st)[kBQ][4][64] = afrag[s & 1];
+        // blocks b = 2 gp + h2 (one 64-bit chunk): block b + 1's fragment reads are issued
+        // between block b's MFMAs (rolling: their latency hides behind the MFMAs)
+        auto frag = [&](int b, int form, int qi) {
+#if IRIS_BATCH2_DIAG == 2
+            const uint4 q = bq[0][b >> 1];
+            return form ? make_uint4(q.x & 0xAAAAAAAAu, q.y & 0xAAAAAAAAu, q.z & 0xAAAAAAAAu, q.w ^ qi)
+                        : make_uint4(q.x & 0x22222222u, q.y & 0x11111111u, q.z & 0x22222222u, q.w & qi);
+#else
+            return st[b >> 1][qi][2 * (b & 1) + form][lane];
+#endif
+        };
+        uint4 fa[kBQ], fe[kBQ];
+#pragma unroll
+        for (int qi = 0; qi < kBQ; ++qi) {
+            fa[qi] = frag(0, 0, qi);
+            fe[qi] = frag(0, 1, qi);
+        }
+#pragma unroll
+        for (int b = 0; b < 2 * kGP; ++b) {
+            const bool nb = b + 1 < 2 * kGP;
+            v8i bd[WT], be[WT];
+#pragma unroll
+            for (int t = 0; t < WT; ++t) {
+                const uint4 q = bq[t][b >> 1];
+                const uint32_t bx = (b & 1) ? q.z : q.x, by = (b & 1) ? q.w : q.y;
+                bd[t] = v8i{(int)(bx & 0x22222222u), (int)(bx & 0x11111111u), (int)(by & 0x22222222u),
+                            (int)(by & 0x11111111u), 0, 0, 0, 0};
+                be[t] = v8i{(int)(bx & 0xAAAAAAAAu), (int)((bx << 1) & 0xAAAAAAAAu), (int)(by & 0xAAAAAAAAu),
+                            (int)((by << 1) & 0xAAAAAAAAu), 0, 0, 0, 0};
+            }
+            if ((b & 1) && (IRIS_BATCH2_DIAG != 3 || s == 0)) {  // both chunks of chunk pair b >> 1 expanded: its registers take step s + 1's
+#pragma unroll
+                for (int t = 0; t < WT; ++t) bq[t][b >> 1] = b_row(s1, t)[(b >> 1) * 64];
+            }
+            uint4 na[kBQ], ne[kBQ];
+#pragma unroll
+            for (int qi = 0; qi < kBQ; ++qi) {
+                if (!IRIS_BATCH2_ROLL) {
+                    fa[qi] = frag(b, 0, qi);
+                    fe[qi] = frag(b, 1, qi);
+                }
+                const v8i a_d = {(int)fa[qi].x, (int)fa[qi].y, (int)fa[qi].z, (int)fa[qi].w, 0, 0, 0, 0};
+                const v8i a_e = {(int)fe[qi].x, (int)fe[qi].y, (int)fe[qi].z, (int)fe[qi].w, 0, 0, 0, 0};
+#pragma unroll
+                for (int t = 0; t < WT; ++t) den[qi][t] = mma(a_d, bd[t], den[qi][t]);
+                if (nb && IRIS_BATCH2_ROLL) na[qi] = frag(b + 1, 0, qi);
+#pragma unroll
+                for (int t = 0; t < WT; ++t) sacc[qi][t] = mma(a_e, be[t], sacc[qi][t]);
+                if (nb && IRIS_BATCH2_ROLL) ne[qi] = frag(b + 1, 1, qi);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            if (nb && IRIS_BATCH2_ROLL) {
+#pragma unroll
+                for (int qi = 0; qi < kBQ; ++qi) {
+                    fa[qi] = na[qi];
+                    fe[qi] = ne[qi];
+                }
+            }
+        }
+        if (IRIS_BATCH2_DIAG != 4 || s == 0) store_a(s + 1, aq);  // the last step fills the idle stage (read by nobody)
+        const uint32_t j = s / kSteps;
+        if (s - j * kSteps == kSteps - 1) {  // N-group done: this wave's tiles, every query
+#pragma unroll
+            for (int t = 0; t < WT; ++t) {
+                const uint64_t trel = (gi + (uint64_t)j * G) * kTilesPerGroup + w * WT + t;
+                const uint64_t tg = (tile0 + trel) * 32 + (lane & 31);
+                const bool valid = trel < ntiles && tg >= first && tg < end;
+#pragma unroll
+                for (int qi = 0; qi < kBQ; ++qi) {
+                    uint32_t bn, bd;
+                    int br;
+                    best_rotation(lane, [&](int r, uint32_t &nn, uint32_t &dd) {
+                        dd = (uint32_t)den[qi][t][r];
+                        nn = (uint32_t)(((int)dd - (int)sacc[qi][t][r]) >> 1);
+                    }, bn, bd, br);
+                    Partial c;
+                    c.num = bn;
+                    c.den = valid ? bd : 0;
+                    c.rot = br;
+                    c.pad = 0;
+                    c.idx = tg - first;
+                    // the wave's best of this tile for query qi, handed to lane qi
+#pragma unroll
+                    for (int off = 32; off >= 1; off >>= 1) {
+                        const Partial o = partial_shfl_xor(c, off);
+                        if (partial_better_dev(o, c)) c = o;
+                    }
+                    if (lane == qi && partial_better_dev(c, best)) best = c;
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+            zero();
+        }
+        barrier();
+    }
+
+    __syncthreads();
+    Partial *sP = (Partial *)&afrag[0][0][0][0][0];  // [wave][query]
+    if (lane < kBQ) sP[w * kBQ + lane] = best;
+    __syncthreads();
+    if (tid < kBQ) {
+        Partial b = sP[tid];
+        for (int ww = 1; ww < NW; ++ww)
+            if (partial_better_dev(sP[ww * kBQ + tid], b)) b = sP[ww * kBQ + tid];
+        partials[(uint64_t)(qg * kBQ + tid) * G + gi] = b;
+    }
+}
+
+// 2 = batch_lds_kernel (default), 1 = batch_kernel; read per launch so tests can run both
+static int batch_kernel_choice() {
+    const char *e = getenv("IRIS_BATCH_KERNEL");
+    return e && atoi(e) == 1 ? 1 : 2;
+}
+
 uint32_t batch_query_group() { return BQ; }
 
 BatchGeometry batch_geometry(LaunchRange r, uint32_t nq) {
@@ -340,13 +604,16 @@ BatchGeometry batch_geometry(LaunchRange r, uint32_t nq) {
     g.ntiles = tile1 - g.tile0;
     g.nqg = (nq + BQ - 1) / BQ;
     const uint64_t ngroups = (g.ntiles + BT - 1) / BT;
-    uint64_t G = (512 + g.nqg - 1) / g.nqg;  // ~2 workgroups per CU in total
+    // batch_kernel: ~2 workgroups per CU in total; batch_lds_kernel (one 128-KB-LDS workgroup
+    // per CU): one round of workgroups
+    const uint64_t want = batch_kernel_choice() >= 2 ? resident_blocks(1) : 512;
+    uint64_t G = (want + g.nqg - 1) / g.nqg;
     if (G > ngroups) G = ngroups ? ngroups : 1;
     g.G = (uint32_t)G;
     g.xqg = 0;
     // XCD-aware grid (IRIS_BATCH_XQG = query groups per XCD per round): the 32 CUs of an XCD
     // run xqg query groups x 32/xqg N-slices, so their query tiles stay in that XCD's L2
-    if (const char *e = getenv("IRIS_BATCH_XQG")) {
+    if (const char *e = batch_kernel_choice() >= 2 ? nullptr : getenv("IRIS_BATCH_XQG")) {
         const uint32_t x = (uint32_t)atoi(e);
         if (x && 32 % x == 0 && g.nqg % (8 * x) == 0 && ngroups >= 32 / x) {
             g.xqg = x;
@@ -359,9 +626,15 @@ BatchGeometry batch_geometry(LaunchRange r, uint32_t nq) {
 int launch_batch(void *stream, const void *db, const void *qtiles, LaunchRange r, const BatchGeometry &g,
                  Partial *partials, Partial *out) {
     if (r.n == 0) return 0;
-    hipLaunchKernelGGL(batch_kernel, dim3(g.nqg * g.G), dim3(64 * NW), 0, (hipStream_t)stream, (const uint4 *)db,
-                       (const uint4 *)qtiles, g.tile0, g.ntiles, r.first, r.first + r.n, g.nqg, g.G, g.xqg,
-                       partials);
+    const int kc = batch_kernel_choice();
+    if (kc == 2)
+        hipLaunchKernelGGL((batch_lds_kernel<8, 1>), dim3(g.nqg * g.G), dim3(64 * 8), 0, (hipStream_t)stream,
+                           (const uint4 *)db, (const uint4 *)qtiles, g.tile0, g.ntiles, r.first, r.first + r.n, g.nqg,
+                           g.G, partials);
+    else
+        hipLaunchKernelGGL(batch_kernel, dim3(g.nqg * g.G), dim3(64 * NW), 0, (hipStream_t)stream, (const uint4 *)db,
+                           (const uint4 *)qtiles, g.tile0, g.ntiles, r.first, r.first + r.n, g.nqg, g.G, g.xqg,
+                           partials);
     if (hipGetLastError() != hipSuccess) return -1;
     hipLaunchKernelGGL(batch_reduce_kernel, dim3(g.nqg * BQ), dim3(256), 0, (hipStream_t)stream, partials, g.G, out);
     return hipGetLastError() == hipSuccess ? 0 : -1;

@@ -59,9 +59,12 @@ def check_all(got, queries, recs, base=0):
             assert (g.num, g.den, g.rotation) == (num, den, rot), (qi, g)
 
 
-def test_batch_1024_queries_vs_oracle(device):
+@pytest.mark.parametrize("kernel", ["2", "1"], ids=["batch_lds_kernel", "batch_kernel"])
+def test_batch_1024_queries_vs_oracle(device, kernel, monkeypatch):
     """Q = 1024 (256 query groups) over 4099 templates and a ragged sub-range: every query's
-    distance bits, index, winning fraction and rotation equal the oracle's."""
+    distance bits, index, winning fraction and rotation equal the oracle's (both batched
+    kernels: IRIS_BATCH_KERNEL)."""
+    monkeypatch.setenv("IRIS_BATCH_KERNEL", kernel)
     n, nq = 4099, 1024
     recs = oc.gen_templates(811, 0, n)
     queries = oc.gen_templates(812, 0, nq)
@@ -84,11 +87,13 @@ def test_batch_1024_queries_vs_oracle(device):
     assert got[600].index == NONE and got[600].distance == np.inf
 
 
+@pytest.mark.parametrize("kernel", ["2", "1"], ids=["batch_lds_kernel", "batch_kernel"])
 @pytest.mark.parametrize("nq", [64, 1024])
-def test_batch_many_groups_200k(device, nq):
+def test_batch_many_groups_200k(device, nq, kernel, monkeypatch):
     """Q = 64 and 1024 over 200 003 templates (6252 tiles: many N-groups per workgroup and a
     ragged last tile): every query against the oracle (Q = 64) or, for Q = 1024, every query
     against the single-query search and 48 of them against the oracle."""
+    monkeypatch.setenv("IRIS_BATCH_KERNEL", kernel)
     n = 200_003
     recs = oc.gen_templates(913, 0, n)
     queries = oc.gen_templates(914, 0, nq)
