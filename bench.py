@@ -249,7 +249,8 @@ def cpu_baseline(args):
         out = np.empty((n, ROT), np.uint16)
         passes, t = _time_passes(lambda: oc_lib.orc_masks_batch(oc._p(q), oc._p(db), n, oc._p(out), threads), secs)
         value, unit = n * passes / t, "records/s"
-        extra["comparisons_per_s"] = ROT * value
+        if wl == "masks":  # the GPU line's unit
+            value, unit = ROT * value, "template comparisons/s"
         sample = f"{passes} passes of MasksEngine::batch_process over {n} masks (src/lib.rs:69-79)"
     elif wl in ("shares", "host-shares"):
         n = 100_000  # 2.56 GB of shares (the 10M-share DB does not fit host RAM): extrapolated per record
