@@ -53,6 +53,7 @@ VALU_INT_PEAK_OPS = 256 * 4 * 16 * 2.4e9
 FP4_DENSE_PEAK_MACS = 10e15 / 2            # MI355X_MICROARCH.md: ~10 PF dense fp4
 MFMA_MACS_PER_TEMPLATE = 2 * 12800 * 32    # den + enc products, 32 rotation rows
 BYTES_PER_TEMPLATE = 3200    # pattern + mask planes, read once per query
+TRITS_BYTES_PER_TEMPLATE = 2560  # --layout trits: 12800 three-state positions, five per byte
 VALU_OPS_PER_TEMPLATE = 400 * 31 * 4   # words x rotations x (and, bitop3, 2x bcnt)
 ROT = 31
 SEED = 20251015
@@ -74,11 +75,11 @@ def parse():
                     help="search: wait for each step's result before enqueueing the next query "
                          "(default: the next query's search is enqueued before this one's result is "
                          "waited for and exchanged)")
-    ap.add_argument("--prewarm-s", type=float, default=1.0,
+    ap.add_argument("--prewarm-s", type=float, default=3.0,
                     help="seconds of untimed steps before the warmup steps (the GPU reaches its steady "
                          "streaming rate after ~0.5-1 s of load)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--layout", choices=["tiles", "lanes"], default="tiles",
+    ap.add_argument("--layout", choices=["tiles", "lanes", "trits"], default="tiles",
                     help="tiles = MFMA kernels (default), lanes = VALU kernels")
     ap.add_argument("--queries", type=int, default=1024, help="queries per batch (workload batch)")
     ap.add_argument("--workload", choices=list(GPU_WORKLOADS + AUX_WORKLOADS), default="search",
@@ -330,7 +331,7 @@ def load_traffic(workload, n_per_launch, layout):
     (profiles/*_pmc_<workload>[_lanes].json, FETCH_SIZE/WRITE_SIZE in separate passes,
     corrected per MI355X_MICROARCH.md §HBM by tools/pmc_summarize.py), scaled to this
     launch size; (None, None) if absent."""
-    suffix = "" if layout == "tiles" else "_lanes"
+    suffix = "" if layout == "tiles" else "_" + layout
     for p in sorted((ROOT / "profiles").glob(f"*_pmc_{workload}{suffix}.json"), reverse=True):
         try:
             j = json.loads(p.read_text())
@@ -689,7 +690,9 @@ def main():
         if world > 1:
             raise SystemExit(f"workload {args.workload} is a single-GPU line (run without --gpus / torchrun)")
         return run_aux(args, dev)
-    layout = ih.LAYOUT_TILES if args.layout == "tiles" else ih.LAYOUT_LANES
+    if args.layout == "trits" and args.workload != "search":
+        raise SystemExit("--layout trits is the search-only template layout (--workload search)")
+    layout = {"tiles": ih.LAYOUT_TILES, "lanes": ih.LAYOUT_LANES, "trits": ih.LAYOUT_TRITS}[args.layout]
     kind = {"search": ih.KIND_TEMPLATES, "batch": ih.KIND_TEMPLATES, "masks": ih.KIND_MASKS,
             "shares": ih.KIND_SHARES}[args.workload]
     db = ih.Database(dev, kind, n, layout)
@@ -818,8 +821,8 @@ def main():
         elapsed = float(t.item())
 
     kname = {"search": "template_search", "batch": "template_batch", "masks": "masks", "shares": "shares"}[args.workload]
-    rec_bytes = {"search": BYTES_PER_TEMPLATE, "batch": BYTES_PER_TEMPLATE, "masks": 1600,
-                 "shares": 25600}[args.workload]
+    rec_bytes = {"search": BYTES_PER_TEMPLATE if args.layout != "trits" else TRITS_BYTES_PER_TEMPLATE,
+                 "batch": BYTES_PER_TEMPLATE, "masks": 1600, "shares": 25600}[args.workload]
     if args.workload in ("search", "batch"):
         results = [m] if args.workload == "search" else m
         found = [{"query": q, "planted_index": site, "found_index": int(results[q].index),
@@ -880,7 +883,7 @@ def main():
             "dtype": {("shares", "tiles"): "i8 MFMA -> i32 (u16 shares as biased byte planes)",
                       ("shares", "lanes"): "u16 (v_pk_mad_u16)"}.get(
                           (args.workload, args.layout),
-                          "fp4 e2m1 MFMA -> f32 (0/+-1 products)" if args.layout == "tiles" else "u32 (VALU popcount)"),
+                          "fp4 e2m1 MFMA -> f32 (0/+-1 products)" if args.layout != "lanes" else "u32 (VALU popcount)"),
             "data": "synthetic (on-device counter-based generator, uniform random pattern+mask bits; planted known answer)",
             "config": {
                 "workload": {
@@ -915,7 +918,8 @@ def main():
                          ("masks", "lanes"): "masks_kernel (VALU popcount)",
                          ("shares", "tiles"): "shares_mfma_kernel (i8 MFMA)",
                          ("shares", "lanes"): "shares_kernel (VALU v_pk_mad_u16)",
-                         ("batch", "tiles"): "batch_kernel (fp4 MFMA, LDS-tiled GEMM)"}[(args.workload, args.layout)],
+                         ("search", "trits"): "trits_mfma_kernel<TR_SEARCH> (fp4 MFMA, 3-state bytes decoded via LDS table)",
+                         ("batch", "tiles"): "batch_lds_kernel (fp4 MFMA GEMM, LDS query-fragment ring)"}[(args.workload, args.layout)],
                 "avg_ms": avg_ms, "launches": launches,
                 "reduce_avg_ms": rms / max(1, launches),
                 "frac_of_guide_copy_bw": achieved / HBM_GUIDE_COPY_GBS,
@@ -923,7 +927,7 @@ def main():
                 "valu_int_frac": (VALU_OPS_PER_TEMPLATE * n / (avg_ms * 1e-3) / VALU_INT_PEAK_OPS
                                   if args.layout == "lanes" and args.workload == "search" else None),
                 "mfma_fp4_frac": (MFMA_MACS_PER_TEMPLATE * n * nq / (step_kernel_ms * 1e-3) / FP4_DENSE_PEAK_MACS
-                                  if args.layout == "tiles" and args.workload in ("search", "batch") else None),
+                                  if args.layout != "lanes" and args.workload in ("search", "batch") else None),
                 "traffic_note": ("FETCH_SIZE counts every L2 miss, Infinity-Cache hits included: the query tiles "
                                  "are re-streamed from the 256-MB MALL for each N-group, "
                                  "the template DB comes from HBM about once per XCD" if args.workload == "batch"

@@ -62,6 +62,13 @@ extern "C" {
 #define IRIS_LAYOUT_DEFAULT 0 /* TILES                                          */
 #define IRIS_LAYOUT_LANES 1   /* record-per-lane blocks of 64 (VALU kernels)   */
 #define IRIS_LAYOUT_TILES 2   /* 32-record MFMA tiles (fp4 / i8 kernels)        */
+/* Search-only template layout: each bit position as one of the three states
+ * encode() distinguishes (masked out, +1, -1), five per byte: 2560 B per
+ * template instead of 3200.  Search, counts and distances are identical to
+ * TILES; the pattern bits under a zero mask are not stored, so iris_db_read
+ * returns pattern & mask (which is all src/template.rs:49-64 and encode()
+ * read).  IRIS_KIND_TEMPLATES only; batched engines of up to 3 queries. */
+#define IRIS_LAYOUT_TRITS 3
 
 typedef struct iris_template {
     uint64_t pattern[IRIS_LIMBS];
@@ -148,8 +155,10 @@ int iris_db_truncate(iris_db_t *db, uint64_t len);
  *   IRIS_KIND_SHARES     *.share-i  EncodedBits 25600 B
  *   IRIS_KIND_TEMPLATES  raw Template (pattern then mask) 3200 B
  * iris_db_load_file appends records [first, first+count) of the file
- * (count = UINT64_MAX: to the end), streamed through pinned buffers with the
- * file reads overlapping the H2D copies and the layout transpose; *loaded
+ * (count = UINT64_MAX: to the end): the mapped file's page-cache pages are
+ * registered with the device and copied by DMA in ~64-MB chunks, overlapping
+ * the layout transpose (if registration fails, the range is read through two
+ * pinned buffers by reader threads instead; IRIS_LOAD_PREAD=1 forces it); *loaded
  * (may be NULL) receives the number appended.  A file whose size is not a
  * multiple of the record size is rejected (IRIS_E_ARG), as the reference's
  * try_cast_slice does ("Share file … invalid.", src/main.rs:390-393,459-462). */
@@ -239,7 +248,8 @@ int iris_pending_wait(iris_pending_t *pending, iris_match_t *out);
 
 /* Batched queries (BASELINE configs[2]): nq query Templates searched against
  * one TILES template database in one pass; out[q] is query q's best match
- * (same rules as iris_template_search).  DB layout must be TILES. */
+ * (same rules as iris_template_search).  DB layout must be TILES, except for
+ * nq <= 3, which runs as streaming passes over any layout. */
 int iris_template_batch_engine_new(iris_device_t *dev, const iris_template_t *queries, uint32_t nq,
                                    iris_engine_t **out);
 int iris_template_batch_search(iris_engine_t *engine, const iris_db_t *db, uint64_t first, uint64_t n,

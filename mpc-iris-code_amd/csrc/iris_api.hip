@@ -388,7 +388,8 @@ int iris_db_create_ex(iris_device_t *d, int kind, uint64_t capacity, int layout,
     ARG(d && out, "NULL argument");
     CHK(check_kind(kind));
     if (layout == IRIS_LAYOUT_DEFAULT) layout = IRIS_LAYOUT_TILES;
-    ARG(layout == IRIS_LAYOUT_LANES || layout == IRIS_LAYOUT_TILES, "unknown layout");
+    ARG(layout == IRIS_LAYOUT_LANES || layout == IRIS_LAYOUT_TILES || layout == IRIS_LAYOUT_TRITS, "unknown layout");
+    ARG(layout != IRIS_LAYOUT_TRITS || kind == IRIS_KIND_TEMPLATES, "the TRITS layout holds templates only");
     std::lock_guard<std::recursive_mutex> g(d->mu);
     CHK(set_device(d));
     iris_db *db = new (std::nothrow) iris_db();
@@ -550,8 +551,19 @@ int iris_distance_engine_new(iris_device_t *d, const uint16_t query[IRIS_BITS], 
 
 namespace {
 int template_engine_locked(iris_device *d, const iris_template_t *query, iris_engine **out) {
-    return engine_from_host_query(d, IRIS_KIND_TEMPLATES, query, (size_t)kPlaneDwords * kTemplateTabStride * 4,
-                                  kTemplateFragDwords * 4, out, launch_query_template);
+    // [LANES table | TILES fragments | TRITS fragments], all built by one launch
+    iris_engine *e = nullptr;
+    void *tfrag = nullptr;
+    CHK(engine_alloc(d, IRIS_KIND_TEMPLATES, (size_t)kPlaneDwords * kTemplateTabStride * 4, kTemplateFragDwords * 4,
+                     kTemplateFragDwords * 4, &e, &tfrag));
+    e->qfrag_trits = tfrag;
+    if (launch_query_template(d->stream, query, (uint32_t *)e->qtab, (uint32_t *)e->qfrag, (uint32_t *)tfrag) != 0) {
+        const hipError_t err = hipGetLastError();
+        engine_free(e);
+        return fail(IRIS_E_HIP, std::string("build query tables: ") + hipGetErrorString(err));
+    }
+    *out = e;
+    return 0;
 }
 }  // namespace
 
@@ -668,6 +680,7 @@ int iris_template_counts(iris_engine_t *e, const iris_db_t *db, uint64_t first, 
         uint16_t *na = num_out ? (uint16_t *)d->out_a.p : nullptr;
         uint16_t *da = den_out ? (uint16_t *)d->out_b.p : nullptr;
         CHK(timed(d, "template_counts", m, [&] {
+            if (db->k.layout == IRIS_LAYOUT_TRITS) return launch_trits_counts(d->stream, db->data, e->qfrag_trits, r, na, da);
             return db->k.layout == IRIS_LAYOUT_TILES
                        ? launch_template_mfma_counts(d->stream, db->data, e->qfrag, r, na, da)
                        : launch_template_counts(d->stream, db->data, e->qtab, r, na, da);
@@ -690,8 +703,10 @@ static int search_enqueue(iris_engine_t *e, const iris_db_t *db, uint64_t first,
     iris_device *d = e->dev;
     if (n == 0) return 0;
     LaunchRange r{first, n};
-    const bool tiles = db->k.layout == IRIS_LAYOUT_TILES;
-    const uint32_t np = tiles ? mfma_search_partials(r) : search_partials(r);
+    const int layout = db->k.layout;
+    const uint32_t np = layout == IRIS_LAYOUT_TILES   ? mfma_search_partials(r)
+                        : layout == IRIS_LAYOUT_TRITS ? trits_search_partials(r)
+                                                      : search_partials(r);
     const size_t pbytes = (size_t)std::max<uint32_t>(np, 1) * sizeof(Partial);
     DevBuf *buf = &d->partials;
     int b = 0;
@@ -709,8 +724,11 @@ static int search_enqueue(iris_engine_t *e, const iris_db_t *db, uint64_t first,
     Partial *part = (Partial *)buf->p;
     uint32_t written = 0;
     CHK(timed(d, "template_search", n, [&] {
-        return tiles ? launch_template_mfma_search(d->stream, db->data, e->qfrag, r, dist_dev, part, &written)
-                     : launch_template_search(d->stream, db->data, e->qtab, r, dist_dev, part, &written);
+        if (layout == IRIS_LAYOUT_TILES)
+            return launch_template_mfma_search(d->stream, db->data, e->qfrag, r, dist_dev, part, &written);
+        if (layout == IRIS_LAYOUT_TRITS)
+            return launch_trits_search(d->stream, db->data, e->qfrag_trits, r, dist_dev, part, &written);
+        return launch_template_search(d->stream, db->data, e->qtab, r, dist_dev, part, &written);
     }));
     if (!side)  // the reduce writes the winner straight into pinned host memory: no copy before the wait
         return timed(d, "reduce", written, [&] { return launch_reduce(d->stream, part, written, dst); });
@@ -943,8 +961,10 @@ int iris_template_batch_search(iris_engine_t *e, const iris_db_t *db, uint64_t f
                                iris_match_t *out) {
     ARG(e && db && out, "NULL argument");
     ARG(e->kind == IRIS_KIND_TEMPLATES && e->nq > 0, "not a batched template engine");
-    ARG(db->k.kind == IRIS_KIND_TEMPLATES && db->k.layout == IRIS_LAYOUT_TILES,
-        "batched search needs a template database in the TILES layout");
+    ARG(db->k.kind == IRIS_KIND_TEMPLATES, "database does not hold templates");
+    // batches of up to kBatchStreamMax queries stream (any layout); the GEMM reads TILES
+    ARG(db->k.layout == IRIS_LAYOUT_TILES || !e->sub.empty(),
+        "batched search of more than 3 queries needs a template database in the TILES layout");
     ARG(e->dev == db->dev, "engine and database live on different devices");
     iris_device *d = e->dev;
     std::lock_guard<std::recursive_mutex> g(d->mu);

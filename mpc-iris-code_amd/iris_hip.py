@@ -32,7 +32,7 @@ LIB_PATH = pathlib.Path(os.environ.get("IRIS_HIP_LIB", HERE / "libiris_hip.so"))
 
 COLS, ROWS, BITS, LIMBS, ROTATIONS = 200, 64, 12800, 200, 31
 KIND_MASKS, KIND_SHARES, KIND_TEMPLATES = 1, 2, 3
-LAYOUT_DEFAULT, LAYOUT_LANES, LAYOUT_TILES = 0, 1, 2
+LAYOUT_DEFAULT, LAYOUT_LANES, LAYOUT_TILES, LAYOUT_TRITS = 0, 1, 2, 3
 _REC_DTYPE = {KIND_MASKS: (np.uint64, LIMBS), KIND_SHARES: (np.uint16, BITS), KIND_TEMPLATES: (np.uint64, 2 * LIMBS)}
 
 
@@ -905,6 +905,6 @@ __all__ = [
     "Bits", "EncodedBits", "Template", "encode", "decode_distance", "resolver_search", "resolver_search_device", "distances", "denominators", "MasksEngine",
     "DistanceEngine", "TemplateEngine", "TemplateBatchEngine", "Device", "Database", "Match", "merge_matches", "dot_bool", "dot_u16",
     "dot_bool_batch", "dot_u16_batch", "IrisError", "load_library", "KIND_MASKS", "KIND_SHARES", "KIND_TEMPLATES",
-    "LAYOUT_DEFAULT", "LAYOUT_LANES", "LAYOUT_TILES",
+    "LAYOUT_DEFAULT", "LAYOUT_LANES", "LAYOUT_TILES", "LAYOUT_TRITS",
     "ROTATIONS", "BITS", "LIMBS", "COLS", "ROWS",
 ]

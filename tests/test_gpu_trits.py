@@ -1,0 +1,232 @@
+"""GPU parity of the TRITS search layout (IRIS_LAYOUT_TRITS, csrc/iris_trits.hip):
+2560 B per template, each position stored as one of the three states encode() tells
+apart (src/lib.rs:16-26).  Counts, distances and the argmin must equal the oracle's
+restatement of Template::distance (src/template.rs:43-64) bit for bit, and equal the
+lossless TILES layout; read-back returns pattern & mask (all the path reads)."""
+import numpy as np
+import pytest
+
+import iris_hip as ih
+from oracle import oracle_c as oc
+
+pytestmark = pytest.mark.gpu
+ROT = 31
+SEED = 42
+TRITS = ih.LAYOUT_TRITS
+
+
+def bits_eq(a, b):
+    return (np.asarray(a, np.float64).view(np.uint64) == np.asarray(b, np.float64).view(np.uint64)).all()
+
+
+def canon(recs):
+    """What a TRITS database keeps of reference Template records: pattern & mask, mask."""
+    out = np.array(recs, np.uint64, copy=True)
+    out[..., :200] &= out[..., 200:]
+    return out
+
+
+@pytest.fixture(params=["wave1", "wave-default"])
+def tiles_per_wave(request, monkeypatch):
+    """Both kernel variants (1 tile per wave for small ranges, the default otherwise);
+    the launcher reads IRIS_TILES_PER_WAVE at every launch."""
+    monkeypatch.setenv("IRIS_TILES_PER_WAVE", "1" if request.param == "wave1" else "4")
+    return request.param
+
+
+def test_trits_generate_and_roundtrip(device):
+    with ih.Database(device, ih.KIND_TEMPLATES, 1000, TRITS) as db:
+        assert db.layout == TRITS
+        db.generate(1000, SEED)
+        assert (db.read(0, 1000) == canon(oc.gen_templates(SEED, 0, 1000))).all()
+        db.clear()
+        db.generate(77, SEED, global_index0=500)
+        assert (db.read(0, 77) == canon(oc.gen_templates(SEED, 500, 77))).all()
+    rng = np.random.default_rng(1)
+    recs = rng.integers(0, 2**64, (150, 400), dtype=np.uint64)
+    with ih.Database(device, ih.KIND_TEMPLATES, 300, TRITS) as db:
+        db.append(recs[:77])
+        db.append(recs[77:])
+        assert (db.read(0, 150) == canon(recs)).all()
+        db.write(10, recs[:5])
+        expect = recs.copy()
+        expect[10:15] = recs[:5]
+        assert (db.read(0, 150) == canon(expect)).all()
+        assert (db.read(63, 3) == canon(expect[63:66])).all()
+
+
+def test_trits_counts_distances_search(device, tiles_per_wave):
+    n = 1000
+    ref = oc.gen_templates(SEED, 0, n)
+    with ih.Database(device, ih.KIND_TEMPLATES, n, TRITS) as db:
+        db.generate(n, SEED)
+        for qi, q in enumerate((ref[3].copy(), oc.gen_templates(SEED + 1, 0, 1)[0])):
+            if qi == 0:
+                q[:200] ^= np.uint64(0x0F0F)  # near a DB member, not equal
+            with ih.TemplateEngine(device, q) as eng:
+                num, den = eng.counts(db)
+                onum, oden = oc.template_counts(q, ref)
+                assert (num == onum).all() and (den == oden).all()
+                num2, den2 = eng.counts(db, first=37, n=500)  # ragged, unaligned to the tiles
+                assert (num2 == onum[37:537]).all() and (den2 == oden[37:537]).all()
+                d = eng.distances(db)
+                od = oc.template_distances(q, ref)
+                assert bits_eq(d, od)
+                m = eng.search(db)
+                best, idx = oc.argmin(od)
+                assert m.index == idx and bits_eq(m.distance, best)
+                assert (m.num, m.den) == (int(onum[idx, m.rotation + 15]), int(oden[idx, m.rotation + 15]))
+                m2 = eng.search(db, first=100, n=333, index_base=10_000)
+                b2, i2 = oc.argmin(od[100:433])
+                assert m2.index == 10_000 + 100 + i2 and bits_eq(m2.distance, b2)
+                one = eng.search(db, first=999, n=1)
+                assert one.index == 999 and bits_eq(one.distance, od[999])
+
+
+def test_trits_golden_edge_cases(device, golden):
+    """The golden vectors' edge cases: identical template, +-15-rotated copies, empty mask
+    (+inf), full mask, a single valid bit."""
+    q, db_ref = golden["query"], golden["db"]
+    with ih.Database(device, ih.KIND_TEMPLATES, db_ref.shape[0], TRITS) as db:
+        db.append(db_ref)
+        with ih.TemplateEngine(device, q) as eng:
+            num, den = eng.counts(db)
+            assert (num == golden["num"]).all() and (den == golden["den"]).all()
+            d = eng.distances(db)
+            assert (d.view(np.uint64) == golden["dist_bits"]).all()
+            m = eng.search(db)
+            assert m.index == int(golden["argmin_index"])
+            assert np.float64(m.distance).view(np.uint64) == golden["argmin_dist_bits"]
+            e = eng.search(db, first=5, n=0)
+            assert e.index == 2**64 - 1 and e.distance == np.inf
+            empty_pos = int(np.where(np.isinf(d))[0][0])
+            z = eng.search(db, first=empty_pos, n=1)
+            assert z.index == 2**64 - 1 and z.distance == np.inf
+
+
+def test_trits_all_invalid_and_all_masked(device):
+    with ih.Database(device, ih.KIND_TEMPLATES, 130, TRITS) as db:
+        db.append(np.zeros((130, 400), np.uint64))
+        with ih.TemplateEngine(device, oc.gen_templates(1, 0, 1)[0]) as eng:
+            m = eng.search(db)
+            assert m.index == 2**64 - 1 and m.distance == np.inf
+            assert np.isinf(eng.distances(db)).all()
+    # every position valid and every pattern bit set: the largest byte value (3^5 - 1 = 242)
+    full = np.full((70, 400), np.uint64(2**64 - 1))
+    q = oc.gen_templates(5, 0, 1)[0]
+    with ih.Database(device, ih.KIND_TEMPLATES, 70, TRITS) as db, ih.TemplateEngine(device, q) as eng:
+        db.append(full)
+        num, den = eng.counts(db)
+        onum, oden = oc.template_counts(q, full)
+        assert (num == onum).all() and (den == oden).all()
+
+
+def test_trits_planted_rotated_copies(device):
+    rng = np.random.default_rng(3)
+    n = 5000
+    with ih.Database(device, ih.KIND_TEMPLATES, n, TRITS) as db:
+        db.generate(n, 9)
+        q = oc.gen_templates(1234, 0, 1)[0]
+        for pos, r in ((4321, 15), (17, -15), (2500, 0)):
+            p = oc.bits_rotated(q[:200], r)
+            mk = oc.bits_rotated(q[200:], r)
+            flips = np.zeros(200, np.uint64)
+            for b in map(int, rng.choice(12800, 25, replace=False)):
+                flips[b // 64] |= np.uint64(1 << (b % 64))
+            db.write(pos, np.concatenate([p ^ flips, mk])[None, :])
+        ref = db.read(0, n)
+        with ih.TemplateEngine(device, q) as eng:
+            m = eng.search(db)
+            best, idx = oc.argmin(oc.template_distances(q, ref))
+            assert m.index == idx and bits_eq(m.distance, best)
+            for pos, r in ((4321, 15), (17, -15), (2500, 0)):
+                num, den = eng.counts(db, first=pos, n=1)
+                assert int(np.argmin(num[0] / den[0])) - 15 == r
+
+
+def test_trits_equals_tiles_200k(device):
+    """200 000 templates (the multi-tile-per-wave kernel, a ragged last tile): TRITS and
+    TILES give identical counts everywhere; 300 sampled rows equal the oracle."""
+    n = 200_003
+    q = oc.gen_templates(SEED + 7, 0, 1)[0]
+    out = {}
+    for lay in (ih.LAYOUT_TILES, TRITS):
+        with ih.Database(device, ih.KIND_TEMPLATES, n, lay) as db, ih.TemplateEngine(device, q) as eng:
+            db.generate(n, 11)
+            out[lay] = (eng.counts(db), eng.distances(db), eng.search(db), eng.search(db, first=12_345, n=150_001))
+    (n0, d0), dist0, m0, s0 = out[ih.LAYOUT_TILES]
+    (n1, d1), dist1, m1, s1 = out[TRITS]
+    assert (n0 == n1).all() and (d0 == d1).all() and bits_eq(dist0, dist1)
+    for a, b in ((m0, m1), (s0, s1)):
+        assert (a.index, a.num, a.den, a.rotation) == (b.index, b.num, b.den, b.rotation)
+    sample = np.random.default_rng(5).choice(n, 300, replace=False)
+    sample[:2] = (0, n - 1)
+    for i in map(int, sample):
+        onum, oden = oc.template_counts(q, oc.gen_templates(11, i, 1))
+        assert (n1[i] == onum[0]).all() and (d1[i] == oden[0]).all()
+
+
+def test_trits_10m_planted_and_sampled(device):
+    """configs[1]'s size in the TRITS layout: planted rotated copies near both ends and a
+    lowest-index tie decide the argmin; 400 sampled distances equal the oracle."""
+    n = 10_000_000
+    q = oc.gen_templates(2024, 0, 1)[0]
+    with ih.Database(device, ih.KIND_TEMPLATES, n, TRITS) as db, ih.TemplateEngine(device, q) as eng:
+        db.generate(n, 77)
+        rec = np.concatenate([oc.bits_rotated(q[:200], 7), oc.bits_rotated(q[200:], 7)])
+        rec[5] ^= np.uint64(0xFF)  # 8 flipped bits: distance small, not zero
+        for pos in (n - 3, 12, 5_000_000):
+            db.write(pos, rec[None, :])
+        m = eng.search(db)
+        assert m.index == 12 and m.rotation == 7  # equal distances: the lowest index wins
+        tail = eng.search(db, first=13, n=n - 13)
+        assert tail.index == 5_000_000 and tail.rotation == 7
+        d = eng.distances(db)
+        assert bits_eq(d[[12, 5_000_000, n - 3]], m.distance)
+        sample = np.random.default_rng(9).choice(n, 400, replace=False)
+        for i in map(int, sample):
+            if i in (12, 5_000_000, n - 3):
+                continue
+            assert bits_eq(d[i], oc.template_distances(q, oc.gen_templates(77, i, 1))[0])
+
+
+def test_trits_layout_limits(device):
+    for kind in (ih.KIND_MASKS, ih.KIND_SHARES):
+        with pytest.raises(ih.IrisError):
+            ih.Database(device, kind, 10, TRITS)
+    qs = oc.gen_templates(3, 0, 8)
+    with ih.Database(device, ih.KIND_TEMPLATES, 300, TRITS) as db:
+        db.generate(300, 4)
+        ref = db.read(0, 300)
+        with ih.TemplateBatchEngine(device, qs) as eng:  # the GEMM path needs TILES
+            with pytest.raises(ih.IrisError):
+                eng.search(db)
+        with ih.TemplateBatchEngine(device, qs[:3]) as eng:  # up to 3 queries stream: works
+            got = eng.search(db)
+            for q, m in zip(qs[:3], got):
+                best, idx = oc.argmin(oc.template_distances(q, ref))
+                assert m.index == idx and bits_eq(m.distance, best)
+
+
+def test_trits_prepare_and_files(device, tmp_path):
+    """encode() and the masks file need only pattern & mask, so share preparation from a
+    TRITS database equals preparation from TILES; a raw template file loads into TRITS."""
+    key = bytes(range(32))
+    t = oc.gen_templates(8, 0, 90)
+    res = {}
+    for lay in (ih.LAYOUT_TILES, TRITS):
+        with ih.Database(device, ih.KIND_TEMPLATES, 90, lay) as tdb:
+            tdb.append(t)
+            sdbs = [ih.Database(device, ih.KIND_SHARES, 90) for _ in range(2)]
+            with ih.Database(device, ih.KIND_MASKS, 90) as mdb:
+                ih.prepare_shares(tdb, sdbs, mdb, key=key, nonce=3)
+                res[lay] = ([s.read(0, 90) for s in sdbs], mdb.read(0, 90))
+            for s in sdbs:
+                s.close()
+    (s0, m0), (s1, m1) = res[ih.LAYOUT_TILES], res[TRITS]
+    assert (m0 == m1).all() and all((a == b).all() for a, b in zip(s0, s1))
+    path = tmp_path / "templates.bin"
+    t.tofile(path)
+    with ih.Database(device, ih.KIND_TEMPLATES, 90, TRITS) as db:
+        db.load_file(str(path))
+        assert len(db) == 90 and (db.read(0, 90) == canon(t)).all()

@@ -10,7 +10,7 @@ import sys
 ROOT = pathlib.Path(__file__).resolve().parents[1]
 PMC = ROOT / "gpurun_out" / "pmc"
 KERNELS = {"search": ("template_mfma_kernel<1", 10_000_000, 3200),  # <1, 4> (and <1, 1> on small ranges)
-           "batch": ("batch_kernel", 10_000_000, 3200),  # 1024 queries: the DB once + query tiles
+           "batch": ("batch_lds_kernel", 10_000_000, 3200),  # 1024 queries: the DB once + query tiles
            "masks": ("masks_mfma_kernel", 10_000_000, 1600 + 62),
            "shares": ("shares_mfma_kernel", 10_000_000, 25600 + 62),
            "resolver": ("resolver_kernel", 10_000_000, 4 * 62),
@@ -39,13 +39,15 @@ def per_launch(dirname, name, kernel):
     return sum(by.values()) / len(by)
 
 
-def main(round_tag="r01"):
+def main(round_tag="r02"):
     for w, (kernel, n, alg) in KERNELS.items():
-        for suffix, lay in (("", "tiles"), ("_lanes", "lanes")):
+        for suffix, lay in (("", "tiles"), ("_lanes", "lanes"), ("_trits", "trits")):
             fdir, wdir = f"{w}_FETCH_SIZE{suffix}", f"{w}_WRITE_SIZE{suffix}"
             if not (PMC / fdir).exists():
                 continue
-            k = kernel if lay == "tiles" else "template_kernel<1>"
+            k = {"tiles": kernel, "lanes": "template_kernel<1>", "trits": "trits_mfma_kernel<1"}[lay]
+            if lay == "trits":
+                alg = 2560
             fetch = per_launch(fdir, "FETCH_SIZE", k)
             write = per_launch(wdir, "WRITE_SIZE", k)
             if fetch is None or write is None:
