@@ -56,7 +56,8 @@ def main(round_tag="r02"):
             rd, wr = fetch * 1024 * 2, write * 1024
             j = {"round": int(round_tag[1:]), "workload": w, "layout": lay, "kernel": k,
                  "command": f"rocprofv3 --pmc FETCH_SIZE|WRITE_SIZE (separate passes) -- python3 bench.py --workload {w} "
-                            + ("--queries 1024 --steps 1 --warmup 0" if w == "batch" else "--steps 3 --warmup 1"),
+                            + ("--queries 1024 --steps 1 --warmup 0" if w == "batch" else "--steps 3 --warmup 1")
+                            + ("" if lay == "tiles" else f" --layout {lay}"),
                  "n_records_per_launch": n, "FETCH_SIZE_kB_raw": fetch, "WRITE_SIZE_kB_raw": write,
                  "correction": "read bytes = FETCH_SIZE*1024*2, write bytes = WRITE_SIZE*1024 (MI355X_MICROARCH.md §HBM)",
                  "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
