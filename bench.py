@@ -343,6 +343,20 @@ def load_traffic(workload, n_per_launch, layout):
     return None, None
 
 
+def batch_pmc():
+    """SQ-counter figures of the 1024-query batched launch from the committed profile
+    (tools/pmc_batch.sh, profiles/r02_pmc_batch_sq.json): VALU and LDS instructions per MFMA
+    and the bytes fetched beyond L2, reported beside the MFMA roofline fraction."""
+    p = ROOT / "profiles" / "r02_pmc_batch_sq.json"
+    try:
+        j = json.loads(p.read_text())
+    except Exception:
+        return None
+    return {"valu_per_mfma": j["valu_per_mfma_incl_mfma"], "valu_per_mfma_excl_mfma": j["valu_per_mfma_excl_mfma"],
+            "lds_insts_per_mfma": j["lds_insts_per_mfma"], "beyond_l2_bytes_per_launch": j["beyond_l2_bytes_per_launch"],
+            "source": "profiles/" + p.name + " (committed rocprofv3 --pmc run of this command)"}
+
+
 # ---------------------------------------------------------------------------- launching
 
 
@@ -932,6 +946,7 @@ def main():
                                  "are re-streamed from the 256-MB MALL for each N-group, "
                                  "the template DB comes from HBM about once per XCD" if args.workload == "batch"
                                  else None),
+                "pmc": batch_pmc() if args.workload == "batch" and nq == 1024 else None,
             },
             "cpu_baseline": cpu,
             "check": check,
