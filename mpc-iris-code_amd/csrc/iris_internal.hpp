@@ -75,9 +75,11 @@ inline KindInfo kind_info(int kind, int layout = IRIS_LAYOUT_LANES) {
 //    (0: mask 0, 1: mask 1 pattern 0, 2: mask 1 pattern 1), five per byte,
 //    digit i of byte v weighing 3^i.  For 5-chunk group G (positions
 //    [320G, 320G+320)) lane L = t + 32h owns the 160 positions
-//    [320G + 160h, +160) = plane dwords 10G + 5h .. +4; its byte j holds the
-//    positions 320G + 160h + 5j .. +4.  Half-stage s = 0, 1 of the group is
-//    bytes 16s .. 16s+15: uint4 [(2G + s) * 64 + L] of the tile.
+//    [320G + 160h, +160) = plane dwords 10G + 5h .. +4 (window position x =
+//    bit x & 31 of plane dword 10G + 5h + (x >> 5)).  Half-stage s = 0, 1 of the
+//    group is bytes 16s .. 16s+15: uint4 [(2G + s) * 64 + L] of the tile; digit k
+//    of its byte jj is window position trit_pos(s, jj, k) (the decode's byte roles,
+//    iris_trits.hip).
 constexpr int kTritGroups = 40;                      // 5-chunk groups per template
 constexpr int kTritTileUint4 = kTritGroups * 2 * 64; // 5120 uint4 = 81920 B per tile
 constexpr size_t kTritRecBytes = 2560;
@@ -86,11 +88,36 @@ inline size_t block_bytes(const KindInfo &k) {
     return (size_t)k.block * (k.layout == IRIS_LAYOUT_TRITS ? kTritRecBytes : k.rec_bytes);
 }
 
-// 5 mask / pattern bits (bit i = position i) -> the TRITS byte
+// 5 mask / pattern bits (bit i = digit i) -> the TRITS byte
 IRIS_HD inline uint32_t trit_byte(uint32_t m5, uint32_t p5) {
     uint32_t v = 0;
     for (int i = 4; i >= 0; --i) v = 3 * v + (((m5 >> i) & 1u) ? 1u + ((p5 >> i) & 1u) : 0u);
     return v;
+}
+// Window position (0..159) of digit k of byte jj of half-stage s.  Every 8 bytes
+// cover 40 positions, five decoded dwords of 8: bytes 0..3 (W_j) positions
+// 8j .. 8j+4, bytes 4..7 (S_j) positions 8j+5 .. 8j+7 (digits 0..2) and 32+2j,
+// 33+2j (digits 3, 4).
+IRIS_HD inline int trit_pos(int s, int jj, int k) {
+    const int base = 80 * s + 40 * (jj >> 3), b = jj & 7;
+    if (b < 4) return base + 8 * b + k;
+    const int j = b - 4;
+    return k < 3 ? base + 8 * j + 5 + k : base + 32 + 2 * j + (k - 3);
+}
+// its inverse: window position x -> (half-stage, byte, digit)
+IRIS_HD inline void trit_slot(int x, int &s, int &jj, int &k) {
+    s = x / 80;
+    const int r = x % 80, q = r / 40, n = r % 40;
+    int slot;
+    if (n < 32) {
+        const int j = n >> 3, o = n & 7;
+        slot = o < 5 ? j : 4 + j;
+        k = o < 5 ? o : o - 5;
+    } else {
+        slot = 4 + ((n - 32) >> 1);
+        k = 3 + ((n - 32) & 1);
+    }
+    jj = 8 * q + slot;
 }
 // TRITS byte -> the fp4 e2m1 encode() values of its 5 positions, nibble i =
 // 0 (masked out), 0x2 (+1.0: pattern 0) or 0xA (-1.0: pattern 1).  Bytes

@@ -11,20 +11,28 @@
 // 12800 positions in 2560 B, 20 % fewer HBM bytes than TILES.
 //
 // Decode: a 243-entry table maps a byte to the fp4 e2m1 encode() values of its
-// five positions (20 bits, nibble i = position i).  The table lives in LDS in
-// 32 copies, entry e of copy c at dword e * 64 + c, and lane l reads copy
-// l & 31: ds_read_b32 banks are (address / 4) mod 32 per 32-lane half, so the
-// 32 lanes of a half always hit 32 distinct banks (no conflict whatever the
-// data).  The address is one v_perm_b32: byte 1 = the data byte, byte 0 =
-// 4 * (lane & 31).  Eight bytes decode into five dwords of 8 nibbles with 11
-// shift/or ops; the den operand is the same nibbles & 0x22222222 (|enc| = 1.0).
+// five positions (T_w: nibble i = digit i; T_s = T_w << 4, nibbles 1..5).  The
+// tables live in LDS in 32 copies each, one 256-B bank row per entry: T_w at
+// dwords 0..31 and T_s at dwords 32..63 of row e, lane l reading copy l & 31.
+// ds_read_b32 banks are (address / 4) mod 32 per 32-lane half, so the 32 lanes of
+// a half always hit 32 distinct banks (no conflict whatever the data), and both
+// tables share the address: one v_perm_b32 (byte 1 = the data byte, byte 0 =
+// 4 * (lane & 31)), T_s through the instruction's offset field.
+//
+// Byte roles: every 8 bytes (40 positions) decode to five stream dwords.  Bytes
+// 0..3 (W_j, read from T_w) fill nibbles 0..4 of dword j; bytes 4..7 (S_j, read
+// from T_s) put digits 0..2 in nibbles 5..7 of dword j and digits 3, 4 in
+// nibbles 2j, 2j+1 of dword 4:  dword j = (s_j << 16) | w_j (one v_lshl_or_b32:
+// the shift drops digits 3, 4) and dword 4 = byte 2 of s_0..s_3 (two v_perm_b32
+// and an or) -- 7 VALU per 8 bytes.  The den operand is the same nibbles
+// & 0x22222222 (|enc| = 1.0).
 //
 // K order: the MFMA sums over K, so any bijection between a lane's fp4 slots
 // and template positions works as long as the query fragments use the same
 // one.  Lane L = t + 32h of a tile owns positions [320G + 160h, +160) of its
 // template in 5-chunk group G, as one 160-nibble stream; chunk c of the group
 // is nibbles [32c, 32c + 32) = plane dword 10G + 5h + c of both operands
-// (iris_internal.hpp: kTritTileUint4, TRITS fragments).
+// (iris_internal.hpp: kTritTileUint4, trit_pos, TRITS fragments).
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
 
@@ -41,12 +49,20 @@ typedef float v16f __attribute__((ext_vector_type(16)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kTileRecs = 32;
-constexpr int kLutStride = 64;  // dwords per table entry (32 copies used: one 256-B bank row)
+constexpr int kLutStride = 64;  // dwords per table entry: T_w copies 0..31, T_s copies 32..63 (one 256-B bank row)
+constexpr int kLutStage = 252 * kLutStride;  // dword offset of the staged 256-entry constant
 constexpr int kHalfStages = 2 * kTritGroups;  // 80 uint4 per lane and template
 #ifndef IRIS_TRITS_TILES
 #define IRIS_TRITS_TILES 2
 #endif
 constexpr int kTritTiles = IRIS_TRITS_TILES;  // tiles per wave
+// VALU per step (T = 2: 80 decode + 8 / 12 query-operand ands), spread over the step's MFMAs
+#ifndef IRIS_TRITS_NV_ODD
+#define IRIS_TRITS_NV_ODD 88
+#endif
+#ifndef IRIS_TRITS_NV_EVEN
+#define IRIS_TRITS_NV_EVEN 92
+#endif
 
 // the decode table, computed at compile time (filling LDS from it costs one load + one
 // store per entry instead of ~35 VALU of base-3 arithmetic)
@@ -86,21 +102,14 @@ __device__ __forceinline__ void tchunk(uint32_t b0, uint32_t b1, uint32_t b2, ui
     s = mfma_fp4(ae, be, s);
 }
 
-// (a << s) | b and a >> s as single instructions (see combine in the kernel)
+// (a << s) | b as one instruction (hipcc would otherwise emit a shift and a v_or / v_bitop3)
 template <int S>
 __device__ __forceinline__ uint32_t lshl_or_i(uint32_t a, uint32_t b) {
     uint32_t r;
     asm("v_lshl_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "I"(S), "v"(b));
     return r;
 }
-template <int S>
-__device__ __forceinline__ uint32_t lshr_i(uint32_t a) {
-    uint32_t r;
-    asm("v_lshrrev_b32 %0, %1, %2" : "=v"(r) : "I"(S), "v"(a));
-    return r;
-}
 #define lshl_or(a, s, b) lshl_or_i<s>((a), (b))
-#define lshr(a, s) lshr_i<s>((a))
 
 struct QF {
     v8i am, ae;
@@ -128,8 +137,13 @@ __global__ void __launch_bounds__(256, 2)
     trits_mfma_kernel(const uint4 *__restrict__ db, const uint4 *__restrict__ qfrag, uint64_t tile0, uint64_t ntiles,
                       uint64_t first, uint64_t end, uint16_t *__restrict__ num_out, uint16_t *__restrict__ den_out,
                       double *__restrict__ dist_out, Partial *__restrict__ partials) {
+    // the table: the 1-KB constant staged through rows 252..255 (never read: bytes are < 243),
+    // one global load per thread, then rows 0..242 written from LDS (a wave reads one row:
+    // broadcast; writes consecutive dwords: conflict-free)
     __shared__ uint32_t lut[256 * kLutStride];
-    for (int i = threadIdx.x; i < 256 * 32; i += 256) lut[(i >> 5) * kLutStride + (i & 31)] = kTritLut.v[i >> 5];
+    lut[kLutStage + threadIdx.x] = kTritLut.v[threadIdx.x];
+    __syncthreads();
+    for (int i = threadIdx.x; i < 243 * kLutStride; i += 256) lut[i] = lut[kLutStage + (i >> 6)] << ((i & 32) >> 3);
     __syncthreads();
 
     const int lane = threadIdx.x & 63;
@@ -151,26 +165,24 @@ __global__ void __launch_bounds__(256, 2)
     if (active) {
         const uint32_t laneoff = (uint32_t)(lane & 31) * 4u;
         const char *lutb = (const char *)lut;
-        // table entries of the 16 bytes of v for this lane's copy (16 ds_read_b32)
+        // table entries of the 16 bytes of v for this lane's copy (16 ds_read_b32): dwords 0, 2
+        // hold W bytes (T_w), dwords 1, 3 S bytes (T_s, 128 B further in the row)
         auto lookups = [&](const uint4 &v, uint32_t *e) {
             const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
             for (int i = 0; i < 16; ++i)
-                e[i] = *(const uint32_t *)(lutb + __builtin_amdgcn_perm(w[i >> 2], laneoff, 0x0C0C0400u + ((i & 3) << 8)));
+                e[i] = *(const uint32_t *)(lutb + ((i >> 2) & 1) * 128 +
+                                           __builtin_amdgcn_perm(w[i >> 2], laneoff, 0x0C0C0400u + ((i & 3) << 8)));
         };
-        // 16 entries (80 nibbles) -> 10 stream dwords: 8 entries -> 5 dwords, twice, in 11
-        // VALU each (hipcc would otherwise merge the ORs into v_bitop3 after separate
-        // shifts: 4 ops where two v_lshl_or_b32 do it in 3)
+        // 16 entries (80 nibbles) -> 10 stream dwords: 8 entries -> 5 dwords, twice, in 7 VALU each
         auto combine = [&](const uint32_t *e, uint32_t *d) {
 #pragma unroll
             for (int q = 0; q < 2; ++q) {
-                const uint32_t *t = e + 8 * q;
+                const uint32_t *w = e + 8 * q, *t = e + 8 * q + 4;
                 uint32_t *o = d + 5 * q;
-                o[0] = lshl_or(t[1], 20, t[0]);
-                o[1] = lshl_or(t[3], 28, lshl_or(t[2], 8, lshr(t[1], 12)));
-                o[2] = lshl_or(t[4], 16, lshr(t[3], 4));
-                o[3] = lshl_or(t[6], 24, lshl_or(t[5], 4, lshr(t[4], 16)));
-                o[4] = lshl_or(t[7], 12, lshr(t[6], 8));
+#pragma unroll
+                for (int j = 0; j < 4; ++j) o[j] = lshl_or(t[j], 16, w[j]);
+                o[4] = __builtin_amdgcn_perm(t[1], t[0], 0x0C0C0602u) | __builtin_amdgcn_perm(t[3], t[2], 0x06020C0Cu);
             }
         };
 
@@ -261,7 +273,7 @@ __global__ void __launch_bounds__(256, 2)
             decode(st, dv[P]);
             mfmas(std::integral_constant<bool, !P>{});
             constexpr int nm = (P ? 4 : 6) * T;  // MFMAs of the previous (opposite-parity) half-stage
-            constexpr int nv = (P ? 100 : 112) / nm;  // the step's ~100-112 VALU spread evenly
+            constexpr int nv = (P ? IRIS_TRITS_NV_ODD : IRIS_TRITS_NV_EVEN) / nm;  // the step's VALU spread evenly
 #pragma unroll
             for (int k = 0; k < nm; ++k) {
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);   // 1 MFMA
@@ -364,20 +376,20 @@ __global__ void __launch_bounds__(256, 2)
 
 namespace {
 
-// 5 bits at bit offset b of a 5-dword (160-bit) window
-__device__ __forceinline__ uint32_t bits5(const uint32_t *w, int b) {
-    const int i = b >> 5, o = b & 31;
-    const uint64_t x = (uint64_t)w[i] | ((uint64_t)(i + 1 < 5 ? w[i + 1] : 0u) << 32);
-    return (uint32_t)(x >> o) & 31u;
-}
-
-// half-stage s (bytes 16s .. 16s+15) of a lane's 160-position window
+// half-stage s (bytes 16s .. 16s+15) of a lane's 160-position window (m, p: its 5 plane
+// dwords); byte jj holds the positions trit_pos(s, jj, 0..4)
 __device__ __forceinline__ uint4 trit_half(const uint32_t *m, const uint32_t *p, int s) {
     uint32_t v[4] = {0, 0, 0, 0};
 #pragma unroll
     for (int jj = 0; jj < 16; ++jj) {
-        const int b = 5 * (16 * s + jj);
-        v[jj >> 2] |= trit_byte(bits5(m, b), bits5(p, b)) << (8 * (jj & 3));
+        uint32_t m5 = 0, p5 = 0;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            const int x = trit_pos(s, jj, k);
+            m5 |= ((m[x >> 5] >> (x & 31)) & 1u) << k;
+            p5 |= ((p[x >> 5] >> (x & 31)) & 1u) << k;
+        }
+        v[jj >> 2] |= trit_byte(m5, p5) << (8 * (jj & 3));
     }
     return make_uint4(v[0], v[1], v[2], v[3]);
 }
@@ -422,10 +434,11 @@ __global__ void __launch_bounds__(256) unpack_trits_kernel(const uint4 *__restri
         const uint64_t t = t_first + i;
         uint32_t em = 0, ep = 0;
         for (int b = 0; b < 32; ++b) {
-            const int pos = 32 * c + b, j = pos / 5;
-            const uint4 *src = db + trit_index(t, G, h, j >> 4);
-            uint32_t v = ((const uint8_t *)src)[j & 15];
-            for (int k = pos % 5; k > 0; --k) v /= 3;
+            int s, jj, k;
+            trit_slot(32 * c + b, s, jj, k);
+            const uint4 *src = db + trit_index(t, G, h, s);
+            uint32_t v = ((const uint8_t *)src)[jj];
+            for (; k > 0; --k) v /= 3;
             const uint32_t dgt = v % 3;
             em |= (dgt != 0 ? 1u : 0u) << b;
             ep |= (dgt == 2 ? 1u : 0u) << b;
