@@ -45,10 +45,22 @@ __device__ __forceinline__ void store_tile_rows(uint16_t *__restrict__ out, uint
         uint4 *dst = (uint4 *)(out + (tile_t0 - first) * kRot);
         const uint4 *src = (const uint4 *)lds;
         // streamed out with nontemporal stores: the rows are not re-read by this launch
-        for (int i = lane; i < 32 * kRot * 2 / 16; i += 64) {
+#ifndef IRIS_STORE_PLAIN
+#define IRIS_STORE_PLAIN 0  // 1: plain (write-back) stores instead of nontemporal
+#endif
+#ifndef IRIS_STORE_DIAG
+#define IRIS_STORE_DIAG 0
+#endif
+        // diagnostic builds only (results wrong by design): 1 = half the row bytes, 2 = none
+        constexpr int kStores = IRIS_STORE_DIAG == 0 ? 32 * kRot * 2 / 16 : IRIS_STORE_DIAG == 1 ? 32 * kRot / 16 : 0;
+        for (int i = lane; i < kStores; i += 64) {
             const uint4 v = src[i];
+#if IRIS_STORE_PLAIN
+            dst[i] = v;
+#else
             const u32x4_nt w = {v.x, v.y, v.z, v.w};
             __builtin_nontemporal_store(w, (u32x4_nt *)&dst[i]);
+#endif
         }
     } else {
         const uint64_t tg = tile_t0 + (lane & 31);
