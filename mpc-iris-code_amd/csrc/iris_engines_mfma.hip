@@ -82,8 +82,10 @@ __device__ __forceinline__ void mask_chunk(uint32_t x, const v8i &a, v16f &acc) 
     acc = mfma_fp4(a, b, acc);
 }
 
+// share-row loads of the fused resolver: plain by default (nontemporal measured the same,
+// 2.75-2.79 ms per 10M either way); 1 selects nontemporal
 #ifndef IRIS_RESOLVE_NT
-#define IRIS_RESOLVE_NT 1
+#define IRIS_RESOLVE_NT 0
 #endif
 // Fused resolver operands (MASKS_RESOLVE): the participants' [n][31] u16
 // outputs, row i = record first + i (src/main.rs:597-607).

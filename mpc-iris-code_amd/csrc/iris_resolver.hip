@@ -39,8 +39,8 @@ __device__ __forceinline__ u16x8 load_word(const uint16_t *__restrict__ src, uin
                                            bool aligned) {
     const uint64_t e = (uint64_t)i * 8;
     if (aligned && e + 8 <= ne) {
-        // read once: nontemporal loads (the plain-load stream tops out lower, MI355X_MICROARCH.md
-        // / profiles/r01_ubench_read_stream_warm.txt)
+        // read once: nontemporal loads (the plain-load stream tops out lower, measured in
+        // profiles/r01_ubench_read_stream_warm.txt: tools/ubench_stream.hip)
         if (IRIS_RESOLVER_NT) return __builtin_nontemporal_load((const u16x8 *)(src + e0 + e));
         return *(const u16x8 *)(src + e0 + e);
     }
