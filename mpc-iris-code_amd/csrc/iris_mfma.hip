@@ -65,8 +65,24 @@ __device__ __forceinline__ void chunk_step(uint32_t x0, uint32_t x1, const QFrag
                     (int)(x1 & 0x11111111u), 0, 0, 0, 0};
     const v8i be = {(int)(x0 & 0xAAAAAAAAu), (int)((x0 << 1) & 0xAAAAAAAAu), (int)(x1 & 0xAAAAAAAAu),
                     (int)((x1 << 1) & 0xAAAAAAAAu), 0, 0, 0, 0};
-    den = mfma_fp4(q.am, bm, den);
-    s = mfma_fp4(q.ae, be, s);
+#ifndef IRIS_MFMA_DIAG
+#define IRIS_MFMA_DIAG 0
+#endif
+    // diagnostic builds only (tools/, results wrong by design): 1 = no den MFMA, 2 = no
+    // MFMAs (operands kept live by an empty asm), 3 = no operand expansion (raw dwords)
+    if constexpr (IRIS_MFMA_DIAG == 0) {
+        den = mfma_fp4(q.am, bm, den);
+        s = mfma_fp4(q.ae, be, s);
+    } else if constexpr (IRIS_MFMA_DIAG == 1) {
+        asm volatile("" ::"v"(bm));
+        s = mfma_fp4(q.ae, be, s);
+    } else if constexpr (IRIS_MFMA_DIAG == 2) {
+        asm volatile("" ::"v"(bm), "v"(be), "v"(q.am), "v"(q.ae));
+    } else {
+        const v8i raw = {(int)x0, (int)x1, (int)x0, (int)x1, 0, 0, 0, 0};
+        den = mfma_fp4(q.am, raw, den);
+        s = mfma_fp4(q.ae, raw, s);
+    }
 }
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));

@@ -98,8 +98,20 @@ __device__ __forceinline__ void tchunk(uint32_t b0, uint32_t b1, uint32_t b2, ui
     const v8i be = {(int)b0, (int)b1, (int)b2, (int)b3, 0, 0, 0, 0};
     const v8i bm = {(int)(b0 & 0x22222222u), (int)(b1 & 0x22222222u), (int)(b2 & 0x22222222u),
                     (int)(b3 & 0x22222222u), 0, 0, 0, 0};
-    den = mfma_fp4(am, bm, den);
-    s = mfma_fp4(ae, be, s);
+#ifndef IRIS_TRITS_DIAG
+#define IRIS_TRITS_DIAG 0
+#endif
+    // diagnostic builds only (tools/, results wrong by design): 1 = no den MFMA, 2 = no MFMAs
+    // (operands kept live by an empty asm)
+    if constexpr (IRIS_TRITS_DIAG == 0) {
+        den = mfma_fp4(am, bm, den);
+        s = mfma_fp4(ae, be, s);
+    } else if constexpr (IRIS_TRITS_DIAG == 1) {
+        asm volatile("" ::"v"(bm), "v"(am));
+        s = mfma_fp4(ae, be, s);
+    } else {
+        asm volatile("" ::"v"(bm), "v"(be), "v"(am), "v"(ae));
+    }
 }
 
 // (a << s) | b as one instruction (hipcc would otherwise emit a shift and a v_or / v_bitop3)
