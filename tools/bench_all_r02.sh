@@ -21,6 +21,7 @@ run load 300 --workload load --steps 2 --warmup 1 --no-cpu-baseline
 run host-shares 300 --workload host-shares --steps 3 --warmup 1
 run host-masks 300 --workload host-masks --steps 3 --warmup 1
 run search_lanes 300 --steps 10 --warmup 2 --layout lanes --no-cpu-baseline
+run search_trits 300 --steps 20 --warmup 3 --layout trits --no-cpu-baseline
 for w in search masks shares resolve-masks; do
   run chunk20k_$w 200 --workload $w --n-per-gpu 20000 --steps 200 --warmup 10 --no-cpu-baseline
 done
