@@ -157,6 +157,21 @@ impl Database {
         Ok(Database { raw, kind: T::KIND, device: device.clone() })
     }
 
+    /// As `new` with an explicit device layout (`ffi::IRIS_LAYOUT_*`): e.g.
+    /// `IRIS_LAYOUT_TRITS` for a search-only template database of 2560 B per template
+    /// (read-back returns `pattern & mask`).
+    pub fn with_layout<T: Record>(device: &Device, capacity: u64, layout: c_int) -> Result<Self> {
+        let mut raw = ptr::null_mut();
+        check(unsafe { ffi::iris_db_create_ex(device.raw(), T::KIND, capacity, layout, &mut raw) })?;
+        Ok(Database { raw, kind: T::KIND, device: device.clone() })
+    }
+
+    /// The device layout the records are held in (`ffi::IRIS_LAYOUT_*`).
+    pub fn layout(&self) -> Result<c_int> {
+        let mut l: c_int = 0;
+        check(unsafe { ffi::iris_db_layout(self.raw, &mut l) }).map(|_| l)
+    }
+
     pub fn raw(&self) -> *mut ffi::IrisDb {
         self.raw
     }
