@@ -28,7 +28,7 @@ def _lines(out):
     return [json.loads(l) for l in out.splitlines() if l.startswith("{")]
 
 
-@pytest.mark.parametrize("n", [2, 3])
+@pytest.mark.parametrize("n", [2, 3, 8])  # 8: the driver's scaling run, rehearsed on gloo
 def test_self_launch_dry_run(n):
     env = dict(os.environ, IRIS_DIST_BACKEND="gloo")
     r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", str(n), "--dry-run"], cwd=ROOT, env=env,
