@@ -184,6 +184,15 @@ __global__ void __launch_bounds__(256) prepare_shares_tiles_kernel(const uint32_
     }
 }
 
+// The 16 mask bits of an xpacked dword (nibble p: bit 1 = em[2p], bit 0 = em[2p+1]) as a
+// plain 16-bit mask word: swap the pair, then compact two bits per nibble (SWAR).
+__device__ __forceinline__ uint32_t xmask(uint32_t x) {
+    uint32_t m = ((x & 0x11111111u) << 1) | ((x >> 1) & 0x11111111u);  // em[2p] bit 0, em[2p+1] bit 1
+    m = (m | (m >> 2)) & 0x0F0F0F0Fu;
+    m = (m | (m >> 4)) & 0x00FF00FFu;
+    return (m | (m >> 8)) & 0xFFFFu;
+}
+
 // Fully in place: templates read from a TILES template database (one 8-byte
 // xpacked pair per (template, dword b), unpacked with xunpack), shares and the
 // optional masks written straight into TILES databases — one launch, no
@@ -196,7 +205,6 @@ __global__ void __launch_bounds__(256) prepare_direct_kernel(const uint4 *__rest
                                                              uint64_t m_first) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint64_t i = (uint64_t)blockIdx.x * 64 + lane;
-    if (i >= m) return;
     const uint64_t tt = t_first + i;
     const uint4 *tbase = tdb + (tt / 32) * (uint64_t)(kPlaneGroups * 64) + (tt % 32);
     uint32_t *mbase = nullptr;
@@ -204,21 +212,27 @@ __global__ void __launch_bounds__(256) prepare_direct_kernel(const uint4 *__rest
         const uint64_t mt = m_first + i;
         mbase = (uint32_t *)(masks + (mt / 32) * (uint64_t)kMaskTileUint4 + (mt % 32));
     }
+    // encode() of an element pair from its xpacked nibble (ep[2q], ep[2q+1], em[2q], em[2q+1] in
+    // bits 3..0): a 16-entry table in LDS; a wave's lanes read at most 16 distinct dwords in 16
+    // distinct banks (broadcasts otherwise), so the lookups never conflict
+    __shared__ uint32_t enc_lut[16];
+    if (threadIdx.x < 16) {
+        const uint32_t n = threadIdx.x, m0 = (n >> 1) & 1u, m1 = n & 1u, p0 = (n >> 3) & 1u, p1 = (n >> 2) & 1u;
+        enc_lut[n] = ((m0 - 2u * (p0 & m0)) & 0xFFFFu) | (((m1 - 2u * (p1 & m1)) & 0xFFFFu) << 16);
+    }
+    __syncthreads();
+    if (i >= m) return;
     const uint64_t g = g0 + i;
     for (int b = w; b < kBlocks; b += 4) {
         // dword b of the pattern / mask planes: word (b / 4, half b & 1), pair (b >> 1) & 1
         const uint2 x = ((const uint2 *)(tbase + (b >> 2) * 64 + 32 * (b & 1)))[(b >> 1) & 1];
-        uint32_t emlo, eplo, emhi, ephi;
-        xunpack(x.x, emlo, eplo);
-        xunpack(x.y, emhi, ephi);
-        const uint32_t mw = emlo | (emhi << 16), pw = eplo | (ephi << 16);
-        if (mbase) mbase[4 * ((b >> 3) * 64 + 32 * (b & 1)) + ((b & 6) >> 1)] = mw;
+        if (mbase) mbase[4 * ((b >> 3) * 64 + 32 * (b & 1)) + ((b & 6) >> 1)] = xmask(x.x) | (xmask(x.y) << 16);
         uint32_t last[16];
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
-            const uint32_t m0 = (mw >> (2 * q)) & 1u, m1 = (mw >> (2 * q + 1)) & 1u;
-            const uint32_t p0 = (pw >> (2 * q)) & 1u, p1 = (pw >> (2 * q + 1)) & 1u;
-            last[q] = ((m0 - 2u * (p0 & m0)) & 0xFFFFu) | (((m1 - 2u * (p1 & m1)) & 0xFFFFu) << 16);
+            const uint32_t xx = q < 8 ? x.x : x.y, sh = 4 * (q & 7);
+            const uint32_t off = sh >= 2 ? (xx >> (sh - 2)) & 0x3Cu : (xx << 2) & 0x3Cu;
+            last[q] = *(const uint32_t *)((const char *)enc_lut + off);
         }
         for (uint32_t j = 0; j + 1 < parties; ++j) {
             uint32_t r[16];
