@@ -441,8 +441,15 @@ __global__ void __launch_bounds__(64 * NW, 1)
 #endif
     };
 
-    // running best per query, lane-distributed: lane qi (< kBQ) holds query qi's
-    Partial best = partial_none();
+    // running best per lane and query across the walk: (num | den << 16, N-group x tile << 5 | rotation);
+    // den 0 = none yet
+    uint32_t run_nd[kBQ], run_jr[kBQ];
+#pragma unroll
+    for (int qi = 0; qi < kBQ; ++qi) {
+        run_nd[qi] = 1;  // (num 1, den 0): none
+        run_jr[qi] = 0;
+    }
+    Partial wave_best;
     v16f den[kBQ][WT], sacc[kBQ][WT];
     auto zero = [&] {
 #pragma unroll
@@ -543,6 +550,9 @@ __global__ void __launch_bounds__(64 * NW, 1)
         if (IRIS_BATCH2_DIAG != 4 || s == 0) store_a(s + 1, aq);  // the last step fills the idle stage (read by nobody)
         const uint32_t j = s / kSteps;
         if (s - j * kSteps == kSteps - 1) {  // N-group done: this wave's tiles, every query
+            // per lane and query: the best of the lane's 16 rotation rows, folded into the
+            // lane's running best (no cross-lane work until the end of the walk)
+            const int h = lane >> 5;
 #pragma unroll
             for (int t = 0; t < WT; ++t) {
                 const uint64_t trel = (gi + (uint64_t)j * G) * kTilesPerGroup + w * WT + t;
@@ -550,26 +560,28 @@ __global__ void __launch_bounds__(64 * NW, 1)
                 const bool valid = trel < ntiles && tg >= first && tg < end;
 #pragma unroll
                 for (int qi = 0; qi < kBQ; ++qi) {
-                    uint32_t bn, bd;
-                    int br;
-                    best_rotation(lane, [&](int r, uint32_t &nn, uint32_t &dd) {
-                        dd = (uint32_t)den[qi][t][r];
-                        nn = (uint32_t)(((int)dd - (int)sacc[qi][t][r]) >> 1);
-                    }, bn, bd, br);
-                    Partial c;
-                    c.num = bn;
-                    c.den = valid ? bd : 0;
-                    c.rot = br;
-                    c.pad = 0;
-                    c.idx = tg - first;
-                    // the wave's best of this tile for query qi, handed to lane qi
+                    // (bn, bd) = (1, 0) is "none": a row with den 0 (no jointly valid bit; also the
+                    // zero row k = 31) is (0, 0) and never wins, n * 0 < 1 * d holds for any real
+                    // candidate, so the scan needs no validity tests
+                    uint32_t bn = 1, bd = 0, br = 0;
 #pragma unroll
-                    for (int off = 32; off >= 1; off >>= 1) {
-                        const Partial o = partial_shfl_xor(c, off);
-                        if (partial_better_dev(o, c)) c = o;
+                    for (int r = 0; r < 16; ++r) {
+                        const int k = (r & 3) + 8 * (r >> 2) + 4 * h;  // ascending in r: ties keep the lower k
+                        const uint32_t dd = (uint32_t)den[qi][t][r];
+                        const uint32_t nn = (uint32_t)(((int)dd - (int)sacc[qi][t][r]) >> 1);
+                        if (__umul24(nn, bd) < __umul24(bn, dd)) {
+                            bn = nn;
+                            bd = dd;
+                            br = (uint32_t)k;
+                        }
                     }
-                    if (lane == qi && partial_better_dev(c, best)) best = c;
-                    __builtin_amdgcn_sched_barrier(0);
+                    const uint32_t rn = run_nd[qi] & 0xFFFFu, rd = run_nd[qi] >> 16;
+                    // strict <: an equal fraction keeps the earlier (lower-index) template; the
+                    // running best starts as (1, 0) too
+                    if (valid && __umul24(bn, rd) < __umul24(rn, bd)) {
+                        run_nd[qi] = bn | (bd << 16);
+                        run_jr[qi] = ((j * (uint32_t)WT + (uint32_t)t) << 5) | br;
+                    }
                 }
             }
             zero();
@@ -577,9 +589,35 @@ __global__ void __launch_bounds__(64 * NW, 1)
         barrier();
     }
 
+    // the lanes' running bests -> one Partial per query (lane qi holds query qi's): exact
+    // fraction, then the lowest index, then the lowest rotation (the two halves of a
+    // template's rotations live in lanes l and l ^ 32)
+    {
+        Partial best = partial_none();
+#pragma unroll
+        for (int qi = 0; qi < kBQ; ++qi) {
+            Partial c = partial_none();
+            if (run_nd[qi] >> 16) {
+                const uint32_t jt = run_jr[qi] >> 5, jj = jt / WT, t = jt - jj * WT;
+                const uint64_t trel = (gi + (uint64_t)jj * G) * kTilesPerGroup + w * WT + t;
+                c.num = run_nd[qi] & 0xFFFFu;
+                c.den = run_nd[qi] >> 16;
+                c.rot = (int)(run_jr[qi] & 31u);
+                c.idx = (tile0 + trel) * 32 + (lane & 31) - first;
+            }
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) {
+                const Partial o = partial_shfl_xor(c, off);
+                if (partial_better_rot(o, c)) c = o;
+            }
+            if (lane == qi) best = c;
+        }
+        wave_best = best;
+    }
+
     __syncthreads();
     Partial *sP = (Partial *)&afrag[0][0][0][0][0];  // [wave][query]
-    if (lane < kBQ) sP[w * kBQ + lane] = best;
+    if (lane < kBQ) sP[w * kBQ + lane] = wave_best;
     __syncthreads();
     if (tid < kBQ) {
         Partial b = sP[tid];

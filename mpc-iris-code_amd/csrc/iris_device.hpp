@@ -91,12 +91,23 @@ __device__ __forceinline__ void split_bytes(const uint32_t *src8, uint4 &lo, uin
 // Candidate order of the resolver / search argmin: exact fraction (u32 cross-
 // multiplication, num and den < 2^16), then the lowest index; den = 0 is "no
 // candidate" (NaN / +inf in the reference, never selected by a strict <).
+// (__umul24: num, den < 2^16, so the 24-bit multiply's low 32 bits are the exact product, at
+// full rate where a 32-bit v_mul_lo_u32 issues at a quarter)
 __device__ __forceinline__ bool partial_better_dev(const Partial &a, const Partial &b) {
     if (a.den == 0) return false;
     if (b.den == 0) return true;
-    const uint32_t l = a.num * b.den, r = b.num * a.den;
+    const uint32_t l = __umul24(a.num, b.den), r = __umul24(b.num, a.den);
     if (l != r) return l < r;
     return a.idx < b.idx;
+}
+// as partial_better_dev, then the lower rotation (two candidates of one template)
+__device__ __forceinline__ bool partial_better_rot(const Partial &a, const Partial &b) {
+    if (a.den == 0) return false;
+    if (b.den == 0) return true;
+    const uint32_t l = __umul24(a.num, b.den), r = __umul24(b.num, a.den);
+    if (l != r) return l < r;
+    if (a.idx != b.idx) return a.idx < b.idx;
+    return a.rot < b.rot;
 }
 
 __device__ __forceinline__ Partial partial_shfl_xor(const Partial &c, int off) {
@@ -126,7 +137,7 @@ __device__ __forceinline__ void best_rotation(int lane, F frac, uint32_t &bn, ui
         const int k = (r & 3) + 8 * (r >> 2) + 4 * h;  // ascending in r within a half
         uint32_t nn, dd;
         frac(r, nn, dd);
-        if (k < kRot && dd != 0 && (bd == 0 || nn * bd < bn * dd)) {
+        if (k < kRot && dd != 0 && (bd == 0 || __umul24(nn, bd) < __umul24(bn, dd))) {
             bn = nn;
             bd = dd;
             br = k;
@@ -134,7 +145,8 @@ __device__ __forceinline__ void best_rotation(int lane, F frac, uint32_t &bn, ui
     }
     const uint32_t pn = __shfl_xor(bn, 32), pd = __shfl_xor(bd, 32);
     const int pr = __shfl_xor(br, 32);
-    if (pd != 0 && (bd == 0 || pn * bd < bn * pd || (pn * bd == bn * pd && pr < br))) {
+    const uint32_t pl = __umul24(pn, bd), pr_ = __umul24(bn, pd);
+    if (pd != 0 && (bd == 0 || pl < pr_ || (pl == pr_ && pr < br))) {
         bn = pn;
         bd = pd;
         br = pr;
