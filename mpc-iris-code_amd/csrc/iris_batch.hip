@@ -363,6 +363,9 @@ __global__ void __launch_bounds__(256) batch_reduce_kernel(const Partial *__rest
 #define IRIS_BATCH2_DIAG 0
 #endif
 // 1: block b + 1's fragment reads issued between block b's MFMAs; 0: each block reads its own
+#ifndef IRIS_BATCH2_STAGGER
+#define IRIS_BATCH2_STAGGER 1
+#endif
 #ifndef IRIS_BATCH2_ROLL
 #define IRIS_BATCH2_ROLL 1
 #endif
@@ -393,6 +396,17 @@ __global__ void __launch_bounds__(64 * NW, 1)
     const uint64_t ngroups = (ntiles + kTilesPerGroup - 1) / kTilesPerGroup;
     const uint32_t my_groups = gi < ngroups ? (uint32_t)((ngroups - gi + G - 1) / G) : 0;
     const uint32_t total = my_groups * kSteps;
+    // Stagger (IRIS_BATCH2_STAGGER): the two waves sharing a SIMD (w and w + 4) run their N-groups
+    // half a group apart, so one wave's epilogue (no MFMAs) overlaps its partner's MFMAs.  The
+    // K-step at time s is s mod kSteps for every wave (the A fragments in LDS are shared); waves
+    // 4..7 start their first group at s = off and the workgroup walks off extra steps, in which
+    // the idle waves' MFMAs run on re-read rows and are discarded.
+    const uint32_t off = (IRIS_BATCH2_STAGGER && NW == 8 && w >= NW / 2) ? (uint32_t)(kSteps / 2) : 0u;
+    const uint32_t walk = total ? total + ((IRIS_BATCH2_STAGGER && NW == 8) ? (uint32_t)(kSteps / 2) : 0u) : 0u;
+    auto group_of = [&](uint32_t s) {  // this wave's N-group at time s (clamped while idle)
+        const uint32_t r = s >= off ? (s - off) / kSteps : 0u;
+        return r < my_groups ? r : my_groups - 1;
+    };
 
     // this wave's compact A rows of a K-step: r = w + NW i -> query r % kBQ, chunk pair r / kBQ
     const uint4 *abase = qtiles + (uint64_t)(qg * kBQ) * kTileU4 + lane;
@@ -405,7 +419,7 @@ __global__ void __launch_bounds__(64 * NW, 1)
         }
     };
     auto b_row = [&](uint32_t s, int t) {  // tile t of this wave, chunk pair 0 of K-step s
-        const uint32_t j = s / kSteps, k = s - j * kSteps;
+        const uint32_t j = group_of(s), k = s % kSteps;
         const uint64_t trel = (gi + (uint64_t)j * G) * kTilesPerGroup + w * WT + t;
         return db + (tile0 + (trel < ntiles ? trel : ntiles - 1)) * (uint64_t)kTileU4 + (k * kGP) * 64 + lane;
     };
@@ -463,7 +477,10 @@ __global__ void __launch_bounds__(64 * NW, 1)
                 }
     };
     zero();
-    if (NW == 8 && w >= NW / 2) __builtin_amdgcn_s_setprio(1);  // the younger half (see batch_kernel)
+#ifndef IRIS_BATCH2_PRIO
+#define IRIS_BATCH2_PRIO 0  // 1: s_setprio 1 for waves 4..7 (helped before the stagger, costs 2.6 % with it)
+#endif
+    if (IRIS_BATCH2_PRIO && NW == 8 && w >= NW / 2) __builtin_amdgcn_s_setprio(1);  // the younger half (see batch_kernel)
 
     // B rolls through bq: chunk pair g of step s + 1 is loaded into bq[t][g] as soon as step s
     // has expanded both of its chunks — one K-step of latency cover
@@ -481,10 +498,10 @@ __global__ void __launch_bounds__(64 * NW, 1)
         barrier();
     }
 #pragma unroll 1
-    for (uint32_t s = 0; s < total; ++s) {
+    for (uint32_t s = 0; s < walk; ++s) {
         // A(s + 1) is loaded first, so waiting for it leaves step s + 1's B loads in flight;
         // branch-free: the last step re-loads its own rows (harmless) instead of skipping
-        const uint32_t s1 = s + 1 < total ? s + 1 : s;
+        const uint32_t s1 = s + 1 < walk ? s + 1 : s;
         uint4 aq[kAper];
         if (IRIS_BATCH2_DIAG != 4 || s == 0) load_a(s1, aq);
         const uint4(*st)[kBQ][4][64] = afrag[s & 1];
@@ -548,8 +565,11 @@ __global__ void __launch_bounds__(64 * NW, 1)
             }
         }
         if (IRIS_BATCH2_DIAG != 4 || s == 0) store_a(s + 1, aq);  // the last step fills the idle stage (read by nobody)
-        const uint32_t j = s / kSteps;
-        if (s - j * kSteps == kSteps - 1) {  // N-group done: this wave's tiles, every query
+        // a group ends at s when s + 1 - off is a multiple of kSteps; the end at s = off - 1 closes
+        // a staggered wave's idle steps (nothing to record, only the zeroing)
+        if (s + 1 >= off && (s + 1 - off) % kSteps == 0) {  // N-group done: this wave's tiles, every query
+            const bool live = s >= off;
+            const uint32_t j = live ? (s + 1 - off) / kSteps - 1 : 0u;
             // per lane and query: the best of the lane's 16 rotation rows, folded into the
             // lane's running best (no cross-lane work until the end of the walk)
             const int h = lane >> 5;
@@ -557,7 +577,7 @@ __global__ void __launch_bounds__(64 * NW, 1)
             for (int t = 0; t < WT; ++t) {
                 const uint64_t trel = (gi + (uint64_t)j * G) * kTilesPerGroup + w * WT + t;
                 const uint64_t tg = (tile0 + trel) * 32 + (lane & 31);
-                const bool valid = trel < ntiles && tg >= first && tg < end;
+                const bool valid = live && trel < ntiles && tg >= first && tg < end;
 #pragma unroll
                 for (int qi = 0; qi < kBQ; ++qi) {
                     // (bn, bd) = (1, 0) is "none": a row with den 0 (no jointly valid bit; also the
