@@ -45,6 +45,23 @@ def test_bench_two_ranks(workload):
         assert len(found) == 4 and len(d["check"]["query_groups"]) >= 2
 
 
+def test_bench_eight_ranks_one_gpu():
+    """The driver's 8-GPU scaling run rehearsed on the one GPU: `python bench.py --gpus 8`
+    (self-launched, 8 ranks sharing the card over gloo, 200k templates each) prints one line
+    with n_gpus 8 whose planted answer lies in a later rank's shard."""
+    env = dict(os.environ, IRIS_DIST_BACKEND="gloo")
+    cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", "8", "--steps", "2", "--warmup", "1",
+           "--n-per-gpu", "200000", "--no-cpu-baseline", "--prewarm-s", "0"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 8 and d["ranks_seen"] == 8 and d["backend"] == "gloo" and d["check"]["ok"]
+    assert d["config"]["total_templates"] == 1_600_000
+    assert d["check"]["planted_index"] >= 200000
+
+
 def test_bench_self_launch_two_ranks():
     """`python bench.py --gpus 2` with no launcher starts both ranks itself (here on the one
     GPU, gloo exchange) and prints one line with n_gpus 2."""
