@@ -197,7 +197,7 @@ def _time_passes(fn, seconds, max_passes=1000):
     return passes, t
 
 
-def cpu_baseline(args):
+def cpu_baseline(args, reserve=0):
     """The oracle's CPU restatement of the reference path for this workload (test
     infrastructure: oracle/), compiled -O3 -march=native for this host and run on every
     CPU the process may use, timed on a bounded sample (~--cpu-seconds) of the same
@@ -212,6 +212,9 @@ def cpu_baseline(args):
     threads = info["affinity_cpus"]
     if info["cgroup_cpu_quota"]:
         threads = max(1, min(threads, int(-(-info["cgroup_cpu_quota"] // 1))))
+    # reserve: CPUs left to a concurrent GPU-driving thread (the leg runs beside the untimed
+    # pre-warm, so the GPU is busy while the CPU is measured; the thread count says so)
+    threads = max(1, threads - reserve)
     path = pathlib.Path(tempfile.gettempdir()) / f"liboracle_native_{os.getpid()}.so"
     try:
         oc.build(path, march="native")
@@ -811,11 +814,29 @@ def main():
     # steady rate (tools/engine_variance.py: the first ~100 searches of a process run up to 4 %
     # slower, then settle); untimed, like the warmup steps, and reported under "setup"
     # local searches only: ranks run different numbers of them, so no collective may be inside
+    # the CPU baseline (rank 0 of a one-rank run) is measured beside the pre-warm, on all but one
+    # of the CPUs (the other drives the GPU), so the run's CPU leg and its GPU load overlap; the
+    # timed steps start after both
+    cpu_box = {}
+    cpu_thread = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        import threading
+
+        def _cpu_leg():
+            try:
+                cpu_box["cpu"] = cpu_baseline(args, reserve=1)
+            except Exception as ex:  # reported, never fatal
+                cpu_box["cpu"] = {"value": None, "error": str(ex)}
+
+        cpu_thread = threading.Thread(target=_cpu_leg, daemon=True)
+        cpu_thread.start()
     t_pre = time.perf_counter()
     prewarm_steps = 0
-    while time.perf_counter() - t_pre < args.prewarm_s:
+    while time.perf_counter() - t_pre < args.prewarm_s or (cpu_thread is not None and cpu_thread.is_alive()):
         step(exchange=False)
         prewarm_steps += 1
+    if cpu_thread is not None:
+        cpu_thread.join()
     prewarm_s = time.perf_counter() - t_pre
     if args.warmup:
         m = run_steps(args.warmup)
@@ -873,12 +894,7 @@ def main():
     value = ROT * total * nq / (elapsed / args.steps)
 
     if rank == 0:
-        cpu = None
-        if world == 1 and not args.no_cpu_baseline:
-            try:
-                cpu = cpu_baseline(args)
-            except Exception as ex:  # reported, never fatal
-                cpu = {"value": None, "error": str(ex)}
+        cpu = cpu_box.get("cpu")
         line = {
             "metric": METRIC,
             "value": value,
