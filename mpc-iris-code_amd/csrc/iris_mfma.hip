@@ -93,17 +93,25 @@ __device__ __forceinline__ uint4 stream_load(const uint4 *p) {
 
 enum { MF_COUNTS = 0, MF_SEARCH = 1 };
 
-template <int MODE, int T = kMfmaTiles>
+// KS > 1 (small ranges, T = 1): the KS waves of a tile group split K -- wave w computes
+// chunk groups [w' * 100 / KS, +100 / KS) of tile blockIdx.x * (4 / KS) + w / KS (w' = w % KS)
+// -- and the partial sums (exact integers in f32) meet in LDS before the epilogue, so a range of
+// a few hundred tiles still puts several waves on every SIMD.
+template <int MODE, int T = kMfmaTiles, int KS = 1>
 __global__ void __launch_bounds__(256, kMfmaWgs)
     template_mfma_kernel(const uint4 *__restrict__ db, const uint4 *__restrict__ qfrag, uint64_t tile0,
                          uint64_t ntiles, uint64_t first, uint64_t end, uint16_t *__restrict__ num_out,
                          uint16_t *__restrict__ den_out, double *__restrict__ dist_out,
                          Partial *__restrict__ partials) {
+    static_assert(KS == 1 || (T == 1 && kWaveSlots % KS == 0 && kPlaneGroups % KS == 0), "K-split geometry");
     const int lane = threadIdx.x & 63;
     const int wslot = threadIdx.x >> 6;
-    const uint64_t wave = (uint64_t)blockIdx.x * kWaveSlots + wslot;
+    const int slice = wslot % KS;
+    const uint64_t wave = (uint64_t)blockIdx.x * (kWaveSlots / KS) + wslot / KS;
     const uint64_t tw = wave * T;  // first tile (relative to tile0) of this wave
     const bool active = tw < ntiles;  // wave-uniform
+    constexpr int kG = kPlaneGroups / KS;  // chunk groups of this wave's K-slice
+    const int g0 = slice * kG;
 
     v16f den[T], s[T];
 #pragma unroll
@@ -130,7 +138,7 @@ __global__ void __launch_bounds__(256, kMfmaWgs)
             uint4 q0, q1;
         };
         auto load = [&](Stage &st, int g) {
-            g = g < kPlaneGroups ? g : kPlaneGroups - 1;
+            g = g0 + (g < kG ? g : kG - 1);
 #pragma unroll
             for (int t = 0; t < T; ++t) st.d[t] = stream_load(dp[t] + g * 64);
             st.q0 = qp[(2 * g) * 64];
@@ -153,7 +161,7 @@ __global__ void __launch_bounds__(256, kMfmaWgs)
         load(sb, 1);
         int g = 0;
 #pragma unroll 1
-        for (; g + 3 <= kPlaneGroups; g += 3) {
+        for (; g + 3 <= kG; g += 3) {
             load(sc, g + 2);
             compute(sa);
             load(sa, g + 3);
@@ -161,8 +169,29 @@ __global__ void __launch_bounds__(256, kMfmaWgs)
             load(sb, g + 4);
             compute(sc);
         }
-        // kPlaneGroups = 100 = 33 * 3 + 1: one step left, its data is in sa
-        if (g < kPlaneGroups) compute(sa);
+        // kG = 3q + {1, 2} (100, 25; 50): the remaining steps' data is in sa (, sb)
+        if constexpr (kG % 3 >= 1) compute(sa);
+        if constexpr (kG % 3 == 2) compute(sb);
+    }
+    if constexpr (KS > 1) {  // the K-slices' partial sums -> slice 0's accumulators (exact)
+        __shared__ float red[kWaveSlots][32][64];
+        if (slice != 0) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                red[wslot][i][lane] = den[0][i];
+                red[wslot][16 + i][lane] = s[0][i];
+            }
+        }
+        __syncthreads();
+        if (slice == 0) {
+#pragma unroll
+            for (int k = 1; k < KS; ++k)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    den[0][i] += red[wslot + k][i][lane];
+                    s[0][i] += red[wslot + k][16 + i][lane];
+                }
+        }
     }
 
     // C layout: lane l holds template (l & 31) of the tile and rotation rows
@@ -172,7 +201,7 @@ __global__ void __launch_bounds__(256, kMfmaWgs)
 #pragma unroll
     for (int t = 0; t < T; ++t) {
         const uint64_t t0 = (tile0 + tw + t) * kTileRecs;  // global index of the tile's first template
-        const bool tv = active && (tw + t < ntiles);
+        const bool tv = active && (tw + t < ntiles) && slice == 0;
         if constexpr (MODE == MF_COUNTS) {
             __shared__ __attribute__((aligned(16))) uint16_t sh_out[kWaveSlots][1024];
             uint16_t *lds = sh_out[wslot];
@@ -448,11 +477,16 @@ int launch_generate_tiles(void *stream, void *db, uint64_t t_first, uint64_t n, 
 struct TileRange {
     uint64_t tile0, ntiles, grid;
     int tiles_per_wave;
+    int ksplit;  // 4: a tile's 4 waves split K (ranges of at most kSplitTiles tiles)
 };
 
 // Below this many tiles, 4 tiles per wave would leave CUs idle (fewer than 2
 // workgroups per CU): small ranges run one tile per wave, 4x the workgroups.
 constexpr uint64_t kSmallTiles = 4 * kWaveSlots * 256 * 2;
+// Up to this many tiles (32k templates: configs[0]'s 10k, the reference's 20k-record chunks)
+// even one tile per wave leaves most SIMDs without a wave: the 4 waves of a workgroup split
+// one tile's K instead.
+constexpr uint64_t kSplitTiles = 1024;
 
 static TileRange tile_range(LaunchRange r) {
     TileRange t;
@@ -460,8 +494,18 @@ static TileRange tile_range(LaunchRange r) {
     const uint64_t tile1 = (r.first + r.n + kTileRecs - 1) / kTileRecs;
     t.ntiles = tile1 - t.tile0;
     t.tiles_per_wave = t.ntiles < kSmallTiles ? 1 : kMfmaTiles;
-    // test hook: IRIS_TILES_PER_WAVE=1|4 pins the variant (tests run both on small ranges)
-    if (const char *f = getenv("IRIS_TILES_PER_WAVE")) t.tiles_per_wave = atoi(f) == 1 ? 1 : kMfmaTiles;
+    t.ksplit = t.ntiles <= kSplitTiles ? 4 : 1;
+    // test hook: IRIS_TILES_PER_WAVE=1|4 pins the variant (tests run all three on small ranges:
+    // unset = the K-split form there)
+    if (const char *f = getenv("IRIS_TILES_PER_WAVE")) {
+        t.tiles_per_wave = atoi(f) == 1 ? 1 : kMfmaTiles;
+        t.ksplit = 1;
+    }
+    if (t.ksplit > 1) {
+        t.tiles_per_wave = 1;
+        t.grid = t.ntiles;  // one tile per workgroup
+        return t;
+    }
     const uint64_t waves = (t.ntiles + t.tiles_per_wave - 1) / t.tiles_per_wave;
     t.grid = (waves + kWaveSlots - 1) / kWaveSlots;
     return t;
@@ -492,7 +536,8 @@ int launch_template_mfma_counts(void *stream, const void *db, const void *qfrag,
                                 uint16_t *den_out) {
     if (r.n == 0) return 0;
     const TileRange t = tile_range(r);
-    auto kern = t.tiles_per_wave == 1 ? template_mfma_kernel<MF_COUNTS, 1> : template_mfma_kernel<MF_COUNTS>;
+    auto kern = t.ksplit > 1 ? template_mfma_kernel<MF_COUNTS, 1, 4>
+                : t.tiles_per_wave == 1 ? template_mfma_kernel<MF_COUNTS, 1> : template_mfma_kernel<MF_COUNTS>;
     hipLaunchKernelGGL(kern, dim3((uint32_t)t.grid), dim3(256), 0, (hipStream_t)stream,
                        (const uint4 *)db, (const uint4 *)qfrag, t.tile0, t.ntiles, r.first, r.first + r.n, num_out,
                        den_out, (double *)nullptr, (Partial *)nullptr);
@@ -504,7 +549,8 @@ int launch_template_mfma_search(void *stream, const void *db, const void *qfrag,
     const TileRange t = tile_range(r);
     *n_partials = (uint32_t)t.grid;
     if (r.n == 0) return 0;
-    auto kern = t.tiles_per_wave == 1 ? template_mfma_kernel<MF_SEARCH, 1> : template_mfma_kernel<MF_SEARCH>;
+    auto kern = t.ksplit > 1 ? template_mfma_kernel<MF_SEARCH, 1, 4>
+                : t.tiles_per_wave == 1 ? template_mfma_kernel<MF_SEARCH, 1> : template_mfma_kernel<MF_SEARCH>;
     hipLaunchKernelGGL(kern, dim3((uint32_t)t.grid), dim3(256), 0, (hipStream_t)stream,
                        (const uint4 *)db, (const uint4 *)qfrag, t.tile0, t.ntiles, r.first, r.first + r.n,
                        (uint16_t *)nullptr, (uint16_t *)nullptr, dist_out, partials);
