@@ -51,7 +51,8 @@ HBM_READ_CEILING_GBS = 7016.0
 # integer VALU issue ceiling for v_bcnt/v_bitop3 (16 lanes/clk/SIMD measured, tools/ubench_ops.hip)
 VALU_INT_PEAK_OPS = 256 * 4 * 16 * 2.4e9
 FP4_DENSE_PEAK_MACS = 10e15 / 2            # MI355X_MICROARCH.md: ~10 PF dense fp4
-MFMA_MACS_PER_TEMPLATE = 2 * 12800 * 32    # den + enc products, 32 rotation rows
+MFMA_MACS_PER_TEMPLATE = 2 * 12800 * 31    # algorithmic: den + enc products of the 31 rotations
+MFMA_MACS_ISSUED_PER_TEMPLATE = 2 * 12800 * 32  # issued: the 32x32 tile carries a zero 32nd row
 BYTES_PER_TEMPLATE = 3200    # pattern + mask planes, read once per query
 TRITS_BYTES_PER_TEMPLATE = 2560  # --layout trits: 12800 three-state positions, five per byte
 VALU_OPS_PER_TEMPLATE = 400 * 31 * 4   # words x rotations x (and, bitop3, 2x bcnt)
@@ -96,6 +97,17 @@ def parse():
     ap.add_argument("--parties", type=int, default=3, help="parties (workloads resolver, prepare)")
     ap.add_argument("--rounds", type=int, default=12, choices=[8, 12, 20],
                     help="ChaCha rounds for --workload prepare (12 = the reference's thread_rng, rand 0.8.5)")
+    ap.add_argument("--single-process", action="store_true",
+                    help="search / batch: ONE process drives --gpus devices as a library device group "
+                         "(iris_group_*: ncclCommInitAll, RCCL all-gather of the shard winners) instead of "
+                         "one torchrun rank per GPU")
+    ap.add_argument("--attached", action="store_true",
+                    help="host-shares / host-masks: the host array is attached to a resident database "
+                         "(iris_db_attach_host), so the reference-signature calls on its slices upload nothing")
+    ap.add_argument("--chunk", type=int, default=None,
+                    help="host-shares / host-masks: records per batch_process call (the reference's "
+                         "participant / resolver use 20 000, src/main.rs:428,473; default: 20 000 with "
+                         "--attached, else the whole array in one call)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher rehearsal without a GPU: start / join the ranks, check the world size, "
                          "exchange and merge a synthetic per-rank result over gloo, print the line (value null)")
@@ -373,14 +385,12 @@ def _free_port():
 
 def launch_ranks(args):
     """`python bench.py --gpus N` (N > 1) without a launcher: run the N ranks under
-    torch.distributed.run as a CHILD process (nothing in this process has touched a GPU;
-    no exec) and return their exit status.  Refuses (rc 2) when the RCCL backend is asked
-    for more GPUs than are visible."""
+    torch.distributed.run as a CHILD process and return their exit status (this process may
+    have initialised HIP by counting devices, so it must only ever spawn children, never
+    re-exec).  Refuses (rc 2) when the RCCL path is asked for more GPUs than are visible."""
     backend = "gloo" if args.dry_run else os.environ.get("IRIS_DIST_BACKEND", "nccl")
     if backend == "nccl":
-        import torch
-
-        have = torch.cuda.device_count()  # counts devices without initialising HIP
+        have = ih.Device.count()
         if have < args.gpus:
             print(f"error: --gpus {args.gpus} needs {args.gpus} visible GPUs for one RCCL rank each; "
                   f"{have} visible", file=sys.stderr)
@@ -392,36 +402,81 @@ def launch_ranks(args):
     return subprocess.call(cmd, env=env)
 
 
-def init_ranks(args):
-    """Process-group setup for a multi-rank run.  Returns (dist module or None, world, rank,
-    device ordinal, backend, exchange device)."""
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        raise SystemExit(f"error: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
-    # "nccl" is RCCL on ROCm (the exchange runs over xGMI); IRIS_DIST_BACKEND=gloo
-    # rehearses the same flow with CPU exchange tensors (e.g. 2 ranks on 1 GPU).
-    backend = "gloo" if args.dry_run else os.environ.get("IRIS_DIST_BACKEND", "nccl")
-    # IRIS_FORCE_DIST=1 runs the process-group path even for one rank (a one-GPU rehearsal of
-    # the RCCL exchange, barriers and max-over-ranks timing)
-    if world == 1 and os.environ.get("IRIS_FORCE_DIST") != "1":
-        return None, 1, 0, 0, None, "cpu"
-    import torch
-    import torch.distributed as dist
+class Ranks:
+    """Who this process is in a multi-rank run.
 
-    ordinal = local
-    if not args.dry_run:
-        have = torch.cuda.device_count()
-        if backend == "nccl" and local >= have:
-            raise SystemExit(f"error: rank {rank} (local {local}) has no GPU of its own: {have} visible")
-        ordinal = local % max(1, have)
-        torch.cuda.set_device(ordinal)
-    dist.init_process_group(backend, rank=rank, world_size=world)
-    if dist.get_world_size() != args.gpus:
-        raise SystemExit(f"error: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
-    xdev = f"cuda:{ordinal}" if backend == "nccl" else "cpu"
-    return dist, world, rank, ordinal, backend, xdev
+    backend "nccl" (the default, one rank per GPU): torch.distributed runs on gloo (CPU) for
+    the rendezvous, barriers and the max-over-ranks timing only; the data-path exchange is
+    the library's own RCCL communicator (iris_group_create_rank, librccl from /opt/rocm):
+    rank 0's 128-byte id is broadcast over gloo, every rank joins with its GPU, and the
+    shard winners are all-gathered by the library.  IRIS_DIST_BACKEND=gloo rehearses the
+    flow without RCCL (several ranks may then share one GPU): the winners go through torch
+    CPU tensors and iris_match_merge.  --single-process: one process, a library group over
+    --gpus devices, no torch at all."""
+
+    def __init__(self, args):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.dist = None
+        self.group = None
+        self.backend = None
+        self.ordinal = 0
+        if args.single_process:
+            if "WORLD_SIZE" in os.environ and self.world > 1:
+                raise SystemExit("error: --single-process drives every GPU from one process; do not launch ranks")
+            self.world, self.rank = 1, 0
+            self.backend = "rccl (library group, ncclCommInitAll)"
+            return
+        if self.world != args.gpus:
+            raise SystemExit(f"error: --gpus {args.gpus} but the launcher started WORLD_SIZE={self.world} ranks")
+        backend = "gloo" if args.dry_run else os.environ.get("IRIS_DIST_BACKEND", "nccl")
+        # IRIS_FORCE_DIST=1 runs the process-group path even for one rank (a one-GPU rehearsal
+        # of the RCCL exchange, barriers and max-over-ranks timing)
+        if self.world == 1 and os.environ.get("IRIS_FORCE_DIST") != "1":
+            return
+        import torch.distributed as dist
+
+        if not args.dry_run:
+            have = ih.Device.count()
+            if backend == "nccl" and self.local >= have:
+                raise SystemExit(f"error: rank {self.rank} (local {self.local}) has no GPU of its own: {have} visible")
+            self.ordinal = self.local % max(1, have)
+        dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit(f"error: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
+        self.dist = dist
+        self.backend = "gloo" if backend == "gloo" else "rccl (library group, ncclCommInitRank; gloo control)"
+        self.rccl = backend == "nccl"
+
+    def join_group(self, args):
+        """The library device group of this run (None: single device, or the gloo rehearsal)."""
+        if args.single_process:
+            self.group = ih.Group(list(range(args.gpus)))
+        elif self.dist is not None and self.rccl:
+            box = [ih.Group.unique_id() if self.rank == 0 else None]
+            self.dist.broadcast_object_list(box, src=0)
+            self.group = ih.Group.rank(self.ordinal, self.world, self.rank, box[0])
+        return self.group
+
+    def barrier(self):
+        if self.dist is not None:
+            self.dist.barrier()
+
+    def max_over_ranks(self, x):
+        if self.dist is None:
+            return x
+        import torch
+
+        t = torch.tensor([x], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def close(self):
+        if self.group is not None:
+            self.group.close()
+        if self.dist is not None:
+            self.dist.destroy_process_group()
 
 
 def launcher_name():
@@ -430,32 +485,26 @@ def launcher_name():
     return "torch.distributed.run" if "WORLD_SIZE" in os.environ else "none"
 
 
-def dry_run(args, dist, world, rank, backend):
+def dry_run(args, ranks):
     """No GPU: each rank contributes a synthetic shard result (equal distances, so the
     lowest global index — rank 0's — must win the merge, src/main.rs:616-621)."""
     import iris_dist
 
     n = args.n_per_gpu or 10_000_000
     t0 = time.perf_counter()
-    local = ih.Match(0.25, rank * n + 7, 10, 40, -3, 0)
-    merged = iris_dist.allgather_merge(local, device="cpu") if dist is not None else local
-    elapsed = time.perf_counter() - t0
-    if dist is not None:
-        import torch
-
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    local = ih.Match(0.25, ranks.rank * n + 7, 10, 40, -3, 0)
+    merged = iris_dist.allgather_merge(local) if ranks.dist is not None else local
+    elapsed = ranks.max_over_ranks(time.perf_counter() - t0)
     ok = merged.index == 7 and merged.distance == 0.25
-    if rank == 0:
-        print(json.dumps({"metric": METRIC, "value": None, "unit": "template comparisons/s", "n_gpus": world,
-                          "ranks_seen": world, "backend": backend, "launcher": launcher_name(), "dry_run": True,
-                          "steps": 0, "warmup": 0, "ms_per_step": elapsed * 1e3, "higher_is_better": True,
-                          "scaling": "weak", "vs_baseline": None, "dtype": None, "data": "none (dry run)",
+    if ranks.rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "template comparisons/s", "n_gpus": ranks.world,
+                          "ranks_seen": ranks.world, "backend": ranks.backend, "launcher": launcher_name(),
+                          "dry_run": True, "steps": 0, "warmup": 0, "ms_per_step": elapsed * 1e3,
+                          "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": None,
+                          "data": "none (dry run)",
                           "config": {"workload": "launcher rehearsal", "templates_per_gpu": n},
                           "check": {"merged_index": int(merged.index), "ok": bool(ok)}}))
-    if dist is not None:
-        dist.destroy_process_group()
+    ranks.close()
     if not ok:
         sys.exit(3)
 
@@ -529,15 +578,28 @@ def run_aux(args, dev):
             host = gen_records(dev, ih.KIND_MASKS, n, SEED)
             eng = ih.MasksEngine(dev, qt[200:])
         hout = np.empty((n, ROT), np.uint16)
+        chunk = args.chunk or (20_000 if args.attached else n)
+        kind = ih.KIND_SHARES if shares_wl else ih.KIND_MASKS
+        adb = None
+        if args.attached:  # the mmap'd file's device copy (iris_db_attach_host), made once
+            adb = ih.Database(dev, kind, n)
+            t_att = time.perf_counter()
+            adb.attach_host(host)
+            extra["attach_s"] = time.perf_counter() - t_att
 
         def step():
-            eng.batch_process(hout, host)
+            for a in range(0, n, chunk):
+                eng.batch_process(hout[a:a + chunk], host[a:a + chunk])
 
         kname, unit = ("shares" if shares_wl else "masks"), "records/s"
         rec_bytes = host.shape[1] * host.itemsize
-        workload = (f"{'DistanceEngine' if shares_wl else 'MasksEngine'}::batch_process(out, db: &[T]) over a host "
-                    "slice (src/lib.rs:42-52, 69-79): H2D of the pageable slice (runtime-staged) + TILES pack per "
-                    "256-MB chunk, then the engine kernel; PCIe-inclusive")
+        workload = (f"{'DistanceEngine' if shares_wl else 'MasksEngine'}::batch_process(out, db: &[T]) over host "
+                    f"slices of {chunk} records (src/lib.rs:42-52, 69-79; the participant / resolver loop of "
+                    "src/main.rs:426-431, 511-516): "
+                    + ("the host array is attached to its resident copy (iris_db_attach_host): no upload"
+                       if args.attached else
+                       "H2D of the pageable slice (runtime-staged) + TILES pack per 256-MB chunk, then the "
+                       "engine kernel; PCIe-inclusive"))
     elif args.workload == "criterion":
         # configs[0]: 1 query x 31 x 10k templates (resident), plus the arch shapes below
         n = min(args.n_per_gpu, 10_000)
@@ -612,6 +674,30 @@ def run_aux(args, dev):
         ok = m.index == idx and np.float64(m.distance).view(np.uint64) == np.float64(best).view(np.uint64)
         check = {"expected_index": int(idx), "found_index": int(m.index), "ok": bool(ok)}
     elif args.workload in ("host-shares", "host-masks"):
+        if args.attached:  # the same chunks through the resident calls, for comparison
+            hdev = dev.alloc(chunk * ROT * 2)
+            res = {}
+            for form in ("host_out", "device_out"):
+                for _ in range(2):
+                    for a in range(0, n, chunk):
+                        if form == "host_out":
+                            eng.batch_process(hout[a:a + chunk], adb, first=a, n=min(chunk, n - a))
+                        else:
+                            eng.batch_process_device(adb, hdev, first=a, n=min(chunk, n - a))
+                dev.synchronize()
+                tr = time.perf_counter()
+                for _ in range(args.steps):
+                    for a in range(0, n, chunk):
+                        if form == "host_out":
+                            eng.batch_process(hout[a:a + chunk], adb, first=a, n=min(chunk, n - a))
+                        else:
+                            eng.batch_process_device(adb, hdev, first=a, n=min(chunk, n - a))
+                dev.synchronize()
+                res[form + "_records_per_s"] = n * args.steps / (time.perf_counter() - tr)
+            dev.free(hdev)
+            res["attached_vs_device_out"] = (n * args.steps / elapsed) / res["device_out_records_per_s"]
+            res["attached_vs_host_out"] = (n * args.steps / elapsed) / res["host_out_records_per_s"]
+            extra["resident_same_chunks"] = res
         sample = np.random.default_rng(2).choice(n, 16, replace=False)
         want = (check_shares_rows(ih.encode(ih.Template.from_array(qt)).values, host[sample])
                 if args.workload == "host-shares" else check_masks_rows(qt[200:], host[sample]))
@@ -661,7 +747,9 @@ def run_aux(args, dev):
                   "host-masks": "fp4 e2m1 MFMA -> f32 (0/1 products)",
                   "criterion": "fp4 e2m1 MFMA -> f32 (0/+-1 products)"}[args.workload],
         "data": "synthetic (uniform random u16 / on-device generated templates)",
-        "config": {"workload": workload, "records_per_gpu": n, "parties": P},
+        "config": {"workload": workload, "records_per_gpu": n, "parties": P,
+                   **({"chunk": chunk, "attached": bool(args.attached)}
+                      if args.workload in ("host-shares", "host-masks") else {})},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
                      "traffic": load_traffic(args.workload, n, "tiles")[0]
@@ -672,7 +760,7 @@ def run_aux(args, dev):
                    "bytes_per_record": rec_bytes},
         "file_GBps": (n * 3200 * args.steps / elapsed / 1e9) if args.workload == "load" else None,
         "host_input_GBps": (n * rec_bytes * args.steps / elapsed / 1e9)
-        if args.workload in ("host-shares", "host-masks") else None,
+        if args.workload in ("host-shares", "host-masks") and not args.attached else None,
         "cpu_baseline": cpu,
         "check": check,
         **extra,
@@ -689,37 +777,54 @@ def main():
     args = parse()
     if args.gpus < 1:
         raise SystemExit("error: --gpus must be >= 1")
-    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1 and not args.single_process:
         sys.exit(launch_ranks(args))
-    dist, world, rank, ordinal, backend, xdev = init_ranks(args)
+    ranks = Ranks(args)
     if args.dry_run:
-        return dry_run(args, dist, world, rank, backend)
-    if dist is not None:
-        import iris_dist
-
+        return dry_run(args, ranks)
+    world_gpus = args.gpus  # GPUs in the run (ranks x 1, or one process x --gpus)
+    rank = ranks.rank
     if args.n_per_gpu is None:  # configs[1] at N=1; configs[4] (100M over 8 GPUs) at N=8
-        args.n_per_gpu = 12_500_000 if (args.workload == "search" and world > 1) else 10_000_000
+        args.n_per_gpu = 12_500_000 if (args.workload == "search" and world_gpus > 1) else 10_000_000
     n = args.n_per_gpu
-    lo = rank * n
-    total = n * world
-    dev = ih.Device(ordinal)
+    total = n * world_gpus
     if args.workload in AUX_WORKLOADS:
-        if world > 1:
+        if world_gpus > 1:
             raise SystemExit(f"workload {args.workload} is a single-GPU line (run without --gpus / torchrun)")
-        return run_aux(args, dev)
+        return run_aux(args, ih.Device(0))
     if args.layout == "trits" and args.workload != "search":
         raise SystemExit("--layout trits is the search-only template layout (--workload search)")
+    if args.single_process and args.workload not in ("search", "batch"):
+        raise SystemExit("--single-process runs the group search (--workload search / batch)")
     layout = {"tiles": ih.LAYOUT_TILES, "lanes": ih.LAYOUT_LANES, "trits": ih.LAYOUT_TRITS}[args.layout]
     kind = {"search": ih.KIND_TEMPLATES, "batch": ih.KIND_TEMPLATES, "masks": ih.KIND_MASKS,
             "shares": ih.KIND_SHARES}[args.workload]
-    db = ih.Database(dev, kind, n, layout)
+    nq = args.queries if args.workload == "batch" else 1
+
+    # the library device group: the search / batch exchange of every multi-GPU run (RCCL)
+    group = ranks.join_group(args) if args.workload in ("search", "batch") else None
+    if group is not None:
+        devs = group.devices
+    else:
+        devs = [ih.Device(ranks.ordinal)]
+    dev = devs[0]
+    lo = rank * n  # this process's first global record (torchrun ranks; 0 for a single process)
+
     t0 = time.time()
-    db.generate(n, SEED, global_index0=lo)
+    if group is not None:
+        gdb = ih.GroupDatabase(group, kind, total, layout)
+        gdb.generate(SEED)
+        shards = [gdb.shard_db(i) for i in range(gdb.local_shards)]
+        shard_lo = [gdb.shard(i)[0] for i in range(gdb.local_shards)]
+    else:
+        gdb = None
+        db = ih.Database(dev, kind, n, layout)
+        db.generate(n, SEED, global_index0=lo)
+        shards, shard_lo = [db], [lo]
     gen_s = time.time() - t0
 
     query = gen_records(dev, ih.KIND_TEMPLATES, 1, SEED + 1)[0]
     out_dev = None
-    nq = args.queries if args.workload == "batch" else 1
     # planted known answers: (query index, global index, rotation)
     plants = []
     if args.workload == "search":
@@ -731,53 +836,74 @@ def main():
         rots = [9, -15, 15, 0, -7]
         plants = [(q, site, rots[k % len(rots)]) for k, (q, site) in enumerate(zip(pq, plant_sites(total, len(pq))))]
     for q, site, r in plants:
-        if lo <= site < lo + n:
-            src = query if args.workload == "search" else batch_q[q]
-            db.write(site - lo, planted_record(src, r)[None, :])
+        rec = planted_record(query if args.workload == "search" else batch_q[q], r)[None, :]
+        if gdb is not None:
+            gdb.write(site, rec)  # every rank writes the part it holds (SPMD)
+        elif lo <= site < lo + n:
+            db.write(site - lo, rec)
     if args.workload in ("masks", "shares"):
         out_dev = dev.alloc(n * ROT * 2)
     share_query = ih.encode(ih.Template.from_array(query)) if args.workload == "shares" else None
 
-    def new_engine():
+    def new_engine(d=dev):
         """The query's engine: its 31 rotations in the kernels' layouts, built on the device
         (DistanceEngine::new / MasksEngine::new, src/lib.rs:33-40, 60-67)."""
         if args.workload == "search":
-            return ih.TemplateEngine(dev, query)
+            return ih.TemplateEngine(d, query)
         if args.workload == "batch":
-            return ih.TemplateBatchEngine(dev, batch_q)
+            return ih.TemplateBatchEngine(d, batch_q)
         if args.workload == "masks":
-            return ih.MasksEngine(dev, query[200:])
-        return ih.DistanceEngine(dev, share_query)
+            return ih.MasksEngine(d, query[200:])
+        return ih.DistanceEngine(d, share_query)
 
     # by default every step prepares its query's engine and frees it again, as the reference's
-    # participant does per request (src/main.rs:427-431); --reuse-engine keeps one engine
-    eng = new_engine() if args.reuse_engine else None
+    # participant does per request (src/main.rs:427-431); --reuse-engine keeps one engine (the
+    # group search always builds its engines inside the step)
+    eng = new_engine() if args.reuse_engine and group is None else None
+    # IRIS_DIST_BACKEND=gloo: the search winners go through torch CPU tensors
+    rehearsal = ranks.dist is not None and group is None and args.workload in ("search", "batch")
+    if rehearsal:
+        import iris_dist
 
     def sync_all():
-        if dist is not None:
-            import torch
+        for d in devs:
+            d.synchronize()
+        ranks.barrier()
+        for d in devs:
+            d.synchronize()
 
-            torch.cuda.synchronize()
-            dist.barrier()
-            torch.cuda.synchronize()
-        else:
-            dev.synchronize()
+    def local_step():
+        """This process's shards searched with no exchange (the pre-warm: ranks run
+        different numbers of these, so no collective may be inside)."""
+        if args.workload in ("search", "batch") and group is not None:
+            engs = [new_engine(s.device) for s in shards]
+            try:
+                if args.workload == "search":
+                    pend = [e.search_async(s, index_base=b) for e, s, b in zip(engs, shards, shard_lo)]
+                    for p in pend:
+                        p.wait()
+                else:
+                    for e, s, b in zip(engs, shards, shard_lo):
+                        e.search(s, index_base=b)
+            finally:
+                for e in engs:
+                    e.close()
+            return
+        step(exchange=False)
 
     def step(exchange=True):
+        if group is not None:
+            return gdb.search(query) if args.workload == "search" else gdb.batch_search(batch_q)
         e = eng if eng is not None else new_engine()
         try:
             if args.workload == "batch":
                 ms = e.search(db, index_base=lo)
-                if dist is not None and exchange:
-                    ms = iris_dist.allgather_merge_many(ms, device=xdev)
-                return ms
+                return iris_dist.allgather_merge_many(ms) if rehearsal and exchange else ms
             if args.workload != "search":
                 e.batch_process_device(db, out_dev)  # [n][31] u16 left in HBM
                 return None
             m = e.search(db, index_base=lo)
-            if dist is not None and exchange:
-                m = iris_dist.allgather_merge(m, device=xdev)
-            return m
+            return iris_dist.allgather_merge(m) if rehearsal and exchange else m
         finally:
             if eng is None:
                 e.close()
@@ -785,10 +911,10 @@ def main():
     pipelined = args.workload == "search" and not args.no_pipeline
 
     def run_steps(k):
-        """k steps; pipelined: step i+1's query engine and search are enqueued before step i's
-        result is waited for and (N > 1) all-gathered, so the exchange and the host work of a
-        step overlap the next step's kernel.  Every step's search runs to completion and every
-        result is exchanged and merged inside the call."""
+        """k steps; pipelined: step i+1's search (engines, kernels and — in a group — the
+        RCCL all-gather and merge) is enqueued before step i's result is waited for, so the
+        host work and the exchange overlap the next kernel.  Every step's search runs to
+        completion and every result is exchanged and merged inside the call."""
         if not pipelined:
             m = None
             for _ in range(k):
@@ -797,63 +923,52 @@ def main():
 
         def finish(p):
             m = p.wait()
-            return iris_dist.allgather_merge(m, device=xdev) if dist is not None else m
+            return iris_dist.allgather_merge(m) if rehearsal else m
 
         pend, m = None, None
         for _ in range(k):
-            e = eng if eng is not None else new_engine()
-            p = e.search_async(db, index_base=lo)
-            if eng is None:
-                e.close()
+            if group is not None:
+                p = gdb.search_async(query)
+            else:
+                e = eng if eng is not None else new_engine()
+                p = e.search_async(db, index_base=lo)
+                if eng is None:
+                    e.close()
             if pend is not None:
                 m = finish(pend)
             pend = p
         return finish(pend) if pend is not None else m
 
+    # the CPU baseline (rank 0 of a one-GPU run): measured on its own, before any GPU step,
+    # on every CPU the process may use (not beside the GPU-driving loop)
+    cpu = None
+    if rank == 0 and world_gpus == 1 and not args.no_cpu_baseline:
+        try:
+            cpu = cpu_baseline(args)
+        except Exception as ex:  # reported, never fatal
+            cpu = {"value": None, "error": str(ex)}
     # pre-warm: the GPU needs ~0.5-1 s of sustained streaming before the search reaches its
     # steady rate (tools/engine_variance.py: the first ~100 searches of a process run up to 4 %
     # slower, then settle); untimed, like the warmup steps, and reported under "setup"
-    # local searches only: ranks run different numbers of them, so no collective may be inside
-    # the CPU baseline (rank 0 of a one-rank run) is measured beside the pre-warm, on all but one
-    # of the CPUs (the other drives the GPU), so the run's CPU leg and its GPU load overlap; the
-    # timed steps start after both
-    cpu_box = {}
-    cpu_thread = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        import threading
-
-        def _cpu_leg():
-            try:
-                cpu_box["cpu"] = cpu_baseline(args, reserve=1)
-            except Exception as ex:  # reported, never fatal
-                cpu_box["cpu"] = {"value": None, "error": str(ex)}
-
-        cpu_thread = threading.Thread(target=_cpu_leg, daemon=True)
-        cpu_thread.start()
     t_pre = time.perf_counter()
     prewarm_steps = 0
-    while time.perf_counter() - t_pre < args.prewarm_s or (cpu_thread is not None and cpu_thread.is_alive()):
-        step(exchange=False)
+    while time.perf_counter() - t_pre < args.prewarm_s:
+        local_step()
         prewarm_steps += 1
-    if cpu_thread is not None:
-        cpu_thread.join()
     prewarm_s = time.perf_counter() - t_pre
     if args.warmup:
         m = run_steps(args.warmup)
-    dev.reset_stats()
-    dev.set_profiling(True)
+    for d in devs:
+        d.reset_stats()
+        d.set_profiling(True)
     sync_all()
     t0 = time.perf_counter()
     m = run_steps(args.steps)
     sync_all()
     elapsed = time.perf_counter() - t0
-    dev.set_profiling(False)
-    if dist is not None:
-        import torch
-
-        t = torch.tensor([elapsed], dtype=torch.float64, device=xdev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    for d in devs:
+        d.set_profiling(False)
+    elapsed = ranks.max_over_ranks(elapsed)
 
     kname = {"search": "template_search", "batch": "template_batch", "masks": "masks", "shares": "shares"}[args.workload]
     rec_bytes = {"search": BYTES_PER_TEMPLATE if args.layout != "trits" else TRITS_BYTES_PER_TEMPLATE,
@@ -879,30 +994,37 @@ def main():
         ok = bool((full[sample] == want).all())
         check = {"sampled_outputs_checked": 64, "ok": bool(ok)}
         del full
-    launches, kms, items = dev.kernel_stats(kname)
-    if launches == 0 and args.workload == "batch":  # a one-query batch runs the single-query search
-        launches, kms, items = dev.kernel_stats("template_search")
-    _, rms, _ = dev.kernel_stats("reduce")
+    # kernel time per launch: averaged over this process's devices (each searches its own shards)
+    stats = [d.kernel_stats(kname) for d in devs]
+    if sum(s[0] for s in stats) == 0 and args.workload == "batch":  # a 1-3 query batch streams
+        stats = [d.kernel_stats("template_search") for d in devs]
+    launches = sum(s[0] for s in stats)
+    kms = sum(s[1] for s in stats)
+    rms = sum(d.kernel_stats("reduce")[1] for d in devs)
     avg_ms = kms / max(1, launches)
-    # kernel time of one step (a batch of 1-2 queries runs as streaming passes: several launches per step)
-    step_kernel_ms = kms / max(1, args.steps)
-    achieved = rec_bytes * n / (avg_ms * 1e-3) / 1e9
+    per_dev_ms = [s[1] / max(1, s[0]) for s in stats]
+    n_launch = total // world_gpus  # records per launch (one shard per device)
+    # kernel time of one step on one device (a batch of 1-3 queries streams: several launches per step)
+    step_kernel_ms = kms / max(1, len(devs)) / max(1, args.steps)
+    achieved = rec_bytes * n_launch / (avg_ms * 1e-3) / 1e9
     # batch: HBM bytes of the 1024-query launch (the DB once per XCD-shared pass + query tiles)
-    traffic, traffic_src = (load_traffic(args.workload, n, args.layout)
+    traffic, traffic_src = (load_traffic(args.workload, n_launch, args.layout)
                             if args.workload != "batch" or nq == 1024 else (None, None))
     ms_per_step = elapsed / args.steps * 1e3
     value = ROT * total * nq / (elapsed / args.steps)
+    mfma_frac = MFMA_MACS_PER_TEMPLATE * n_launch * nq / (step_kernel_ms * 1e-3) / FP4_DENSE_PEAK_MACS
 
     if rank == 0:
-        cpu = cpu_box.get("cpu")
         line = {
             "metric": METRIC,
             "value": value,
             "unit": "template comparisons/s",
-            "n_gpus": world,
-            "ranks_seen": dist.get_world_size() if dist is not None else 1,
-            "backend": backend,
-            "launcher": launcher_name(),
+            "value_per_gpu": value / world_gpus,
+            "n_gpus": world_gpus,
+            "ranks_seen": ranks.dist.get_world_size() if ranks.dist is not None else 1,
+            "processes": ranks.world,
+            "backend": ranks.backend,
+            "launcher": launcher_name() if not args.single_process else "none (one process, library device group)",
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
@@ -917,15 +1039,19 @@ def main():
             "data": "synthetic (on-device counter-based generator, uniform random pattern+mask bits; planted known answer)",
             "config": {
                 "workload": {
-                    "search": "1 query x 31 rotations x N templates, Template masked Hamming + fused min/argmin (BASELINE configs[1] at N=1: 10M; 12.5M per GPU from 2 ranks, configs[4] = 100M over 8 GPUs)",
+                    "search": "1 query x 31 rotations x N templates, Template masked Hamming + fused min/argmin (BASELINE configs[1] at N=1: 10M; 12.5M per GPU from 2 GPUs, configs[4] = 100M over 8 GPUs)",
                     "masks": "MasksEngine: 1 query mask x 31 rotations x N masks, [u16;31] denominators left in HBM",
                     "shares": "DistanceEngine: 1 encoded query x 31 rotations x N u16 shares, [u16;31] left in HBM (BASELINE configs[3])",
                     "batch": f"{nq} queries x 31 rotations x N templates in one pass, per-query min/argmin (BASELINE configs[2])",
                 }[args.workload],
                 "templates_per_gpu": n, "total_templates": total, "queries": nq, "rotations": ROT,
-                "bytes_per_template": rec_bytes, "parallelism": f"db-shard x{world}", "layout": args.layout,
-                "engine_per_step": not args.reuse_engine,
+                "bytes_per_template": rec_bytes, "parallelism": f"db-shard x{world_gpus}", "layout": args.layout,
+                "engine_per_step": not args.reuse_engine or group is not None,
                 "pipelined": pipelined,
+                "exchange": ("library RCCL all-gather of 24-B shard winners + on-device merge (iris_group_*)"
+                             if group is not None else
+                             "torch gloo all-gather of 32-B matches + iris_match_merge (rehearsal)"
+                             if rehearsal else None),
             },
             "roofline": ({
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -933,10 +1059,11 @@ def main():
                 "traffic_source": ("committed PMC bytes per record (profiles/" + traffic_src + "), scaled to this launch")
                 if traffic_src else None,
             } if args.workload != "batch" else {
-                # compute-bound: fp4 MFMA FLOPs (2 per MAC) of the den + encode products
-                "bound": "mfma", "achieved": 2 * MFMA_MACS_PER_TEMPLATE * n * nq / (step_kernel_ms * 1e-3) / 1e12,
+                # compute-bound: fp4 MFMA FLOPs (2 per MAC) of the den + encode products, 31 rotation rows
+                "bound": "mfma", "achieved": 2 * MFMA_MACS_PER_TEMPLATE * n_launch * nq / (step_kernel_ms * 1e-3) / 1e12,
                 "peak": 2 * FP4_DENSE_PEAK_MACS / 1e12, "unit": "TFLOP/s",
-                "frac": MFMA_MACS_PER_TEMPLATE * n * nq / (step_kernel_ms * 1e-3) / FP4_DENSE_PEAK_MACS,
+                "frac": mfma_frac,
+                "issued_frac": mfma_frac * MFMA_MACS_ISSUED_PER_TEMPLATE / MFMA_MACS_PER_TEMPLATE,
                 "traffic": traffic,
                 "traffic_source": ("committed PMC bytes per launch (profiles/" + traffic_src + ")")
                 if traffic_src else None,
@@ -950,14 +1077,13 @@ def main():
                          ("shares", "lanes"): "shares_kernel (VALU v_pk_mad_u16)",
                          ("search", "trits"): "trits_mfma_kernel<TR_SEARCH> (fp4 MFMA, 3-state bytes decoded via LDS table)",
                          ("batch", "tiles"): "batch_lds_kernel (fp4 MFMA GEMM, LDS query-fragment ring)"}[(args.workload, args.layout)],
-                "avg_ms": avg_ms, "launches": launches,
+                "avg_ms": avg_ms, "launches": launches, "per_device_avg_ms": per_dev_ms,
                 "reduce_avg_ms": rms / max(1, launches),
                 "frac_of_guide_copy_bw": achieved / HBM_GUIDE_COPY_GBS,
                 "frac_of_read_ceiling": achieved / HBM_READ_CEILING_GBS,
-                "valu_int_frac": (VALU_OPS_PER_TEMPLATE * n / (avg_ms * 1e-3) / VALU_INT_PEAK_OPS
+                "valu_int_frac": (VALU_OPS_PER_TEMPLATE * n_launch / (avg_ms * 1e-3) / VALU_INT_PEAK_OPS
                                   if args.layout == "lanes" and args.workload == "search" else None),
-                "mfma_fp4_frac": (MFMA_MACS_PER_TEMPLATE * n * nq / (step_kernel_ms * 1e-3) / FP4_DENSE_PEAK_MACS
-                                  if args.layout != "lanes" and args.workload in ("search", "batch") else None),
+                "mfma_fp4_frac": mfma_frac if args.layout != "lanes" and args.workload in ("search", "batch") else None,
                 "traffic_note": ("FETCH_SIZE counts every L2 miss, Infinity-Cache hits included: the query tiles "
                                  "are re-streamed from the 256-MB MALL for each N-group, "
                                  "the template DB comes from HBM about once per XCD" if args.workload == "batch"
@@ -973,10 +1099,12 @@ def main():
         dev.free(out_dev)
     if eng is not None:
         eng.close()
-    db.close()
-    dev.close()
-    if dist is not None:
-        dist.destroy_process_group()
+    if gdb is not None:
+        gdb.close()
+    else:
+        db.close()
+        dev.close()
+    ranks.close()
     if not ok:
         print(f"result check failed: {check}", file=sys.stderr)
         sys.exit(3)

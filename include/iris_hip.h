@@ -147,6 +147,23 @@ int iris_db_clear(iris_db_t *db);
 /* Drops the records [len, current length) (no device work; later appends overwrite them). */
 int iris_db_truncate(iris_db_t *db, uint64_t len);
 
+/* ---------------------------------------------------------------- host residency
+ * The reference's participant and resolver mmap their record file once and
+ * call batch_process(out, chunk) on 20 000-record slices of the mapping
+ * (src/main.rs:389-391, 426-431; 458-460, 511-516).  iris_db_attach_host
+ * declares that db's records [0, n) are the n records of the host array at
+ * `host` (e.g. that mapping): with upload != 0 the (empty) database receives
+ * them now; with upload == 0 it must already hold exactly them (e.g. loaded
+ * from the same file with iris_db_load_file; the first, middle and last
+ * record are compared).  From then on iris_engine_batch_process_host on any
+ * record range inside the array (same kind, whole records) runs the engine on
+ * the resident copy and uploads nothing; other slices still upload.  The host
+ * array must stay unchanged while attached; any write to the database
+ * (append, write, generate, clear, truncate, load, prepare) or its
+ * destruction detaches it.  TILES / LANES databases (not TRITS). */
+int iris_db_attach_host(iris_db_t *db, const void *host, uint64_t n, int upload);
+int iris_db_detach_host(iris_db_t *db);
+
 /* ---------------------------------------------------------------- on-disk formats
  * Record files hold the raw little-endian bytes of a record slice
  * (bytemuck::bytes_of): `prepare` writes them and `participant` / `resolver`
@@ -164,7 +181,8 @@ int iris_db_truncate(iris_db_t *db, uint64_t len);
  * try_cast_slice does ("Share file … invalid.", src/main.rs:390-393,459-462). */
 int iris_db_load_file(iris_db_t *db, const char *path, uint64_t first, uint64_t count, uint64_t *loaded);
 /* Writes records [first, first+n) of db to `path` (created / truncated) in
- * the same raw format. */
+ * the same raw format.  A TRITS database is refused (IRIS_E_ARG): it keeps only
+ * pattern & mask, so the file would differ from what was loaded. */
 int iris_db_save_file(const iris_db_t *db, const char *path, uint64_t first, uint64_t n);
 /* JSON template files: a top-level array of {"pattern": hex, "mask": hex}
  * objects, each Bits the hex of its 1600 LE bytes (serde form of Template,
@@ -217,7 +235,9 @@ int iris_engine_batch_process(iris_engine_t *engine, const iris_db_t *db, uint64
 int iris_engine_batch_process_device(iris_engine_t *engine, const iris_db_t *db, uint64_t first, uint64_t n,
                                      uint16_t *out_device);
 /* Host-slice form with exactly the reference signature: `db` is a host array
- * of n reference-layout records, `out` a host array of n*31 uint16_t. */
+ * of n reference-layout records, `out` a host array of n*31 uint16_t.  A slice
+ * of an attached host array (iris_db_attach_host) runs on the resident copy;
+ * any other slice is uploaded (PCIe) and packed first. */
 int iris_engine_batch_process_host(iris_engine_t *engine, const void *db, uint64_t n, uint16_t *out);
 
 /* Template engine, per template and rotation k: num = popcount((qp^ep)&qm&em),
@@ -318,6 +338,84 @@ int iris_host_query_tables(int kind, const void *query, uint32_t nq, void *tab, 
 /* Merges per-shard search results into the global one (min fraction, then
  * lowest index) — the cross-shard step of the resolver's argmin (src/main.rs:616-621). */
 int iris_match_merge(const iris_match_t *records, uint64_t count, iris_match_t *out);
+
+/* ------------------------------------------------------- device groups (multi-GPU)
+ * The reference fans a query out to its participants and folds their answers
+ * with a sequential strict-< minimum (src/main.rs:486-504, 616-621).  Here a
+ * template database is split into contiguous shards across the gfx950 devices
+ * of a group — shard s of S holds global records [s*N/S, (s+1)*N/S) — every
+ * device searches its own shards with no data-path communication, and the
+ * per-shard winners (24 B each, global indices) are exchanged with one RCCL
+ * ncclAllGather over xGMI (librccl from /opt/rocm) and merged on every device
+ * (exact fraction, then the lowest global index).
+ *
+ * Two ways to form a group:
+ *  - iris_group_create: ONE process drives `n` devices (ncclCommInitAll).
+ *  - iris_group_create_rank: one device per process (e.g. a torchrun rank):
+ *    rank 0 calls iris_group_unique_id and hands the 128 id bytes to every
+ *    rank (any side channel); each rank then calls iris_group_create_rank with
+ *    the same id (ncclCommInitRank).  Every rank makes the same group calls
+ *    (SPMD); each holds and fills only its own shards.
+ * Group calls are blocking and serialised per group, like the device calls. */
+#define IRIS_GROUP_ID_BYTES 128
+typedef struct iris_group iris_group_t;
+typedef struct iris_group_db iris_group_db_t;
+typedef struct iris_group_pending iris_group_pending_t;
+
+int iris_group_create(const int *ordinals, uint32_t n, iris_group_t **out);
+int iris_group_unique_id(uint8_t id[IRIS_GROUP_ID_BYTES]);
+int iris_group_create_rank(int ordinal, uint32_t nranks, uint32_t rank, const uint8_t id[IRIS_GROUP_ID_BYTES],
+                           iris_group_t **out);
+int iris_group_destroy(iris_group_t *group);
+/* local_devices: devices this process drives; ranks: RCCL ranks in the group
+ * (all processes); first_rank: the rank of local device 0. */
+int iris_group_info(const iris_group_t *group, uint32_t *local_devices, uint32_t *ranks, uint32_t *first_rank);
+/* Local device i of the group (borrowed: valid until iris_group_destroy), e.g.
+ * for iris_device_set_profiling / iris_device_kernel_stats. */
+int iris_group_device(const iris_group_t *group, uint32_t i, iris_device_t **dev);
+
+/* A sharded database of `total` records of `kind` over the whole group:
+ * S = ranks * shards_per_device contiguous shards (shards_per_device >= 1;
+ * more than one splits a device's range into several shards, each searched
+ * and exchanged separately).  Every record starts empty (a zero mask: never a
+ * candidate, as the reference's NaN rows, src/lib.rs:105-106).  layout as
+ * iris_db_create_ex.  A process holds the shards of its local devices. */
+int iris_group_db_create(iris_group_t *group, int kind, uint64_t total, int layout, uint32_t shards_per_device,
+                         iris_group_db_t **out);
+int iris_group_db_destroy(iris_group_db_t *gdb);
+/* total records; S = shards in the group; the local shards are [first_shard, first_shard + local_shards). */
+int iris_group_db_info(const iris_group_db_t *gdb, uint64_t *total, uint32_t *shards, uint32_t *first_shard,
+                       uint32_t *local_shards);
+/* Local shard i (0 <= i < local_shards): its database (borrowed; searchable with
+ * the single-device calls) and the global index of its record 0. */
+int iris_group_db_shard(const iris_group_db_t *gdb, uint32_t i, iris_db_t **db, uint64_t *first, uint64_t *count);
+/* Fills every local shard with the synthetic records of iris_db_generate
+ * (generator index = global index), all local devices in parallel. */
+int iris_group_db_generate(iris_group_db_t *gdb, uint64_t seed);
+/* records = host records of the global range [index, index+n) (reference
+ * layout); the part held by this process's shards is written. */
+int iris_group_db_write(iris_group_db_t *gdb, uint64_t index, const void *records, uint64_t n);
+/* Reads the global range [index, index+n) back; it must lie in local shards. */
+int iris_group_db_read(const iris_group_db_t *gdb, uint64_t index, uint64_t n, void *records);
+/* Global record i <- record first+i of a raw record file (iris_db_load_file's
+ * formats and DMA path), local shards only, all local devices in parallel; the
+ * file must hold first + total records (IRIS_E_RANGE otherwise). */
+int iris_group_db_load_file(iris_group_db_t *gdb, const char *path, uint64_t first);
+
+/* 1 query against the whole sharded template database: on every device the
+ * query's engine is built, each local shard searched, the winners all-gathered
+ * over RCCL and merged; *out = the global (min distance, lowest index) as
+ * iris_template_search over the concatenated database (index = global). */
+int iris_group_template_search(iris_group_db_t *gdb, const iris_template_t *query, iris_match_t *out);
+/* Pipelined form: enqueues the search, the exchange and the merge, returns at
+ * once; wait blocks for THAT search and frees the handle (every local device
+ * must agree on the merged winner, IRIS_E_HIP otherwise). */
+int iris_group_template_search_async(iris_group_db_t *gdb, const iris_template_t *query, iris_group_pending_t **out);
+int iris_group_pending_wait(iris_group_pending_t *pending, iris_match_t *out);
+/* nq queries in one pass per shard (iris_template_batch_search rules: TILES
+ * layout for nq > 3); out[q] = query q's global winner. */
+int iris_group_template_batch_search(iris_group_db_t *gdb, const iris_template_t *queries, uint32_t nq,
+                                     iris_match_t *out);
 
 #ifdef __cplusplus
 }

@@ -28,6 +28,7 @@ namespace {
 
 int db_write_locked(iris_db *db, uint64_t index, const void *records, uint64_t n) {
     iris_device *d = db->dev;
+    db_detach(db);
     if (index > db->len) return fail(IRIS_E_RANGE, "iris_db_write: index beyond the end of the database");
     if (n > db->cap - index) return fail(IRIS_E_RANGE, "iris_db_write: database capacity exceeded");
     if (n == 0) return 0;
@@ -128,7 +129,9 @@ int qbuf_take(iris_device *d, size_t bytes, void **p, size_t *got) {
     return 0;
 }
 
-void engine_free(iris_engine *e) {
+}  // namespace
+
+void iris_api::engine_free(iris_engine *e) {
     if (!e) return;
     for (iris_engine *c : e->sub) engine_free(c);
     if (e->qbuf) {
@@ -139,6 +142,8 @@ void engine_free(iris_engine *e) {
     }
     delete e;
 }
+
+namespace {
 
 // A new engine whose query buffer holds [table | fragments | extra] (each 256-B aligned).
 int engine_alloc(iris_device *dev, int kind, size_t tab_bytes, size_t frag_bytes, size_t extra_bytes,
@@ -238,10 +243,14 @@ void device_teardown(iris_device *d) {
     delete d;
 }
 
-inline void device_retain(iris_device *d) { d->refs.fetch_add(1, std::memory_order_relaxed); }
-inline void device_release(iris_device *d) {
+}  // namespace
+
+void iris_api::device_retain(iris_device *d) { d->refs.fetch_add(1, std::memory_order_relaxed); }
+void iris_api::device_release(iris_device *d) {
     if (d->refs.fetch_sub(1, std::memory_order_acq_rel) == 1) device_teardown(d);
 }
+
+namespace {
 
 constexpr size_t kMaskFragBytes = kMaskFragUint4 * 16;
 constexpr size_t kShareFragBytes = kShareFragUint4 * 16 + 32 * 8;
@@ -259,7 +268,15 @@ double rust_f64_min(double a, double b) {
 extern "C" {
 
 const char *iris_last_error(void) { return g_err.c_str(); }
-const char *iris_version(void) { return "iris-hip 0.1.0 (gfx950)"; }
+#ifndef IRIS_BUILD_KNOBS
+#define IRIS_BUILD_KNOBS ""
+#endif
+// "iris-hip X (gfx950)", plus " knobs: -DIRIS_..." when the build set compile-time knobs
+const char *iris_version(void) {
+    static const std::string v = std::string("iris-hip 0.3.0 (gfx950)") +
+                                 (sizeof(IRIS_BUILD_KNOBS) > 1 ? std::string(" knobs: ") + IRIS_BUILD_KNOBS : std::string());
+    return v.c_str();
+}
 
 int iris_device_count(int *count) {
     ARG(count, "count is NULL");
@@ -435,6 +452,7 @@ int iris_db_destroy(iris_db_t *db) {
         std::lock_guard<std::recursive_mutex> g(d->mu);
         (void)hipSetDevice(d->ordinal);
         (void)hipStreamSynchronize(d->stream);
+        db_detach(db);
         if (db->data) (void)hipFree(db->data);
     }
     delete db;
@@ -502,6 +520,7 @@ int iris_db_generate(iris_db_t *db, uint64_t n, uint64_t seed, uint64_t global_i
     CHK(set_device(d));
     if (n > db->cap - db->len) return fail(IRIS_E_RANGE, "iris_db_generate: database capacity exceeded");
     if (n == 0) return 0;
+    db_detach(db);
     CHK(timed(d, "generate", n, [&] { return launch_generate(d->stream, db->k, db->data, db->len, n, seed, global_index0); }));
     CHK(sync(d));
     db->len += n;
@@ -512,7 +531,45 @@ int iris_db_truncate(iris_db_t *db, uint64_t len) {
     ARG(db, "database is NULL");
     std::lock_guard<std::recursive_mutex> g(db->dev->mu);
     if (len > db->len) return fail(IRIS_E_RANGE, "iris_db_truncate: len beyond the current length");
+    if (len != db->len) db_detach(db);
     db->len = len;
+    return 0;
+}
+
+int iris_db_attach_host(iris_db_t *db, const void *host, uint64_t n, int upload) {
+    ARG(db && (host || n == 0), "NULL argument");
+    ARG(db->k.layout != IRIS_LAYOUT_TRITS, "a TRITS database does not hold the records exactly (search-only layout)");
+    iris_device *d = db->dev;
+    std::lock_guard<std::recursive_mutex> g(d->mu);
+    CHK(set_device(d));
+    db_detach(db);
+    const size_t rb = db->k.rec_bytes;
+    if (upload) {
+        ARG(db->len == 0, "iris_db_attach_host(upload): the database must be empty");
+        CHK(db_write_locked(db, 0, host, n));
+    } else {
+        ARG(db->len == n, "iris_db_attach_host: the database must hold exactly the n records of the host array");
+        // the caller's promise (e.g. the same file loaded with iris_db_load_file) is spot-checked
+        const uint64_t probe[3] = {0, n / 2, n ? n - 1 : 0};
+        std::vector<char> rec(rb);
+        for (int i = 0; i < 3 && n; ++i) {
+            CHK(iris_db_read(db, probe[i], 1, rec.data()));
+            if (memcmp(rec.data(), (const char *)host + probe[i] * rb, rb) != 0)
+                return fail(IRIS_E_ARG, "iris_db_attach_host: record " + std::to_string(probe[i]) +
+                                            " of the database differs from the host array");
+        }
+    }
+    if (n == 0) return 0;
+    db->host_base = (uintptr_t)host;
+    db->host_n = n;
+    d->attached.push_back(db);
+    return 0;
+}
+
+int iris_db_detach_host(iris_db_t *db) {
+    ARG(db, "database is NULL");
+    std::lock_guard<std::recursive_mutex> g(db->dev->mu);
+    db_detach(db);
     return 0;
 }
 
@@ -520,6 +577,7 @@ int iris_db_clear(iris_db_t *db) {
     ARG(db, "database is NULL");
     std::lock_guard<std::recursive_mutex> g(db->dev->mu);
     CHK(set_device(db->dev));
+    db_detach(db);
     const size_t bytes = std::max<uint64_t>(1, db->cap / db->k.block) * block_bytes(db->k);
     HIPCHK(hipMemsetAsync(db->data, 0, bytes, db->dev->stream));
     CHK(sync(db->dev));
@@ -549,8 +607,9 @@ int iris_distance_engine_new(iris_device_t *d, const uint16_t query[IRIS_BITS], 
     return 0;
 }
 
-namespace {
-int template_engine_locked(iris_device *d, const iris_template_t *query, iris_engine **out) {
+}  // extern "C"
+
+int iris_api::template_engine_locked(iris_device *d, const iris_template_t *query, iris_engine **out) {
     // [LANES table | TILES fragments | TRITS fragments], all built by one launch
     iris_engine *e = nullptr;
     void *tfrag = nullptr;
@@ -565,7 +624,8 @@ int template_engine_locked(iris_device *d, const iris_template_t *query, iris_en
     *out = e;
     return 0;
 }
-}  // namespace
+
+extern "C" {
 
 int iris_template_engine_new(iris_device_t *d, const iris_template_t *query, iris_engine_t **out) {
     ARG(d && query && out, "NULL argument");
@@ -642,6 +702,14 @@ int iris_engine_batch_process_host(iris_engine_t *e, const void *records, uint64
     if (n == 0) return 0;
     ARG(records && out, "NULL argument");
     const KindInfo k = kind_info(e->kind);
+    // a slice of an attached host array: run on its resident copy, nothing is uploaded
+    const uintptr_t p = (uintptr_t)records;
+    for (iris_db *a : d->attached) {
+        if (a->k.kind != e->kind || p < a->host_base) continue;
+        const uintptr_t off = p - a->host_base;
+        if (off % k.rec_bytes != 0 || off / k.rec_bytes > a->host_n || n > a->host_n - off / k.rec_bytes) continue;
+        return run_u16_engine(e, a, off / k.rec_bytes, n, out);
+    }
     const uint64_t ch = std::min<uint64_t>(n, 1ull << 20 >> (e->kind == IRIS_KIND_SHARES ? 4 : 0));
     TempDb t;
     CHK(temp_db(d, e->kind, ch, t));
@@ -698,8 +766,10 @@ int iris_template_counts(iris_engine_t *e, const iris_db_t *db, uint64_t first, 
 // `dst` (pinned host memory); nothing waits.  side = true (asynchronous
 // searches): the reduce runs on the side stream over one of two alternating
 // partials buffers, and `done` (if given) is recorded there after it.
-static int search_enqueue(iris_engine_t *e, const iris_db_t *db, uint64_t first, uint64_t n, double *dist_dev,
-                          Partial *dst, bool side = false, hipEvent_t done = nullptr) {
+}  // extern "C"
+
+int iris_api::search_enqueue(iris_engine_t *e, const iris_db_t *db, uint64_t first, uint64_t n, double *dist_dev,
+                             Partial *dst, bool side, hipEvent_t done, uint64_t idx_base) {
     iris_device *d = e->dev;
     if (n == 0) return 0;
     LaunchRange r{first, n};
@@ -711,7 +781,7 @@ static int search_enqueue(iris_engine_t *e, const iris_db_t *db, uint64_t first,
     DevBuf *buf = &d->partials;
     int b = 0;
     if (side) {
-        if (!d->aux) HIPCHK(hipStreamCreateWithFlags(&d->aux, hipStreamNonBlocking));
+        CHK(ensure_aux(d));
         b = d->apart_next;
         d->apart_next ^= 1;
         buf = &d->apart[b];
@@ -731,14 +801,16 @@ static int search_enqueue(iris_engine_t *e, const iris_db_t *db, uint64_t first,
         return launch_template_search(d->stream, db->data, e->qtab, r, dist_dev, part, &written);
     }));
     if (!side)  // the reduce writes the winner straight into pinned host memory: no copy before the wait
-        return timed(d, "reduce", written, [&] { return launch_reduce(d->stream, part, written, dst); });
+        return timed(d, "reduce", written, [&] { return launch_reduce(d->stream, part, written, dst, idx_base); });
     HIPCHK(hipEventRecord(d->apart_written[b], d->stream));
     HIPCHK(hipStreamWaitEvent(d->aux, d->apart_written[b], 0));
-    CHK(timed(d, "reduce", written, [&] { return launch_reduce(d->aux, part, written, dst); }, d->aux));
+    CHK(timed(d, "reduce", written, [&] { return launch_reduce(d->aux, part, written, dst, idx_base); }, d->aux));
     HIPCHK(hipEventRecord(d->apart_read[b], d->aux));
     if (done) HIPCHK(hipEventRecord(done, d->aux));
     return 0;
 }
+
+extern "C" {
 
 static int search_locked(iris_engine_t *e, const iris_db_t *db, uint64_t first, uint64_t n, uint64_t index_base,
                          double *dist_dev, iris_match_t *out) {
@@ -824,7 +896,9 @@ int iris_template_search(iris_engine_t *e, const iris_db_t *db, uint64_t first, 
     return search_locked(e, db, first, n, index_base, dist_out_device, out);
 }
 
-static void match_from(const Partial &r, bool any, uint64_t base, iris_match_t *out) {
+}  // extern "C"
+
+void iris_api::match_from(const Partial &r, bool any, uint64_t base, iris_match_t *out) {
     if (!any || r.den == 0) {
         out->distance = INFINITY;
         out->index = UINT64_MAX;
@@ -840,6 +914,8 @@ static void match_from(const Partial &r, bool any, uint64_t base, iris_match_t *
     }
     out->reserved = 0;
 }
+
+extern "C" {
 
 struct iris_pending {
     iris_device *dev = nullptr;

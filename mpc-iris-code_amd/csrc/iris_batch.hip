@@ -303,7 +303,7 @@ __global__ void __launch_bounds__(64 * NW, NW <= 8 ? 8 / NW : 1)
 
 // one workgroup per query: reduce its G partials
 __global__ void __launch_bounds__(256) batch_reduce_kernel(const Partial *__restrict__ partials, uint32_t G,
-                                                           Partial *__restrict__ out) {
+                                                           Partial *__restrict__ out, uint64_t idx_base) {
     const uint32_t q = blockIdx.x;
     Partial c;
     c.num = 0;
@@ -327,6 +327,7 @@ __global__ void __launch_bounds__(256) batch_reduce_kernel(const Partial *__rest
         Partial b = sh[0];
         for (int i = 1; i < 4; ++i)
             if (partial_better_dev(sh[i], b)) b = sh[i];
+        if (b.den != 0) b.idx += idx_base;
         out[q] = b;
     }
 }
@@ -682,7 +683,7 @@ BatchGeometry batch_geometry(LaunchRange r, uint32_t nq) {
 }
 
 int launch_batch(void *stream, const void *db, const void *qtiles, LaunchRange r, const BatchGeometry &g,
-                 Partial *partials, Partial *out) {
+                 Partial *partials, Partial *out, uint64_t idx_base) {
     if (r.n == 0) return 0;
     const int kc = batch_kernel_choice();
     if (kc == 2)
@@ -694,7 +695,8 @@ int launch_batch(void *stream, const void *db, const void *qtiles, LaunchRange r
                            (const uint4 *)qtiles, g.tile0, g.ntiles, r.first, r.first + r.n, g.nqg, g.G, g.xqg,
                            partials);
     if (hipGetLastError() != hipSuccess) return -1;
-    hipLaunchKernelGGL(batch_reduce_kernel, dim3(g.nqg * BQ), dim3(256), 0, (hipStream_t)stream, partials, g.G, out);
+    hipLaunchKernelGGL(batch_reduce_kernel, dim3(g.nqg * BQ), dim3(256), 0, (hipStream_t)stream, partials, g.G, out,
+                       idx_base);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -87,6 +87,9 @@ struct iris_device {
     std::atomic<int> refs{1};
     // freed engines' query buffers, reused by later engines (stream-ordered)
     std::vector<std::pair<size_t, void *>> qpool;
+    // databases attached to a host array (iris_db_attach_host): host-slice engine calls
+    // on a range inside one of them run on the resident copy
+    std::vector<struct iris_db *> attached;
 };
 
 struct iris_db {
@@ -94,6 +97,9 @@ struct iris_db {
     KindInfo k{};
     uint64_t len = 0, cap = 0;
     void *data = nullptr;
+    // iris_db_attach_host: records [0, host_n) equal the host array at host_base
+    uintptr_t host_base = 0;
+    uint64_t host_n = 0;
 };
 
 struct iris_engine {
@@ -230,5 +236,34 @@ inline int check_kind(int kind) {
         return fail(IRIS_E_ARG, "unknown record kind");
     return 0;
 }
+
+// Any change to a database's records ends its host attachment (caller holds the device lock).
+inline void db_detach(iris_db *db) {
+    if (!db->host_base) return;
+    auto &v = db->dev->attached;
+    v.erase(std::remove(v.begin(), v.end(), db), v.end());
+    db->host_base = 0;
+    db->host_n = 0;
+}
+
+inline int ensure_aux(iris_device *d) {
+    if (!d->aux) HIPCHK(hipStreamCreateWithFlags(&d->aux, hipStreamNonBlocking));
+    return 0;
+}
+
+// Shared by the API translation units (defined in iris_api.hip).
+void device_retain(iris_device *d);
+void device_release(iris_device *d);  // tears the device down with its last handle
+void engine_free(iris_engine *e);     // query buffer back to the device's pool (stream-ordered)
+// single-query template engine (query passed by value to the build kernel); caller holds d->mu
+int template_engine_locked(iris_device *d, const iris_template_t *query, iris_engine **out);
+// Enqueues the search of [first, first+n) of db and its partials reduce; the winner (idx =
+// range-relative index + idx_base) lands in `dst` (pinned host or device memory); nothing
+// waits.  side = true: the reduce runs on the device's side stream over one of two
+// alternating partials buffers, and `done` (if given) is recorded there after it.
+int search_enqueue(iris_engine *e, const iris_db *db, uint64_t first, uint64_t n, double *dist_dev, iris::Partial *dst,
+                   bool side = false, hipEvent_t done = nullptr, uint64_t idx_base = 0);
+// Partial (indices offset by base) -> iris_match_t; +inf / UINT64_MAX when none
+void match_from(const iris::Partial &r, bool any, uint64_t base, iris_match_t *out);
 
 }  // namespace iris_api

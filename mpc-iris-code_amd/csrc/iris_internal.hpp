@@ -20,6 +20,16 @@
 #define IRIS_HD
 #endif
 
+// The shipped library (Makefile: LIB = libiris_hip.so) never carries a diagnostic knob:
+// those build kernels that drop work on purpose (tools/build_variant.sh variants only).
+#if defined(IRIS_SHIPPED_BUILD)
+#if (defined(IRIS_MFMA_DIAG) && IRIS_MFMA_DIAG) || (defined(IRIS_BATCH_DIAG) && IRIS_BATCH_DIAG) || \
+    (defined(IRIS_BATCH2_DIAG) && IRIS_BATCH2_DIAG) || (defined(IRIS_STORE_DIAG) && IRIS_STORE_DIAG) || \
+    (defined(IRIS_TRITS_DIAG) && IRIS_TRITS_DIAG)
+#error "diagnostic knob in the shipped libiris_hip.so"
+#endif
+#endif
+
 namespace iris {
 
 constexpr int kLanes = 64;            // records per block (= wavefront width)
@@ -295,14 +305,17 @@ struct BatchGeometry {
 BatchGeometry batch_geometry(LaunchRange r, uint32_t nq);
 uint32_t batch_query_group();  // queries per batch_kernel query group (padding unit)
 int launch_batch(void *stream, const void *db, const void *qtiles, LaunchRange r, const BatchGeometry &g,
-                 Partial *partials, Partial *out);
+                 Partial *partials, Partial *out, uint64_t idx_base = 0);
 int launch_resolver(void *stream, const uint16_t *const *shares, uint32_t parts, const uint16_t *denoms, uint64_t n,
                     double *dist_out, Partial *partials);
 size_t shares_workspace_bytes(LaunchRange r);  // > 0: launch_shares_mfma splits K over slices
 int launch_shares_mfma(void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *out, void *ws);
 int launch_template_search(void *stream, const void *db, const void *qtab, LaunchRange r, double *dist_out,
                            Partial *partials, uint32_t *n_partials);
-int launch_reduce(void *stream, Partial *partials, uint32_t n_partials, Partial *out);  // consumes partials
+// consumes partials; the winner's idx (range-relative) is offset by idx_base
+int launch_reduce(void *stream, Partial *partials, uint32_t n_partials, Partial *out, uint64_t idx_base = 0);
+// group search merge: out[q] = best of recv[s * stride + q], s < shards (indices already global)
+int launch_group_merge(void *stream, const Partial *recv, uint32_t shards, uint32_t nq, uint32_t stride, Partial *out);
 int launch_masks(void *stream, const void *db, const void *qtab, LaunchRange r, uint16_t *out);
 int launch_shares(void *stream, const void *db, const void *qtab, LaunchRange r, uint16_t *out);
 

@@ -120,6 +120,7 @@ int iris_db_load_file(iris_db_t *db, const char *path, uint64_t first, uint64_t 
     const uint64_t n = std::min<uint64_t>(count, total - first);
     if (n > db->cap - db->len) return fail(IRIS_E_RANGE, "iris_db_load_file: database capacity exceeded");
     if (n == 0) return 0;
+    db_detach(db);
 
     const uint64_t ch = std::max<uint64_t>(1, kIoChunkBytes / k.rec_bytes);
     const size_t chb = ch * k.rec_bytes;
@@ -226,6 +227,9 @@ int iris_db_load_file(iris_db_t *db, const char *path, uint64_t first, uint64_t 
 
 int iris_db_save_file(const iris_db_t *db, const char *path, uint64_t first, uint64_t n) {
     ARG(db && path, "NULL argument");
+    // TRITS keeps pattern & mask only: a saved file would silently differ from what was loaded
+    if (db->k.layout == IRIS_LAYOUT_TRITS)
+        return fail(IRIS_E_ARG, "iris_db_save_file: a TRITS database is a search-only layout (pattern bits under a zero mask are not stored)");
     iris_device *d = db->dev;
     std::lock_guard<std::recursive_mutex> g(d->mu);
     CHK(set_device(d));
@@ -456,6 +460,8 @@ extern "C" int iris_prepare_shares(const iris_db_t *templates, uint64_t first, u
     if (first > templates->len || n > templates->len - first)
         return fail(IRIS_E_RANGE, "record range outside the database");
     if (n == 0) return 0;
+    for (uint32_t j = 0; j < parties; ++j) db_detach(shares[j]);
+    if (masks) db_detach(masks);
     bool all_tiles = templates->k.layout == IRIS_LAYOUT_TILES && (!masks || masks->k.layout == IRIS_LAYOUT_TILES);
     for (uint32_t j = 0; j < parties; ++j) all_tiles &= shares[j]->k.layout == IRIS_LAYOUT_TILES;
     if (all_tiles) {  // one in-place launch: TILES templates -> TILES shares + masks

@@ -286,7 +286,7 @@ __global__ void __launch_bounds__(256, 8)
 // workgroup reads ~10 B/clk, so tens of thousands of partials (one per search
 // workgroup) first go through reduce_stage_kernel below.
 __global__ void __launch_bounds__(1024) reduce_kernel(const Partial *__restrict__ partials, uint32_t n,
-                                                      Partial *__restrict__ out, uint32_t stride = 1) {
+                                                      Partial *__restrict__ out, uint32_t stride, uint64_t idx_base) {
     Partial c;
     c.num = 0;
     c.den = 0;
@@ -307,8 +307,30 @@ __global__ void __launch_bounds__(1024) reduce_kernel(const Partial *__restrict_
         const int nw = (blockDim.x + 63) / 64;
         for (int w = 1; w < nw; ++w)
             if (better(sh[w], b)) b = sh[w];
+        if (b.den != 0) b.idx += idx_base;  // range-relative -> caller's index space
         *out = b;
     }
+}
+
+// Cross-shard merge of a group search (iris_group.hip): recv holds, for each of the S
+// shards (all ranks, all-gathered), nq winners with global indices at recv[s * stride + q];
+// thread q folds query q's S candidates (exact fraction, then lowest global index, the
+// resolver's strict-< scan, src/main.rs:616-621) into out[q].
+__global__ void __launch_bounds__(256) group_merge_kernel(const Partial *__restrict__ recv, uint32_t S, uint32_t nq,
+                                                          uint32_t stride, Partial *__restrict__ out) {
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= nq) return;
+    Partial c;
+    c.num = 0;
+    c.den = 0;
+    c.rot = 0;
+    c.pad = 0;
+    c.idx = ~0ull;
+    for (uint32_t s = 0; s < S; ++s) {
+        const Partial p = recv[(uint64_t)s * stride + q];
+        if (better(p, c)) c = p;
+    }
+    out[q] = c;
 }
 
 constexpr uint32_t kReduceChunk = 1024;  // partials per first-stage workgroup
@@ -490,16 +512,24 @@ int launch_template_search(void *stream, const void *db, const void *qtab, Launc
 }
 
 // Consumes the partials (a large set is folded in place by a first stage).
-int launch_reduce(void *stream, Partial *partials, uint32_t n_partials, Partial *out) {
+int launch_reduce(void *stream, Partial *partials, uint32_t n_partials, Partial *out, uint64_t idx_base) {
     if (n_partials <= 4 * kReduceChunk) {
-        hipLaunchKernelGGL(reduce_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, partials, n_partials, out, 1u);
+        hipLaunchKernelGGL(reduce_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, partials, n_partials, out, 1u,
+                           idx_base);
         return check_launch();
     }
     const uint32_t g = (n_partials + kReduceChunk - 1) / kReduceChunk;
     hipLaunchKernelGGL(reduce_stage_kernel, dim3(g), dim3(256), 0, (hipStream_t)stream, partials, n_partials);
     if (check_launch() != 0) return -1;
     hipLaunchKernelGGL(reduce_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, (const Partial *)partials, g, out,
-                       kReduceChunk);
+                       kReduceChunk, idx_base);
+    return check_launch();
+}
+
+int launch_group_merge(void *stream, const Partial *recv, uint32_t shards, uint32_t nq, uint32_t stride, Partial *out) {
+    if (nq == 0) return 0;
+    hipLaunchKernelGGL(group_merge_kernel, dim3((nq + 255) / 256), dim3(256), 0, (hipStream_t)stream, recv, shards, nq,
+                       stride, out);
     return check_launch();
 }
 

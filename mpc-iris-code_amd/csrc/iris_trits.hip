@@ -152,7 +152,7 @@ __global__ void __launch_bounds__(256, 2)
     // the table: the 1-KB constant staged through rows 252..255 (never read: bytes are < 243),
     // one global load per thread, then rows 0..242 written from LDS (a wave reads one row:
     // broadcast; writes consecutive dwords: conflict-free)
-    __shared__ uint32_t lut[256 * kLutStride];
+    __shared__ __attribute__((aligned(16))) uint32_t lut[256 * kLutStride];  // also the 16-B store staging of the epilogue
     lut[kLutStage + threadIdx.x] = kTritLut.v[threadIdx.x];
     __syncthreads();
     for (int i = threadIdx.x; i < 243 * kLutStride; i += 256) lut[i] = lut[kLutStage + (i >> 6)] << ((i & 32) >> 3);

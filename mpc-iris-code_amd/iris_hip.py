@@ -137,6 +137,28 @@ def load_library(path=None):
             "iris_engine_query_tables": ([P, P, ctypes.c_size_t, P, ctypes.c_size_t], ctypes.c_int),
             "iris_host_query_tables": ([ctypes.c_int, P, ctypes.c_uint32, P, ctypes.c_size_t, P, ctypes.c_size_t],
                                        ctypes.c_int),
+            "iris_db_attach_host": ([P, P, u64, ctypes.c_int], ctypes.c_int),
+            "iris_db_detach_host": ([P], ctypes.c_int),
+            "iris_group_create": ([ctypes.POINTER(ctypes.c_int), ctypes.c_uint32, PP], ctypes.c_int),
+            "iris_group_unique_id": ([P], ctypes.c_int),
+            "iris_group_create_rank": ([ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, P, PP], ctypes.c_int),
+            "iris_group_destroy": ([P], ctypes.c_int),
+            "iris_group_info": ([P, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32),
+                                 ctypes.POINTER(ctypes.c_uint32)], ctypes.c_int),
+            "iris_group_device": ([P, ctypes.c_uint32, PP], ctypes.c_int),
+            "iris_group_db_create": ([P, ctypes.c_int, u64, ctypes.c_int, ctypes.c_uint32, PP], ctypes.c_int),
+            "iris_group_db_destroy": ([P], ctypes.c_int),
+            "iris_group_db_info": ([P, ctypes.POINTER(u64), ctypes.POINTER(ctypes.c_uint32),
+                                    ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)], ctypes.c_int),
+            "iris_group_db_shard": ([P, ctypes.c_uint32, PP, ctypes.POINTER(u64), ctypes.POINTER(u64)], ctypes.c_int),
+            "iris_group_db_generate": ([P, u64], ctypes.c_int),
+            "iris_group_db_write": ([P, u64, P, u64], ctypes.c_int),
+            "iris_group_db_read": ([P, u64, u64, P], ctypes.c_int),
+            "iris_group_db_load_file": ([P, ctypes.c_char_p, u64], ctypes.c_int),
+            "iris_group_template_search": ([P, P, ctypes.POINTER(Match)], ctypes.c_int),
+            "iris_group_template_search_async": ([P, P, PP], ctypes.c_int),
+            "iris_group_pending_wait": ([P, ctypes.POINTER(Match)], ctypes.c_int),
+            "iris_group_template_batch_search": ([P, P, ctypes.c_uint32, ctypes.POINTER(Match)], ctypes.c_int),
         }
         for name, (args, res) in sig.items():
             f = getattr(lib, name)
@@ -164,6 +186,12 @@ def exported_symbols():
         "iris_db_truncate", "iris_memcpy_h2d", "iris_resolver_search_masks",
         "iris_query_table_sizes", "iris_engine_query_tables", "iris_host_query_tables", "iris_device_memory",
         "iris_template_search_async", "iris_pending_wait",
+        "iris_db_attach_host", "iris_db_detach_host",
+        "iris_group_create", "iris_group_unique_id", "iris_group_create_rank", "iris_group_destroy", "iris_group_info",
+        "iris_group_device", "iris_group_db_create", "iris_group_db_destroy", "iris_group_db_info",
+        "iris_group_db_shard", "iris_group_db_generate", "iris_group_db_write", "iris_group_db_read",
+        "iris_group_db_load_file", "iris_group_template_search", "iris_group_template_search_async",
+        "iris_group_pending_wait", "iris_group_template_batch_search",
     ]
 
 
@@ -584,9 +612,11 @@ class Database:
 
     def clear(self):
         _check(load_library().iris_db_clear(self.handle))
+        self._attached = None
 
     def truncate(self, n):
         _check(load_library().iris_db_truncate(self.handle, int(n)))
+        self._attached = None
 
     def load_file(self, path, first=0, count=None):
         """Appends records [first, first+count) of a raw record file (.masks / .share-i /
@@ -598,10 +628,27 @@ class Database:
         return got.value
 
     def save_file(self, path, first=0, n=None):
-        """Writes records [first, first+n) to a raw record file."""
+        """Writes records [first, first+n) to a raw record file (refused for TRITS databases)."""
         if n is None:
             n = len(self) - int(first)
         _check(load_library().iris_db_save_file(self.handle, os.fsencode(path), int(first), int(n)))
+
+    def attach_host(self, host, upload=True):
+        """Declares this database the resident copy of the host record array `host` (e.g. a
+        memory-mapped record file, src/main.rs:389-391,458-460): upload=True fills the (empty)
+        database from it; upload=False checks it already holds them.  Engine batch_process
+        calls on slices (numpy views) of `host` then run on the device copy without an
+        upload.  Keeps a reference to `host` while attached."""
+        a = host if isinstance(host, np.ndarray) else np.asarray(host)
+        dt, width = _REC_DTYPE[self.kind]
+        if a.dtype != dt or a.ndim != 2 or a.shape[1] != width or not a.flags["C_CONTIGUOUS"]:
+            raise IrisError(-1, f"host must be a C-contiguous [n, {width}] {np.dtype(dt).name} array")
+        _check(load_library().iris_db_attach_host(self.handle, _ptr(a), a.shape[0], 1 if upload else 0))
+        self._attached = a
+
+    def detach_host(self):
+        _check(load_library().iris_db_detach_host(self.handle))
+        self._attached = None
 
 
 # ====================================================================== engines
@@ -649,7 +696,7 @@ class _Engine:
                 raise IrisError(-1, f"assertion `out.len() == db.len()` failed: {out.shape[0]} != {n}")
             _check(lib.iris_engine_batch_process(self.handle, db.handle, int(first), int(n), _ptr(out)))
         else:
-            a = _records(self.kind, db)
+            a = _records(self.kind, db)  # a contiguous view of the caller's array is passed as is
             if out.shape[0] != a.shape[0]:
                 raise IrisError(-1, f"assertion `out.len() == db.len()` failed: {out.shape[0]} != {a.shape[0]}")
             _check(lib.iris_engine_batch_process_host(self.handle, _ptr(a), a.shape[0], _ptr(out)))
@@ -817,6 +864,197 @@ class TemplateBatchEngine(_Engine):
         return list(out)
 
 
+# ====================================================================== device groups
+
+
+class Group:
+    """Devices searched together (include/iris_hip.h "device groups"): a sharded template
+    database, per-shard winners all-gathered over RCCL and merged on every device.
+    Group(ordinals) drives several devices from this process (ncclCommInitAll);
+    Group.rank(ordinal, nranks, rank, uid) is one device of a multi-process group whose
+    128-byte id comes from Group.unique_id() on rank 0."""
+
+    def __init__(self, ordinals=(0,), _handle=None):
+        if _handle is not None:
+            self.handle = _handle
+        else:
+            ords = (ctypes.c_int * len(ordinals))(*[int(o) for o in ordinals])
+            h = ctypes.c_void_p()
+            _check(load_library().iris_group_create(ords, len(ordinals), ctypes.byref(h)))
+            self.handle = h
+        l, r, f = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+        _check(load_library().iris_group_info(self.handle, ctypes.byref(l), ctypes.byref(r), ctypes.byref(f)))
+        self.local_devices, self.ranks, self.first_rank = l.value, r.value, f.value
+        self.devices = []
+        for i in range(self.local_devices):
+            d = ctypes.c_void_p()
+            _check(load_library().iris_group_device(self.handle, i, ctypes.byref(d)))
+            self.devices.append(_BorrowedDevice(d))
+
+    @staticmethod
+    def unique_id():
+        buf = (ctypes.c_uint8 * 128)()
+        _check(load_library().iris_group_unique_id(buf))
+        return bytes(buf)
+
+    @classmethod
+    def rank(cls, ordinal, nranks, rank, uid):
+        if len(uid) != 128:
+            raise ValueError("the group id is 128 bytes")
+        buf = (ctypes.c_uint8 * 128).from_buffer_copy(bytes(uid))
+        h = ctypes.c_void_p()
+        _check(load_library().iris_group_create_rank(int(ordinal), int(nranks), int(rank), buf, ctypes.byref(h)))
+        return cls(_handle=h)
+
+    def close(self):
+        if getattr(self, "handle", None):
+            load_library().iris_group_destroy(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class _BorrowedDevice(Device):
+    """A group's device handle (owned by the group: close() does nothing)."""
+
+    def __init__(self, handle):
+        self.handle = handle
+        self.ordinal = None
+
+    def close(self):
+        self.handle = None
+
+
+class _BorrowedDatabase(Database):
+    """A group shard's database (owned by the group database: close() does nothing)."""
+
+    def __init__(self, handle, device, kind):
+        self.handle = handle
+        self.device = device
+        self.kind = kind
+
+    def close(self):
+        self.handle = None
+
+
+class GroupDatabase:
+    """`total` records of `kind` in S = ranks x shards_per_device contiguous shards over a
+    Group; every record starts empty (never a candidate)."""
+
+    def __init__(self, group, kind, total, layout=LAYOUT_DEFAULT, shards_per_device=1):
+        self.group = group
+        self.kind = kind
+        h = ctypes.c_void_p()
+        _check(load_library().iris_group_db_create(group.handle, int(kind), int(total), int(layout),
+                                                   int(shards_per_device), ctypes.byref(h)))
+        self.handle = h
+        t, S, f, l = ctypes.c_uint64(), ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+        _check(load_library().iris_group_db_info(h, ctypes.byref(t), ctypes.byref(S), ctypes.byref(f),
+                                                 ctypes.byref(l)))
+        self.total, self.shards, self.first_shard, self.local_shards = t.value, S.value, f.value, l.value
+
+    def shard(self, i):
+        """-> (first global index, count) of local shard i."""
+        f, c = ctypes.c_uint64(), ctypes.c_uint64()
+        _check(load_library().iris_group_db_shard(self.handle, int(i), None, ctypes.byref(f), ctypes.byref(c)))
+        return f.value, c.value
+
+    def shard_db(self, i):
+        """Local shard i as a Database (borrowed: owned by this group database), e.g. for a
+        local search with no exchange; its record j is global record shard(i)[0] + j."""
+        h = ctypes.c_void_p()
+        _check(load_library().iris_group_db_shard(self.handle, int(i), ctypes.byref(h), None, None))
+        spd = self.local_shards // self.group.local_devices
+        return _BorrowedDatabase(h, self.group.devices[int(i) // spd], self.kind)
+
+    def close(self):
+        if getattr(self, "handle", None):
+            load_library().iris_group_db_destroy(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __len__(self):
+        return self.total
+
+    def generate(self, seed):
+        _check(load_library().iris_group_db_generate(self.handle, int(seed)))
+
+    def write(self, index, records):
+        a = _records(self.kind, records)
+        _check(load_library().iris_group_db_write(self.handle, int(index), _ptr(a), a.shape[0]))
+
+    def read(self, index, n):
+        dt, width = _REC_DTYPE[self.kind]
+        out = np.empty((n, width), dt)
+        _check(load_library().iris_group_db_read(self.handle, int(index), int(n), _ptr(out)))
+        return out
+
+    def load_file(self, path, first=0):
+        _check(load_library().iris_group_db_load_file(self.handle, os.fsencode(path), int(first)))
+
+    def search(self, query):
+        """Global (min distance, lowest index) of one query Template -> Match."""
+        q = query.to_array() if isinstance(query, Template) else _c(query, np.uint64)
+        m = Match()
+        _check(load_library().iris_group_template_search(self.handle, _ptr(_c(q, np.uint64)), ctypes.byref(m)))
+        return m
+
+    def search_async(self, query):
+        q = query.to_array() if isinstance(query, Template) else _c(query, np.uint64)
+        h = ctypes.c_void_p()
+        _check(load_library().iris_group_template_search_async(self.handle, _ptr(_c(q, np.uint64)), ctypes.byref(h)))
+        return GroupPendingSearch(h)
+
+    def batch_search(self, queries):
+        q = _records(KIND_TEMPLATES, queries)
+        out = (Match * q.shape[0])()
+        _check(load_library().iris_group_template_batch_search(self.handle, _ptr(q), q.shape[0], out))
+        return list(out)
+
+
+class GroupPendingSearch:
+    """An enqueued group search; wait() -> Match, once."""
+
+    def __init__(self, handle):
+        self.handle = handle
+
+    def wait(self):
+        if self.handle is None:
+            raise IrisError(-1, "GroupPendingSearch.wait called twice")
+        m = Match()
+        h, self.handle = self.handle, None
+        _check(load_library().iris_group_pending_wait(h, ctypes.byref(m)))
+        return m
+
+    def __del__(self):
+        if getattr(self, "handle", None) is not None:
+            try:
+                load_library().iris_group_pending_wait(self.handle, None)
+            except Exception:
+                pass
+
+
 def distances(query, entry, device=None):
     """distances(&EncodedBits, &EncodedBits) -> [u16; 31] (src/lib.rs:82-87)."""
     dev = device or default_device()
@@ -904,6 +1142,7 @@ def f64_bits(x):
 __all__ = [
     "Bits", "EncodedBits", "Template", "encode", "decode_distance", "resolver_search", "resolver_search_device", "distances", "denominators", "MasksEngine",
     "DistanceEngine", "TemplateEngine", "TemplateBatchEngine", "Device", "Database", "Match", "merge_matches", "dot_bool", "dot_u16",
+    "Group", "GroupDatabase", "GroupPendingSearch",
     "dot_bool_batch", "dot_u16_batch", "IrisError", "load_library", "KIND_MASKS", "KIND_SHARES", "KIND_TEMPLATES",
     "LAYOUT_DEFAULT", "LAYOUT_LANES", "LAYOUT_TILES", "LAYOUT_TRITS",
     "ROTATIONS", "BITS", "LIMBS", "COLS", "ROWS",

@@ -1,8 +1,8 @@
-"""GPU box: bench.py's multi-rank path end to end (torch.distributed.run, 2 ranks on
-the one GPU, gloo exchange): each rank generates its shard, searches it, the ranks
-all-gather and merge their minima, and rank 0 prints one JSON line whose planted
-known answer (in rank 1's shard) must be found.  The 8-GPU RCCL run is the driver's;
-this rehearses the same code with the exchange on CPU tensors."""
+"""GPU box: bench.py's multi-GPU paths end to end on the one GPU: torch.distributed.run
+ranks with the gloo rehearsal exchange (2 ranks, and the driver's 8-rank run sharing the card),
+the default RCCL path on one rank (library communicator via ncclCommInitRank, gloo only for the
+rendezvous) and the single-process library device group (--single-process).  Each run plants a
+known answer (in a later rank's shard when there are several) that must be found."""
 import json
 import os
 import pathlib
@@ -88,34 +88,32 @@ def test_bench_more_gpus_than_visible_fails():
     assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
 
 
-def test_rccl_exchange_single_rank():
-    """The RCCL form of the exchange (all_gather_into_tensor on device tensors) on a
-    one-rank "nccl" process group: the code path the 8-GPU run takes."""
-    code = f"""
-import os, sys
-sys.path[:0] = [{str(ROOT)!r}, {str(ROOT / 'mpc-iris-code_amd')!r}]
-os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT="{_free_port()}")
-import torch, torch.distributed as dist
-import iris_hip as ih, iris_dist
-torch.cuda.set_device(0)
-dist.init_process_group("nccl", rank=0, world_size=1)
-m = ih.Match(0.25, 1234, 5, 20, -3, 0)
-r = iris_dist.allgather_merge(m, device="cuda:0")
-assert (r.index, r.num, r.den, r.rotation) == (1234, 5, 20, -3) and r.distance == 0.25, r
-dist.destroy_process_group()
-print("rccl ok")
-"""
-    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, timeout=240)
-    assert r.returncode == 0 and "rccl ok" in r.stdout, r.stdout + r.stderr[-3000:]
+def test_bench_single_process_group():
+    """`bench.py --single-process`: one process, a library device group over --gpus devices
+    (ncclCommInitAll + the RCCL all-gather of the shard winners + on-device merge), no
+    torch; here a 1-device group, for the search (pipelined) and a 9-query batch."""
+    for extra in ([], ["--workload", "batch", "--queries", "9"]):
+        cmd = [sys.executable, str(ROOT / "bench.py"), "--gpus", "1", "--single-process", "--steps", "3", "--warmup",
+               "1", "--n-per-gpu", "300000", "--no-cpu-baseline", "--prewarm-s", "0.2", *extra]
+        r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, r.stderr[-3000:]
+        d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+        assert d["n_gpus"] == 1 and d["check"]["ok"] and d["processes"] == 1
+        assert d["backend"].startswith("rccl") and "RCCL" in d["config"]["exchange"]
+        assert d["value_per_gpu"] == d["value"]
 
 
 def test_bench_rccl_single_rank():
-    """bench.py's process-group path with the default "nccl" (RCCL) backend on one rank."""
+    """bench.py's process-group path with the default RCCL backend on one rank: gloo for the
+    rendezvous, the library's own communicator (ncclCommInitRank, id broadcast over gloo)
+    for the exchange."""
     env = dict(os.environ, IRIS_FORCE_DIST="1", IRIS_DIST_BACKEND="nccl")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(ROOT / "bench.py"),
-           "--steps", "3", "--warmup", "1", "--n-per-gpu", "300000", "--no-cpu-baseline"]
-    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
-    assert r.returncode == 0, r.stderr[-3000:]
-    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
-    assert d["n_gpus"] == 1 and d["check"]["ok"]
+    for extra in ([], ["--workload", "batch", "--queries", "5"]):
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(ROOT / "bench.py"),
+               "--steps", "3", "--warmup", "1", "--n-per-gpu", "300000", "--no-cpu-baseline", *extra]
+        r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, r.stderr[-3000:]
+        d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+        assert d["n_gpus"] == 1 and d["check"]["ok"] and d["ranks_seen"] == 1
+        assert "ncclCommInitRank" in d["backend"] and "RCCL" in d["config"]["exchange"]

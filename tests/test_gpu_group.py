@@ -1,0 +1,202 @@
+"""GPU: device groups (iris_group_*, csrc/iris_group.hip) — a template database split
+into contiguous shards, each searched on its device, the per-shard winners all-gathered
+over RCCL (librccl from /opt/rocm) and merged with the resolver's rule: exact fraction,
+then the lowest global index (src/main.rs:616-621).  On the one-GPU box a group has one
+device (a 1-rank RCCL communicator); shards_per_device > 1 splits its range into several
+logical shards that are searched and exchanged separately, so cross-shard ties and empty
+shards are exercised.  Every answer must equal a single-device search of the same records
+and the CPU oracle (Template::distance, src/template.rs:43-64)."""
+import numpy as np
+import pytest
+
+import iris_hip as ih
+from oracle import oracle_c as oc
+
+pytestmark = pytest.mark.gpu
+SEED = 77
+
+
+def planted(query, r, flips=0):
+    p = ih.Bits(query[:200]).rotated(r).limbs.copy()
+    m = ih.Bits(query[200:]).rotated(r).limbs
+    p[3] ^= np.uint64(flips)
+    return np.concatenate([p, m])
+
+
+def oracle_best(query, recs):
+    d = oc.template_distances(query, recs)
+    return oc.argmin(d)
+
+
+def same(m, best, idx):
+    return m.index == idx and np.float64(m.distance).view(np.uint64) == np.float64(best).view(np.uint64)
+
+
+@pytest.fixture(scope="module")
+def group():
+    with ih.Group([0]) as g:
+        assert (g.local_devices, g.ranks, g.first_rank) == (1, 1, 0)
+        yield g
+
+
+@pytest.mark.parametrize("spd", [1, 3, 8])
+def test_group_search_equals_single_device_and_oracle(group, device, spd):
+    n = 5003
+    ref = oc.gen_templates(SEED, 0, n)
+    query = oc.gen_templates(SEED + 1, 0, 1)[0]
+    with ih.GroupDatabase(group, ih.KIND_TEMPLATES, n, shards_per_device=spd) as gdb:
+        assert gdb.shards == spd and gdb.local_shards == spd and gdb.total == n
+        bounds = [gdb.shard(i) for i in range(spd)]
+        assert bounds[0][0] == 0 and sum(c for _, c in bounds) == n
+        assert all(bounds[i][0] + bounds[i][1] == bounds[i + 1][0] for i in range(spd - 1))
+        gdb.generate(SEED)
+        assert (gdb.read(0, n) == ref).all()
+        site = 4321
+        rec = planted(query, -6, 0x0F0F)
+        gdb.write(site, rec[None, :])
+        ref[site] = rec
+        m = gdb.search(query)
+        best, idx = oracle_best(query, ref)
+        assert same(m, best, idx) and idx == site and m.rotation == -6
+        with ih.Database(device, ih.KIND_TEMPLATES, n) as db, ih.TemplateEngine(device, query) as eng:
+            db.append(ref)
+            s = eng.search(db)
+        assert (s.index, s.num, s.den, s.rotation) == (m.index, m.num, m.den, m.rotation)
+
+
+def test_group_cross_shard_tie_lowest_global_index(group):
+    """Two exact copies of the query (distance 0) in different logical shards: the lower
+    global index wins whichever shard reports first; a strictly better one in a later shard
+    beats both."""
+    n, spd = 4099, 4
+    query = oc.gen_templates(SEED + 2, 0, 1)[0]
+    with ih.GroupDatabase(group, ih.KIND_TEMPLATES, n, shards_per_device=spd) as gdb:
+        gdb.generate(SEED)
+        lo, hi = gdb.shard(1)[0] + 5, gdb.shard(3)[0] + 7
+        exact = planted(query, 0)
+        gdb.write(hi, exact[None, :])
+        gdb.write(lo, exact[None, :])
+        m = gdb.search(query)
+        assert m.index == lo and m.distance == 0.0 and m.rotation == 0
+        # the tie at the shard boundary: last record of shard 2 and first of shard 3
+        f3 = gdb.shard(3)[0]
+        gdb.write(f3 - 1, exact[None, :])
+        gdb.write(f3, exact[None, :])
+        assert gdb.search(query).index == lo
+        # a copy whose valid bits are all equal but fewer: still distance 0, lowest index rules
+        ref = gdb.read(0, n)
+        best, idx = oracle_best(query, ref)
+        assert same(gdb.search(query), best, idx)
+
+
+def test_group_empty_shards_and_tiny_db(group):
+    query = oc.gen_templates(SEED + 3, 0, 1)[0]
+    with ih.GroupDatabase(group, ih.KIND_TEMPLATES, 3, shards_per_device=8) as gdb:
+        assert sum(gdb.shard(i)[1] for i in range(8)) == 3
+        m = gdb.search(query)  # nothing written: every record is empty
+        assert m.index == 2**64 - 1 and m.distance == float("inf")
+        gdb.generate(SEED)
+        ref = gdb.read(0, 3)
+        best, idx = oracle_best(query, ref)
+        assert same(gdb.search(query), best, idx)
+    with ih.GroupDatabase(group, ih.KIND_TEMPLATES, 0) as gdb:
+        assert gdb.search(query).index == 2**64 - 1
+
+
+def test_group_async_out_of_order(group):
+    n, spd = 20000, 2
+    ref = oc.gen_templates(SEED, 0, n)
+    qs = oc.gen_templates(SEED + 10, 0, 5)
+    with ih.GroupDatabase(group, ih.KIND_TEMPLATES, n, shards_per_device=spd) as gdb:
+        gdb.generate(SEED)
+        for k, q in enumerate(qs):
+            gdb.write(1000 + 3700 * k, planted(q, k - 2, 0x3)[None, :])
+        ref = gdb.read(0, n)
+        pend = [gdb.search_async(q) for q in qs]
+        got = [None] * len(qs)
+        for k in (3, 0, 4, 1, 2):
+            got[k] = pend[k].wait()
+        for k, q in enumerate(qs):
+            best, idx = oracle_best(q, ref)
+            assert same(got[k], best, idx) and idx == 1000 + 3700 * k
+
+
+@pytest.mark.parametrize("layout", [ih.LAYOUT_LANES, ih.LAYOUT_TRITS])
+def test_group_other_layouts(group, layout):
+    n = 3001
+    ref = oc.gen_templates(SEED, 0, n)
+    query = oc.gen_templates(SEED + 4, 0, 1)[0]
+    with ih.GroupDatabase(group, ih.KIND_TEMPLATES, n, layout, shards_per_device=3) as gdb:
+        gdb.generate(SEED)
+        gdb.write(2999, planted(query, 15, 0x11)[None, :])
+        ref[2999] = planted(query, 15, 0x11)
+        best, idx = oracle_best(query, ref)
+        m = gdb.search(query)
+        assert same(m, best, idx) and idx == 2999 and m.rotation == 15
+
+
+@pytest.mark.parametrize("nq", [2, 3, 9])
+def test_group_batch_search(group, device, nq):
+    n, spd = 6000, 3
+    ref = oc.gen_templates(SEED, 0, n)
+    qs = oc.gen_templates(SEED + 20, 0, nq)
+    with ih.GroupDatabase(group, ih.KIND_TEMPLATES, n, shards_per_device=spd) as gdb:
+        gdb.generate(SEED)
+        sites = [gdb.shard(k % spd)[0] + 17 * k + 3 for k in range(nq)]
+        for k, s in enumerate(sites):
+            if k % 2 == 0:  # every other query gets a planted answer
+                rec = planted(qs[k], (k % 31) - 15, 0x5)
+                gdb.write(s, rec[None, :])
+                ref[s] = rec
+        got = gdb.batch_search(qs)
+        for k, q in enumerate(qs):
+            best, idx = oracle_best(q, ref)
+            assert same(got[k], best, idx), (k, got[k], best, idx)
+
+
+def test_group_write_read_across_shards_and_load_file(group, tmp_path):
+    n, spd = 2500, 4
+    rng = np.random.default_rng(5)
+    recs = rng.integers(0, 2**64, (n, 400), dtype=np.uint64)
+    path = tmp_path / "t.templates"
+    recs.tofile(path)
+    with ih.GroupDatabase(group, ih.KIND_TEMPLATES, n - 100, shards_per_device=spd) as gdb:
+        gdb.load_file(path, first=100)
+        assert (gdb.read(0, n - 100) == recs[100:]).all()
+        a, b = gdb.shard(2)[0] - 3, gdb.shard(2)[0] + 4  # a range across a shard boundary
+        gdb.write(a, recs[:b - a])
+        assert (gdb.read(a, b - a) == recs[:b - a]).all()
+        query = recs[7]
+        best, idx = oracle_best(query, gdb.read(0, n - 100))
+        assert same(gdb.search(query), best, idx)
+    with ih.GroupDatabase(group, ih.KIND_TEMPLATES, n, shards_per_device=spd) as gdb:
+        with pytest.raises(ih.IrisError):
+            gdb.load_file(path, first=1)  # the file holds fewer than first + total records
+
+
+def test_group_rejects_duplicate_device_and_bad_args():
+    with pytest.raises(ih.IrisError):
+        ih.Group([0, 0])
+    with ih.Group([0]) as g:
+        with pytest.raises(ih.IrisError):
+            ih.GroupDatabase(g, ih.KIND_TEMPLATES, 10, shards_per_device=0)
+        with ih.GroupDatabase(g, ih.KIND_MASKS, 10) as gdb:
+            with pytest.raises(ih.IrisError):
+                gdb.search(oc.gen_templates(1, 0, 1)[0])
+
+
+def test_group_single_rank_communicator():
+    """The multi-process form (ncclCommInitRank) with one rank: what each torchrun rank of
+    bench.py builds."""
+    uid = ih.Group.unique_id()
+    assert len(uid) == 128
+    n = 3000
+    ref = oc.gen_templates(SEED, 0, n)
+    query = ref[1234].copy()
+    query[5] ^= np.uint64(0xFF)
+    with ih.Group.rank(0, 1, 0, uid) as g:
+        assert (g.local_devices, g.ranks, g.first_rank) == (1, 1, 0)
+        with ih.GroupDatabase(g, ih.KIND_TEMPLATES, n, shards_per_device=2) as gdb:
+            gdb.generate(SEED)
+            best, idx = oracle_best(query, ref)
+            assert same(gdb.search(query), best, idx) and idx == 1234
