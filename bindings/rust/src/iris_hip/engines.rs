@@ -18,7 +18,7 @@
 //! once its share or masks file is loaded into a `Database`.
 use std::ptr;
 
-use super::{check, default_device, ffi, match_to_pair, Database, Device, Record, Result};
+use super::{check, default_device, ffi, match_to_pair, Database, Device, Record, Result, ShardedDatabase};
 use crate::{Bits, EncodedBits, Template};
 
 /// An engine handle plus the device it lives on (kept alive by the clone).
@@ -148,6 +148,7 @@ pub fn denominators(query: &Bits, entry: &Bits) -> [u16; 31] {
 /// `(min_distance, min_index)` (src/main.rs:616-621), bit-exact.
 pub struct TemplateEngine {
     h: Handle,
+    query: Template,
 }
 
 /// An enqueued search (`iris_template_search_async`); `wait` blocks for it alone.
@@ -186,7 +187,13 @@ impl TemplateEngine {
         let mut raw = ptr::null_mut();
         let q = query as *const Template as *const ffi::IrisTemplate;
         check(unsafe { ffi::iris_template_engine_new(device.raw(), q, &mut raw) })?;
-        Ok(Self { h: Handle { raw, _device: device.clone() } })
+        Ok(Self { h: Handle { raw, _device: device.clone() }, query: *query })
+    }
+
+    /// The same query over a sharded multi-GPU database (every device builds its own
+    /// engine, searches its shards; winners all-gathered over RCCL and merged).
+    pub fn search_sharded(&self, db: &ShardedDatabase) -> Result<(f64, usize)> {
+        db.search(&self.query)
     }
 
     /// `Template::distance(query, db[i])` for i in [first, first + out.len()).
@@ -278,5 +285,40 @@ mod tests {
         }
         let (best, index) = engine.search(&db, 0, records.len() as u64, 0).unwrap();
         assert_eq!((best, index), (0.0, 61));
+    }
+
+    #[test]
+    fn attached_slices_match_host_loop() {
+        // the resolver's loop (src/main.rs:511-516) over an attached array: no upload per chunk
+        let mut rng = thread_rng();
+        let q: Bits = rng.gen();
+        let masks: Vec<Bits> = (0..5000).map(|_| rng.gen()).collect();
+        let att = crate::iris_hip::AttachedDatabase::new(default_device(), &masks).unwrap();
+        let engine = MasksEngine::new(&q);
+        for chunk in masks.chunks(1234) {
+            let mut out = vec![[0u16; 31]; chunk.len()];
+            engine.batch_process(&mut out, chunk);
+            for (row, e) in out.iter().zip(chunk.iter()) {
+                for (k, &got) in row.iter().enumerate() {
+                    let r = q.rotated(k as i32 - 15);
+                    let want: u32 = r.0.iter().zip(e.0.iter()).map(|(&a, &b)| (a & b).count_ones()).sum();
+                    assert_eq!(got as u32, want);
+                }
+            }
+        }
+        drop(att);
+    }
+
+    #[test]
+    fn sharded_search_matches_single_device() {
+        let mut rng = thread_rng();
+        let query: Template = rng.gen();
+        let mut records: Vec<Template> = (0..1000).map(|_| rng.gen()).collect();
+        records[777] = query.rotated(-4);
+        let group = crate::iris_hip::Group::new(&[0]).unwrap();
+        let mut sdb = ShardedDatabase::new(&group, records.len() as u64, ffi::IRIS_LAYOUT_DEFAULT, 4).unwrap();
+        sdb.write(0, &records).unwrap();
+        let engine = TemplateEngine::new(&query);
+        assert_eq!(engine.search_sharded(&sdb).unwrap(), (0.0, 777));
     }
 }

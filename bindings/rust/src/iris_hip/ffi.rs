@@ -39,6 +39,9 @@ pub const IRIS_LAYOUT_TILES: c_int = 2;
 /// Search-only template layout: 2560 B per template (pattern & mask read back).
 pub const IRIS_LAYOUT_TRITS: c_int = 3;
 
+/// Bytes of a device group's RCCL id (`iris_group_unique_id`).
+pub const IRIS_GROUP_ID_BYTES: usize = 128;
+
 /// Opaque handles (`iris_device_t`, `iris_db_t`, `iris_engine_t`, `iris_pending_t`).
 #[repr(C)]
 pub struct IrisDevice {
@@ -54,6 +57,19 @@ pub struct IrisEngine {
 }
 #[repr(C)]
 pub struct IrisPending {
+    _private: [u8; 0],
+}
+/// Device groups (`iris_group_t`, `iris_group_db_t`, `iris_group_pending_t`).
+#[repr(C)]
+pub struct IrisGroup {
+    _private: [u8; 0],
+}
+#[repr(C)]
+pub struct IrisGroupDb {
+    _private: [u8; 0],
+}
+#[repr(C)]
+pub struct IrisGroupPending {
     _private: [u8; 0],
 }
 
@@ -125,6 +141,10 @@ extern "C" {
     pub fn iris_db_generate(db: *mut IrisDb, n: u64, seed: u64, global_index0: u64) -> c_int;
     pub fn iris_db_clear(db: *mut IrisDb) -> c_int;
     pub fn iris_db_truncate(db: *mut IrisDb, len: u64) -> c_int;
+
+    // host residency
+    pub fn iris_db_attach_host(db: *mut IrisDb, host: *const c_void, n: u64, upload: c_int) -> c_int;
+    pub fn iris_db_detach_host(db: *mut IrisDb) -> c_int;
 
     // on-disk formats
     pub fn iris_db_load_file(db: *mut IrisDb, path: *const c_char, first: u64, count: u64, loaded: *mut u64)
@@ -293,4 +313,64 @@ extern "C" {
         frag_bytes: usize,
     ) -> c_int;
     pub fn iris_match_merge(records: *const IrisMatch, count: u64, out: *mut IrisMatch) -> c_int;
+
+    // device groups (multi-GPU)
+    pub fn iris_group_create(ordinals: *const c_int, n: u32, out: *mut *mut IrisGroup) -> c_int;
+    pub fn iris_group_unique_id(id: *mut u8) -> c_int;
+    pub fn iris_group_create_rank(
+        ordinal: c_int,
+        nranks: u32,
+        rank: u32,
+        id: *const u8,
+        out: *mut *mut IrisGroup,
+    ) -> c_int;
+    pub fn iris_group_destroy(group: *mut IrisGroup) -> c_int;
+    pub fn iris_group_info(
+        group: *const IrisGroup,
+        local_devices: *mut u32,
+        ranks: *mut u32,
+        first_rank: *mut u32,
+    ) -> c_int;
+    pub fn iris_group_device(group: *const IrisGroup, i: u32, dev: *mut *mut IrisDevice) -> c_int;
+    pub fn iris_group_db_create(
+        group: *mut IrisGroup,
+        kind: c_int,
+        total: u64,
+        layout: c_int,
+        shards_per_device: u32,
+        out: *mut *mut IrisGroupDb,
+    ) -> c_int;
+    pub fn iris_group_db_destroy(gdb: *mut IrisGroupDb) -> c_int;
+    pub fn iris_group_db_info(
+        gdb: *const IrisGroupDb,
+        total: *mut u64,
+        shards: *mut u32,
+        first_shard: *mut u32,
+        local_shards: *mut u32,
+    ) -> c_int;
+    pub fn iris_group_db_shard(
+        gdb: *const IrisGroupDb,
+        i: u32,
+        db: *mut *mut IrisDb,
+        first: *mut u64,
+        count: *mut u64,
+    ) -> c_int;
+    pub fn iris_group_db_generate(gdb: *mut IrisGroupDb, seed: u64) -> c_int;
+    pub fn iris_group_db_write(gdb: *mut IrisGroupDb, index: u64, records: *const c_void, n: u64) -> c_int;
+    pub fn iris_group_db_read(gdb: *const IrisGroupDb, index: u64, n: u64, records: *mut c_void) -> c_int;
+    pub fn iris_group_db_load_file(gdb: *mut IrisGroupDb, path: *const c_char, first: u64) -> c_int;
+    pub fn iris_group_template_search(gdb: *mut IrisGroupDb, query: *const IrisTemplate, out: *mut IrisMatch)
+        -> c_int;
+    pub fn iris_group_template_search_async(
+        gdb: *mut IrisGroupDb,
+        query: *const IrisTemplate,
+        out: *mut *mut IrisGroupPending,
+    ) -> c_int;
+    pub fn iris_group_pending_wait(pending: *mut IrisGroupPending, out: *mut IrisMatch) -> c_int;
+    pub fn iris_group_template_batch_search(
+        gdb: *mut IrisGroupDb,
+        queries: *const IrisTemplate,
+        nq: u32,
+        out: *mut IrisMatch,
+    ) -> c_int;
 }

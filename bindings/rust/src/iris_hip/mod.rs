@@ -17,6 +17,7 @@ pub mod ffi;
 use std::{
     ffi::{CStr, CString},
     fmt,
+    marker::PhantomData,
     os::raw::c_int,
     path::Path,
     ptr,
@@ -193,7 +194,7 @@ impl Database {
         self.len() == 0
     }
 
-    fn expect_kind<T: Record>(&self) -> Result<()> {
+    pub(crate) fn expect_kind<T: Record>(&self) -> Result<()> {
         if T::KIND != self.kind {
             return Err(Error { code: ffi::IRIS_E_ARG, message: "record kind does not match the database".into() });
         }
@@ -235,6 +236,204 @@ impl Drop for Database {
     fn drop(&mut self) {
         unsafe {
             ffi::iris_db_destroy(self.raw);
+        }
+    }
+}
+
+/// A `Database` that is the device copy of a host record array — typically the
+/// participant's or resolver's memory-mapped record file (src/main.rs:389-391,
+/// 458-460).  While it lives, the reference-signature calls
+/// `DistanceEngine::batch_process(out, chunk)` / `MasksEngine::batch_process(out, chunk)`
+/// on any sub-slice `chunk` of that array (the 20 000-record loop of src/main.rs:428-431,
+/// 513-516) run on the resident copy and upload nothing (`iris_db_attach_host`).  The
+/// borrow keeps the array alive and unchanged; dropping this detaches and frees the
+/// device copy.
+pub struct AttachedDatabase<'a> {
+    db: Database,
+    _host: PhantomData<&'a [u8]>,
+}
+
+impl<'a> AttachedDatabase<'a> {
+    /// Uploads `records` into a new database on `device` and attaches it.
+    pub fn new<T: Record>(device: &Device, records: &'a [T]) -> Result<Self> {
+        let db = Database::new::<T>(device, records.len() as u64)?;
+        check(unsafe { ffi::iris_db_attach_host(db.raw, records.as_ptr().cast(), records.len() as u64, 1) })?;
+        Ok(AttachedDatabase { db, _host: PhantomData })
+    }
+
+    /// Attaches a database that already holds exactly `records` (e.g. loaded from the
+    /// same file with `Database::load_file`; its first, middle and last record are checked).
+    pub fn from_loaded<T: Record>(db: Database, records: &'a [T]) -> Result<Self> {
+        db.expect_kind::<T>()?;
+        check(unsafe { ffi::iris_db_attach_host(db.raw, records.as_ptr().cast(), records.len() as u64, 0) })?;
+        Ok(AttachedDatabase { db, _host: PhantomData })
+    }
+
+    /// The resident database (device-resident engine forms, searches).
+    pub fn database(&self) -> &Database {
+        &self.db
+    }
+
+    /// Ends the attachment and returns the database.
+    pub fn into_inner(self) -> Database {
+        unsafe {
+            ffi::iris_db_detach_host(self.db.raw);
+        }
+        let me = std::mem::ManuallyDrop::new(self);
+        unsafe { ptr::read(&me.db) }
+    }
+}
+
+impl Drop for AttachedDatabase<'_> {
+    fn drop(&mut self) {
+        unsafe {
+            ffi::iris_db_detach_host(self.db.raw);
+        }
+    }
+}
+
+/// Devices searched together (`iris_group_*`): the multi-GPU form of the resolver's
+/// fan-out and sequential minimum (src/main.rs:486-504, 616-621).  A template database is
+/// split into contiguous shards, every device searches its own, and the per-shard winners
+/// are all-gathered by the library's RCCL communicator and merged on every device.
+pub struct Group {
+    raw: *mut ffi::IrisGroup,
+}
+
+unsafe impl Send for Group {}
+unsafe impl Sync for Group {}
+
+impl Group {
+    /// One process driving `ordinals` (ncclCommInitAll).
+    pub fn new(ordinals: &[i32]) -> Result<Self> {
+        let mut raw = ptr::null_mut();
+        check(unsafe { ffi::iris_group_create(ordinals.as_ptr(), ordinals.len() as u32, &mut raw) })?;
+        Ok(Group { raw })
+    }
+
+    /// The 128-byte id rank 0 creates and every rank of a multi-process group joins with.
+    pub fn unique_id() -> Result<[u8; ffi::IRIS_GROUP_ID_BYTES]> {
+        let mut id = [0u8; ffi::IRIS_GROUP_ID_BYTES];
+        check(unsafe { ffi::iris_group_unique_id(id.as_mut_ptr()) })?;
+        Ok(id)
+    }
+
+    /// This process's one device as `rank` of `nranks` (ncclCommInitRank).
+    pub fn rank(ordinal: i32, nranks: u32, rank: u32, id: &[u8; ffi::IRIS_GROUP_ID_BYTES]) -> Result<Self> {
+        let mut raw = ptr::null_mut();
+        check(unsafe { ffi::iris_group_create_rank(ordinal, nranks, rank, id.as_ptr(), &mut raw) })?;
+        Ok(Group { raw })
+    }
+
+    /// (local devices, ranks in the group, rank of local device 0).
+    pub fn info(&self) -> Result<(u32, u32, u32)> {
+        let (mut l, mut r, mut f) = (0u32, 0u32, 0u32);
+        check(unsafe { ffi::iris_group_info(self.raw, &mut l, &mut r, &mut f) })?;
+        Ok((l, r, f))
+    }
+}
+
+impl Drop for Group {
+    fn drop(&mut self) {
+        unsafe {
+            ffi::iris_group_destroy(self.raw);
+        }
+    }
+}
+
+/// `total` templates in S = ranks x `shards_per_device` contiguous shards over a `Group`
+/// (shard s holds global records [s*total/S, (s+1)*total/S)); records start empty.
+pub struct ShardedDatabase {
+    raw: *mut ffi::IrisGroupDb,
+}
+
+unsafe impl Send for ShardedDatabase {}
+unsafe impl Sync for ShardedDatabase {}
+
+/// An enqueued group search; `wait` blocks for it alone.
+pub struct PendingShardedSearch {
+    raw: *mut ffi::IrisGroupPending,
+}
+
+unsafe impl Send for PendingShardedSearch {}
+
+impl PendingShardedSearch {
+    pub fn wait(mut self) -> Result<(f64, usize)> {
+        let mut m = ffi::IrisMatch::default();
+        let raw = std::mem::replace(&mut self.raw, ptr::null_mut());
+        check(unsafe { ffi::iris_group_pending_wait(raw, &mut m) })?;
+        Ok(match_to_pair(&m))
+    }
+}
+
+impl Drop for PendingShardedSearch {
+    fn drop(&mut self) {
+        if !self.raw.is_null() {
+            let mut m = ffi::IrisMatch::default();
+            unsafe {
+                ffi::iris_group_pending_wait(self.raw, &mut m);
+            }
+        }
+    }
+}
+
+impl ShardedDatabase {
+    pub fn new(group: &Group, total: u64, layout: c_int, shards_per_device: u32) -> Result<Self> {
+        let mut raw = ptr::null_mut();
+        check(unsafe {
+            ffi::iris_group_db_create(group.raw, ffi::IRIS_KIND_TEMPLATES, total, layout, shards_per_device, &mut raw)
+        })?;
+        Ok(ShardedDatabase { raw })
+    }
+
+    pub fn raw(&self) -> *mut ffi::IrisGroupDb {
+        self.raw
+    }
+
+    /// Writes global records [index, index + records.len()) (this process's part of them).
+    pub fn write(&mut self, index: u64, records: &[Template]) -> Result<()> {
+        check(unsafe { ffi::iris_group_db_write(self.raw, index, records.as_ptr().cast(), records.len() as u64) })
+    }
+
+    pub fn read(&self, index: u64, out: &mut [Template]) -> Result<()> {
+        check(unsafe { ffi::iris_group_db_read(self.raw, index, out.len() as u64, out.as_mut_ptr().cast()) })
+    }
+
+    /// Global record i <- record first + i of a raw template file (local shards, in parallel).
+    pub fn load_file(&mut self, path: &Path, first: u64) -> Result<()> {
+        let c = path_cstring(path)?;
+        check(unsafe { ffi::iris_group_db_load_file(self.raw, c.as_ptr(), first) })
+    }
+
+    /// The resolver's `(min_distance, min_index)` of `query` over every shard, bit-exact
+    /// with `Template::distance` and the strict-< scan (src/template.rs:43-64, src/main.rs:616-621).
+    pub fn search(&self, query: &Template) -> Result<(f64, usize)> {
+        let mut m = ffi::IrisMatch::default();
+        let q = query as *const Template as *const ffi::IrisTemplate;
+        check(unsafe { ffi::iris_group_template_search(self.raw, q, &mut m) })?;
+        Ok(match_to_pair(&m))
+    }
+
+    pub fn search_async(&self, query: &Template) -> Result<PendingShardedSearch> {
+        let mut raw = ptr::null_mut();
+        let q = query as *const Template as *const ffi::IrisTemplate;
+        check(unsafe { ffi::iris_group_template_search_async(self.raw, q, &mut raw) })?;
+        Ok(PendingShardedSearch { raw })
+    }
+
+    pub fn batch_search(&self, queries: &[Template]) -> Result<Vec<(f64, usize)>> {
+        let mut out = vec![ffi::IrisMatch::default(); queries.len()];
+        check(unsafe {
+            ffi::iris_group_template_batch_search(self.raw, queries.as_ptr().cast(), queries.len() as u32, out.as_mut_ptr())
+        })?;
+        Ok(out.iter().map(match_to_pair).collect())
+    }
+}
+
+impl Drop for ShardedDatabase {
+    fn drop(&mut self) {
+        unsafe {
+            ffi::iris_group_db_destroy(self.raw);
         }
     }
 }

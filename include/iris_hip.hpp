@@ -323,10 +323,108 @@ public:
         check(iris_db_save_file(h_, path.c_str(), first, n));
     }
     void generate(uint64_t n, uint64_t seed, uint64_t global_index0) { check(iris_db_generate(h_, n, seed, global_index0)); }
+    // This database is the device copy of the host array `records` (e.g. the mmap'd record
+    // file, src/main.rs:389-391, 458-460): batch_process(out, slice) on slices of it then runs
+    // on the resident copy (iris_db_attach_host).  upload: fill the empty database from it;
+    // otherwise it must already hold exactly these records.  `records` must outlive the
+    // attachment and stay unchanged; any write or detach() ends it.
+    template <class Rec>
+    void attach_host(const Rec *records, uint64_t n, bool upload = true) {
+        check(iris_db_attach_host(h_, records, n, upload ? 1 : 0));
+    }
+    void detach_host() { check(iris_db_detach_host(h_)); }
 
 private:
     Device *dev_;
     iris_db_t *h_ = nullptr;
+};
+
+// ------------------------------------------------------------------ device groups (multi-GPU)
+
+// Devices searched together: the resolver's fan-out and sequential minimum
+// (src/main.rs:486-504, 616-621) over contiguous shards of one template database, the
+// per-shard winners all-gathered by the library's RCCL communicator.
+class Group {
+public:
+    explicit Group(const std::vector<int> &ordinals) {
+        check(iris_group_create(ordinals.data(), (uint32_t)ordinals.size(), &h_));
+    }
+    // one device of a multi-process group; `id` from unique_id() on rank 0
+    Group(int ordinal, uint32_t nranks, uint32_t rank, const std::array<uint8_t, IRIS_GROUP_ID_BYTES> &id) {
+        check(iris_group_create_rank(ordinal, nranks, rank, id.data(), &h_));
+    }
+    static std::array<uint8_t, IRIS_GROUP_ID_BYTES> unique_id() {
+        std::array<uint8_t, IRIS_GROUP_ID_BYTES> id{};
+        check(iris_group_unique_id(id.data()));
+        return id;
+    }
+    ~Group() {
+        if (h_) iris_group_destroy(h_);
+    }
+    Group(const Group &) = delete;
+    Group &operator=(const Group &) = delete;
+    iris_group_t *handle() const { return h_; }
+
+private:
+    iris_group_t *h_ = nullptr;
+};
+
+class GroupPendingSearch {
+public:
+    explicit GroupPendingSearch(iris_group_pending_t *p) : p_(p) {}
+    GroupPendingSearch(GroupPendingSearch &&o) noexcept : p_(o.p_) { o.p_ = nullptr; }
+    GroupPendingSearch(const GroupPendingSearch &) = delete;
+    GroupPendingSearch &operator=(const GroupPendingSearch &) = delete;
+    ~GroupPendingSearch() {
+        if (p_) (void)iris_group_pending_wait(p_, nullptr);
+    }
+    Match wait() {
+        if (!p_) throw Error(IRIS_E_ARG, "GroupPendingSearch::wait called twice");
+        Match m{};
+        iris_group_pending_t *p = p_;
+        p_ = nullptr;
+        check(iris_group_pending_wait(p, &m));
+        return m;
+    }
+
+private:
+    iris_group_pending_t *p_;
+};
+
+// `total` templates split into ranks x shards_per_device contiguous shards over a Group
+class ShardedDatabase {
+public:
+    ShardedDatabase(Group &g, uint64_t total, int layout = IRIS_LAYOUT_DEFAULT, uint32_t shards_per_device = 1) {
+        check(iris_group_db_create(g.handle(), IRIS_KIND_TEMPLATES, total, layout, shards_per_device, &h_));
+    }
+    ~ShardedDatabase() {
+        if (h_) iris_group_db_destroy(h_);
+    }
+    ShardedDatabase(const ShardedDatabase &) = delete;
+    ShardedDatabase &operator=(const ShardedDatabase &) = delete;
+    void generate(uint64_t seed) { check(iris_group_db_generate(h_, seed)); }
+    void write(uint64_t index, const Template *records, uint64_t n) { check(iris_group_db_write(h_, index, records, n)); }
+    void load_file(const std::string &path, uint64_t first = 0) { check(iris_group_db_load_file(h_, path.c_str(), first)); }
+    Match search(const Template &query) {
+        Match m{};
+        check(iris_group_template_search(h_, query.c(), &m));
+        return m;
+    }
+    GroupPendingSearch search_async(const Template &query) {
+        iris_group_pending_t *p = nullptr;
+        check(iris_group_template_search_async(h_, query.c(), &p));
+        return GroupPendingSearch(p);
+    }
+    std::vector<Match> batch_search(const std::vector<Template> &queries) {
+        std::vector<Match> out(queries.size());
+        static_assert(sizeof(Template) == sizeof(iris_template_t), "Template is the reference's 3200-B record");
+        check(iris_group_template_batch_search(h_, queries.empty() ? nullptr : queries[0].c(), (uint32_t)queries.size(),
+                                               out.data()));
+        return out;
+    }
+
+private:
+    iris_group_db_t *h_ = nullptr;
 };
 
 // ------------------------------------------------------------------ engines (src/lib.rs:28-80)

@@ -259,6 +259,40 @@ std::vector<Case> cases() {
              const Match ta = ps.wait();
              CHECK(ta.index == 33 && ta.distance == 0.0 && ta.rotation == 4);
          }},
+        // the participant / resolver loop (src/main.rs:426-431, 511-516) over an attached array
+        {"main::attached_chunks", true, [] {
+             const Template q = gen_template();
+             std::vector<Bits> masks;
+             for (int i = 0; i < 300; ++i) masks.push_back(gen_bits());
+             Device &dev = Device::default_device();
+             Database mdb(dev, IRIS_KIND_MASKS, masks.size());
+             mdb.attach_host(masks.data(), masks.size());
+             MasksEngine eng(q.mask, dev);
+             for (std::size_t a = 0; a < masks.size(); a += 70) {
+                 const std::size_t b = std::min(masks.size(), a + 70);
+                 std::vector<Rotations> out(b - a);
+                 check(iris_engine_batch_process_host(eng.handle(), masks.data() + a, b - a, out[0].data()));
+                 for (std::size_t i = a; i < b; i += 13)
+                     for (int k = 0; k < 31; ++k) CHECK(out[i - a][k] == q.mask.rotated(k - 15).dot(masks[i]));
+             }
+         }},
+        // the resolver's cross-participant minimum (src/main.rs:616-621) over 5 logical shards
+        {"main::sharded_search", true, [] {
+             const Template q = gen_template();
+             std::vector<Template> db;
+             for (int i = 0; i < 500; ++i) db.push_back(gen_template());
+             db[401] = q.rotated(-9);
+             db[99] = q.rotated(-9);  // an equal distance in an earlier shard: the lower index wins
+             Group g({0});
+             ShardedDatabase sdb(g, db.size(), IRIS_LAYOUT_DEFAULT, 5);
+             sdb.write(0, db.data(), db.size());
+             const Match m = sdb.search(q);
+             CHECK(m.index == 99 && m.distance == 0.0 && m.rotation == -9);
+             GroupPendingSearch p = sdb.search_async(q);
+             CHECK(p.wait().index == 99);
+             const std::vector<Match> b = sdb.batch_search({q, db[7]});
+             CHECK(b.size() == 2 && b[0].index == 99 && b[1].index == 7 && b[1].distance == 0.0);
+         }},
     };
 }
 

@@ -23,11 +23,13 @@ RUST = ROOT / "bindings" / "rust"
 HEADER = ROOT / "include" / "iris_hip.h"
 
 C_BASE = {"void", "char", "int", "double", "size_t", "uint8_t", "uint16_t", "uint32_t", "uint64_t", "int32_t",
-          "iris_device_t", "iris_db_t", "iris_engine_t", "iris_pending_t", "iris_match_t", "iris_template_t"}
+          "iris_device_t", "iris_db_t", "iris_engine_t", "iris_pending_t", "iris_match_t", "iris_template_t",
+          "iris_group_t", "iris_group_db_t", "iris_group_pending_t"}
 RUST_TO_C = {"c_void": "void", "c_char": "char", "c_int": "int", "f64": "double", "usize": "size_t", "u8": "uint8_t",
              "u16": "uint16_t", "u32": "uint32_t", "u64": "uint64_t", "i32": "int32_t", "IrisDevice": "iris_device_t",
              "IrisDb": "iris_db_t", "IrisEngine": "iris_engine_t", "IrisPending": "iris_pending_t",
-             "IrisMatch": "iris_match_t", "IrisTemplate": "iris_template_t"}
+             "IrisMatch": "iris_match_t", "IrisTemplate": "iris_template_t", "IrisGroup": "iris_group_t",
+             "IrisGroupDb": "iris_group_db_t", "IrisGroupPending": "iris_group_pending_t"}
 
 
 def _strip_c_comments(s):
@@ -234,3 +236,28 @@ def test_reference_patch_applies(tmp_path):
     r = subprocess.run(["patch", "-p1", "--dry-run", "-i", str(RUST / "reference.patch")], cwd=tmp_path,
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+@pytest.mark.skipif(not pathlib.Path("/root/reference/src/lib.rs").exists(),
+                    reason="reference sources not present (GPU box)")
+def test_reference_items_the_binding_relies_on():
+    """Textual checks of the reference items bindings/rust uses (what rustc would check):
+    crate-visible LIMBS (arch/hip.rs), public tuple fields of Bits / EncodedBits
+    (engines.rs passes query.0), a Copy Template (TemplateEngine keeps its query), and the
+    exact `pub use` / struct lines reference.patch rewrites."""
+    ref = pathlib.Path("/root/reference/src")
+    bits = (ref / "bits.rs").read_text()
+    assert re.search(r"pub(\(crate\))? const LIMBS: usize", bits)
+    assert "pub struct Bits(pub [u64; LIMBS]);" in bits
+    assert re.search(r"pub struct EncodedBits\(pub \[u16; BITS\]\);", (ref / "encoded_bits.rs").read_text())
+    tmpl = (ref / "template.rs").read_text()
+    derive = re.search(r"#\[derive\(([^)]*)\)\]\s*pub struct Template", tmpl, flags=re.S)
+    assert derive and re.search(r"\bCopy\b", derive.group(1))
+    assert "pub use generic::{dot_bool, dot_u16};" in (ref / "arch" / "mod.rs").read_text()
+    lib = (ref / "lib.rs").read_text()
+    for line in ("pub use crate::{bits::Bits, encoded_bits::EncodedBits, template::Template};",
+                 "pub struct DistanceEngine {", "pub struct MasksEngine {", "impl DistanceEngine {",
+                 "impl MasksEngine {", "mod template;"):
+        assert line in lib, line
+    patch = (RUST / "reference.patch").read_text()
+    assert "+pub use hip::{dot_bool, dot_u16};" in patch and "+pub use iris_hip::engines::{DistanceEngine, MasksEngine};" in patch
