@@ -220,7 +220,7 @@ void device_teardown(iris_device *d) {
         std::lock_guard<std::recursive_mutex> g(d->mu);
         (void)hipSetDevice(d->ordinal);
         (void)hipStreamSynchronize(d->stream);
-        for (DevBuf *b : {&d->partials, &d->result, &d->staging, &d->out_a, &d->out_b})
+        for (DevBuf *b : {&d->partials, &d->result, &d->staging, &d->out_a, &d->out_b, &d->ticket})
             if (b->p) (void)hipFree(b->p);
         if (d->aux) (void)hipStreamSynchronize(d->aux);
         for (int b = 0; b < 2; ++b) {
@@ -300,6 +300,15 @@ int iris_device_open(int ordinal, iris_device_t **out) {
     if (!d) return fail(IRIS_E_NOMEM, "out of host memory");
     d->ordinal = ordinal;
     hipError_t e = hipSetDevice(ordinal);
+    // IRIS_SCHEDULE = spin | yield | blocking: how host waits on this device behave (diagnostic;
+    // takes effect only before the process's first context on the device)
+    if (const char *sch = getenv("IRIS_SCHEDULE")) {
+        const unsigned f = !strcmp(sch, "spin") ? hipDeviceScheduleSpin
+                           : !strcmp(sch, "yield") ? hipDeviceScheduleYield
+                           : !strcmp(sch, "blocking") ? hipDeviceScheduleBlockingSync : hipDeviceScheduleAuto;
+        (void)hipSetDeviceFlags(f);
+        (void)hipGetLastError();
+    }
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
         delete d;
@@ -774,6 +783,27 @@ int iris_api::search_enqueue(iris_engine_t *e, const iris_db_t *db, uint64_t fir
     if (n == 0) return 0;
     LaunchRange r{first, n};
     const int layout = db->k.layout;
+    if (layout == IRIS_LAYOUT_TILES && fused_search_ok(r)) {
+        // small range: the kernel's last workgroup reduces and writes dst itself (no reduce launch)
+        CHK(ensure_ticket(d));
+        CHK(ensure(d->partials, (size_t)mfma_search_partials(r) * sizeof(Partial)));
+        const FusedFinish fin{(uint32_t *)d->ticket.p, dst, idx_base};
+        uint32_t written = 0;
+        CHK(timed(d, "template_search", n, [&] {
+            return launch_template_mfma_search(d->stream, db->data, e->qfrag, r, dist_dev, (Partial *)d->partials.p,
+                                               &written, &fin);
+        }));
+        if (!side) return 0;
+        // later side-stream work (a group's all-gather) and `done` follow the kernel
+        CHK(ensure_aux(d));
+        const int b = d->apart_next;
+        d->apart_next ^= 1;
+        if (!d->apart_written[b]) HIPCHK(hipEventCreateWithFlags(&d->apart_written[b], hipEventDisableTiming));
+        HIPCHK(hipEventRecord(d->apart_written[b], d->stream));
+        HIPCHK(hipStreamWaitEvent(d->aux, d->apart_written[b], 0));
+        if (done) HIPCHK(hipEventRecord(done, d->aux));
+        return 0;
+    }
     const uint32_t np = layout == IRIS_LAYOUT_TILES   ? mfma_search_partials(r)
                         : layout == IRIS_LAYOUT_TRITS ? trits_search_partials(r)
                                                       : search_partials(r);

@@ -67,6 +67,9 @@ struct iris_device {
     std::vector<Pending> pending;
     std::vector<hipEvent_t> event_pool;
     DevBuf partials, result, staging, out_a, out_b;
+    // zeroed device word of the fused (last-workgroup) search reduce; searches on the stream
+    // are serialised, and each launch leaves it zeroed
+    DevBuf ticket;
     // pinned host words the reduce kernels write their final Partials into (no
     // device-to-host copy between the last kernel and the stream sync)
     void *host_result = nullptr;
@@ -244,6 +247,13 @@ inline void db_detach(iris_db *db) {
     v.erase(std::remove(v.begin(), v.end(), db), v.end());
     db->host_base = 0;
     db->host_n = 0;
+}
+
+inline int ensure_ticket(iris_device *d) {
+    if (d->ticket.p) return 0;
+    CHK(ensure(d->ticket, 256));
+    HIPCHK(hipMemsetAsync(d->ticket.p, 0, 256, d->stream));
+    return 0;
 }
 
 inline int ensure_aux(iris_device *d) {

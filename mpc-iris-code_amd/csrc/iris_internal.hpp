@@ -269,8 +269,18 @@ int launch_template_counts(void *stream, const void *db, const void *qtab, Launc
                            uint16_t *den_out);
 int launch_template_mfma_counts(void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *num_out,
                                 uint16_t *den_out);
+// Fused finish of a small search (grids of at most kFusedReduceMax workgroups): the last
+// workgroup to finish reduces the partials and writes the winner (idx + idx_base) to dst;
+// ticket is a zeroed device word that the kernel leaves zeroed.
+struct FusedFinish {
+    uint32_t *ticket;
+    Partial *dst;
+    uint64_t idx_base;
+};
+constexpr uint32_t kFusedReduceMax = 4096;
+bool fused_search_ok(LaunchRange r);
 int launch_template_mfma_search(void *stream, const void *db, const void *qfrag, LaunchRange r, double *dist_out,
-                                Partial *partials, uint32_t *n_partials);
+                                Partial *partials, uint32_t *n_partials, const FusedFinish *fin = nullptr);
 uint32_t mfma_search_partials(LaunchRange r);
 // nq = 2 queries per streamed pass; partials [nq][*n_partials]
 uint32_t multi_search_partials(LaunchRange r, int nq);

@@ -97,12 +97,14 @@ enum { MF_COUNTS = 0, MF_SEARCH = 1 };
 // chunk groups [w' * 100 / KS, +100 / KS) of tile blockIdx.x * (4 / KS) + w / KS (w' = w % KS)
 // -- and the partial sums (exact integers in f32) meet in LDS before the epilogue, so a range of
 // a few hundred tiles still puts several waves on every SIMD.
-template <int MODE, int T = kMfmaTiles, int KS = 1>
+// FUSED (search, small grids): the last workgroup to finish folds every workgroup's
+// partial and writes the winner to fin.dst itself (iris_device.hpp, fold_partials_last).
+template <int MODE, int T = kMfmaTiles, int KS = 1, bool FUSED = false>
 __global__ void __launch_bounds__(256, kMfmaWgs)
     template_mfma_kernel(const uint4 *__restrict__ db, const uint4 *__restrict__ qfrag, uint64_t tile0,
                          uint64_t ntiles, uint64_t first, uint64_t end, uint16_t *__restrict__ num_out,
                          uint16_t *__restrict__ den_out, double *__restrict__ dist_out,
-                         Partial *__restrict__ partials) {
+                         Partial *__restrict__ partials, FusedFinish fin) {
     static_assert(KS == 1 || (T == 1 && kWaveSlots % KS == 0 && kPlaneGroups % KS == 0), "K-split geometry");
     const int lane = threadIdx.x & 63;
     const int wslot = threadIdx.x >> 6;
@@ -240,13 +242,14 @@ __global__ void __launch_bounds__(256, kMfmaWgs)
         __shared__ Partial sh[kWaveSlots];
         if (lane == 0) sh[wslot] = best;
         __syncthreads();
+        Partial b = sh[0];
         if (threadIdx.x == 0) {
-            Partial b = sh[0];
 #pragma unroll
             for (int w = 1; w < kWaveSlots; ++w)
                 if (partial_better_dev(sh[w], b)) b = sh[w];
-            partials[blockIdx.x] = b;
+            if constexpr (!FUSED) partials[blockIdx.x] = b;
         }
+        if constexpr (FUSED) fold_partials_last(partials, b, fin);
     }
 }
 
@@ -540,21 +543,33 @@ int launch_template_mfma_counts(void *stream, const void *db, const void *qfrag,
                 : t.tiles_per_wave == 1 ? template_mfma_kernel<MF_COUNTS, 1> : template_mfma_kernel<MF_COUNTS>;
     hipLaunchKernelGGL(kern, dim3((uint32_t)t.grid), dim3(256), 0, (hipStream_t)stream,
                        (const uint4 *)db, (const uint4 *)qfrag, t.tile0, t.ntiles, r.first, r.first + r.n, num_out,
-                       den_out, (double *)nullptr, (Partial *)nullptr);
+                       den_out, (double *)nullptr, (Partial *)nullptr, FusedFinish{});
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int launch_template_mfma_search(void *stream, const void *db, const void *qfrag, LaunchRange r, double *dist_out,
-                                Partial *partials, uint32_t *n_partials) {
+                                Partial *partials, uint32_t *n_partials, const FusedFinish *fin) {
     const TileRange t = tile_range(r);
     *n_partials = (uint32_t)t.grid;
     if (r.n == 0) return 0;
-    auto kern = t.ksplit > 1 ? template_mfma_kernel<MF_SEARCH, 1, 4>
-                : t.tiles_per_wave == 1 ? template_mfma_kernel<MF_SEARCH, 1> : template_mfma_kernel<MF_SEARCH>;
+    const bool fused = fin && t.grid <= kFusedReduceMax;
+    if (fin && !fused) return -1;  // the caller asks fused_search_ok() first
+    auto kern = fused ? (t.ksplit > 1 ? template_mfma_kernel<MF_SEARCH, 1, 4, true>
+                         : t.tiles_per_wave == 1 ? template_mfma_kernel<MF_SEARCH, 1, 1, true>
+                                                 : template_mfma_kernel<MF_SEARCH, kMfmaTiles, 1, true>)
+                      : (t.ksplit > 1 ? template_mfma_kernel<MF_SEARCH, 1, 4>
+                         : t.tiles_per_wave == 1 ? template_mfma_kernel<MF_SEARCH, 1> : template_mfma_kernel<MF_SEARCH>);
     hipLaunchKernelGGL(kern, dim3((uint32_t)t.grid), dim3(256), 0, (hipStream_t)stream,
                        (const uint4 *)db, (const uint4 *)qfrag, t.tile0, t.ntiles, r.first, r.first + r.n,
-                       (uint16_t *)nullptr, (uint16_t *)nullptr, dist_out, partials);
+                       (uint16_t *)nullptr, (uint16_t *)nullptr, dist_out, partials, fin ? *fin : FusedFinish{});
     return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// test hook: IRIS_FUSED_REDUCE=0 runs small searches with the separate reduce kernel
+bool fused_search_ok(LaunchRange r) {
+    const char *f = getenv("IRIS_FUSED_REDUCE");
+    if (f && f[0] == '0') return false;
+    return r.n > 0 && tile_range(r).grid <= kFusedReduceMax;
 }
 
 }  // namespace iris

@@ -78,3 +78,36 @@ def test_fuzz_masks_and_shares(device, monkeypatch, tiles_per_wave):
                 assert m.index == idx and bits_eq(m.distance, best), (total, first, n, layout)
             else:
                 assert m.index == 2**64 - 1
+
+
+def test_fused_reduce_equals_reduce_kernel(device, monkeypatch):
+    """Small searches finish in the kernel (its last workgroup folds the partials, published
+    with system-scope atomics across the XCDs): 300 random queries over ranges up to the
+    fused limit (4096 workgroups) must equal the separate reduce kernel and the oracle."""
+    import iris_hip as ih
+    from oracle import oracle_c as oc
+
+    n = 140_000
+    rng = np.random.default_rng(12)
+    ref = oc.gen_templates(5, 0, n)
+    with ih.Database(device, ih.KIND_TEMPLATES, n) as db:
+        db.generate(n, 5)
+        for it in range(300):
+            q = oc.gen_templates(1000 + it, 0, 1)[0]
+            first = int(rng.integers(0, n - 1))
+            cnt = int(rng.integers(1, min(n - first, 130_000) + 1))
+            if it % 4 == 0:  # a planted answer somewhere in the range
+                site = first + int(rng.integers(0, cnt))
+                p = ih.Bits(q[:200]).rotated(int(rng.integers(-15, 16))).limbs
+                m = ih.Bits(q[200:]).rotated(0).limbs
+                db.write(site, np.concatenate([p, m])[None, :])
+                ref[site] = np.concatenate([p, m])
+            with ih.TemplateEngine(device, q) as eng:
+                monkeypatch.setenv("IRIS_FUSED_REDUCE", "1")
+                a = eng.search(db, first, cnt, index_base=7)
+                monkeypatch.setenv("IRIS_FUSED_REDUCE", "0")
+                b = eng.search(db, first, cnt, index_base=7)
+            assert (a.index, a.num, a.den, a.rotation) == (b.index, b.num, b.den, b.rotation), (it, a, b)
+            if it % 25 == 0:
+                best, idx = oc.argmin(oc.template_distances(q, ref[first:first + cnt]))
+                assert a.index == idx + first + 7 and a.distance == best
