@@ -362,8 +362,8 @@ def batch_pmc():
     """SQ-counter figures of the 1024-query batched launch from the committed profile
     (tools/pmc_batch.sh, profiles/r02_pmc_batch_sq.json): VALU and LDS instructions per MFMA
     and the bytes fetched beyond L2, reported beside the MFMA roofline fraction."""
-    p = ROOT / "profiles" / "r02_pmc_batch_sq.json"
     try:
+        p = sorted((ROOT / "profiles").glob("r*_pmc_batch_sq.json"))[-1]  # the newest round's
         j = json.loads(p.read_text())
     except Exception:
         return None
@@ -1076,7 +1076,7 @@ def main():
                          ("shares", "tiles"): "shares_mfma_kernel (i8 MFMA)",
                          ("shares", "lanes"): "shares_kernel (VALU v_pk_mad_u16)",
                          ("search", "trits"): "trits_mfma_kernel<TR_SEARCH> (fp4 MFMA, 3-state bytes decoded via LDS table)",
-                         ("batch", "tiles"): "batch_lds_kernel (fp4 MFMA GEMM, LDS query-fragment ring)"}[(args.workload, args.layout)],
+                         ("batch", "tiles"): "batch_lds_kernel<8,2,2,2> (fp4 MFMA GEMM: 2-query groups x 16-tile N-groups, 2 x 2 per wave, LDS query-fragment ring)"}[(args.workload, args.layout)],
                 "avg_ms": avg_ms, "launches": launches, "per_device_avg_ms": per_dev_ms,
                 "reduce_avg_ms": rms / max(1, launches),
                 "frac_of_guide_copy_bw": achieved / HBM_GUIDE_COPY_GBS,

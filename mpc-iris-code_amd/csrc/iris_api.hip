@@ -1084,7 +1084,7 @@ int iris_template_batch_search(iris_engine_t *e, const iris_db_t *db, uint64_t f
     }
     LaunchRange r{first, n};
     const BatchGeometry geo = batch_geometry(r, e->nq);
-    const uint32_t nqp = geo.nqg * batch_query_group();
+    const uint32_t nqp = geo.nqg * geo.qper;
     std::vector<Partial> res(nqp);
     if (n > 0) {
         CHK(ensure(d->partials, (size_t)nqp * geo.G * sizeof(Partial)));

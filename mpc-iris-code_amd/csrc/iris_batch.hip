@@ -371,28 +371,36 @@ __global__ void __launch_bounds__(256) batch_reduce_kernel(const Partial *__rest
 #define IRIS_BATCH2_ROLL 1
 #endif
 namespace lds2 {
-constexpr int kBQ = 4;                   // queries per workgroup (must equal batch_kernel's: padding)
 constexpr int kGP = IRIS_BATCH2_GP;      // chunk pairs per K-step
 constexpr int kSteps = kPlaneGroups / kGP;
-constexpr int kArows = kBQ * kGP;        // compact A rows (1 KB) per K-step
-constexpr int kTilesPerGroup = 8;        // template tiles per N-group (NW waves x WT tiles)
 static_assert(kPlaneGroups % kGP == 0, "K-step must tile the 100 chunk pairs");
-static_assert(kBQ == IRIS_BATCH_BQ, "query groups must pad like batch_kernel's");
 }  // namespace lds2
 
-// NW waves x WT tiles per wave = 8 tiles per N-group: NW = 8, WT = 1 (two waves per SIMD,
-// 128 accumulator registers) or NW = 4, WT = 2 (one wave per SIMD, 256 accumulators).
-template <int NW, int WT>
+// Waves: QW = kBQ / WQL query sets x NW / QW tile sets; a wave holds WQL queries x WT tiles
+// and the tile sets x WT = 8 tiles per N-group.  NW = 8, WQL = 4, WT = 1: every wave reads
+// all four queries' fragments from LDS (one fragment read per MFMA pair); NW = 8, WQL = 2,
+// WT = 2: each fragment read feeds two tiles (half the LDS reads per MFMA), each template
+// tile is loaded and expanded by the two waves of its tile set; both 128 accumulators.
+// NW = 4, WQL = 4, WT = 2: one wave per SIMD, 256 accumulators.
+// BQL = queries per workgroup (a query group): 4 (tiles per N-group = 8 with the shapes
+// above) or 2 with WQL = 2, WT = 2 (16 tiles per N-group: each query tile read from beyond L2
+// is applied to twice the templates, half the A traffic per query).
+template <int NW, int WT, int WQL = 4, int BQL = 4>
 __global__ void __launch_bounds__(64 * NW, 1)
     batch_lds_kernel(const uint4 *__restrict__ db, const uint4 *__restrict__ qtiles, uint64_t tile0, uint64_t ntiles,
                      uint64_t first, uint64_t end, uint32_t nqg, uint32_t G, Partial *__restrict__ partials) {
     using namespace lds2;
-    static_assert(NW * WT == kTilesPerGroup && kArows % NW == 0, "geometry");
+    constexpr int kBQ = BQL;
+    constexpr int kArows = kBQ * kGP;               // compact A rows (1 KB) per K-step
+    constexpr int QW = kBQ / WQL;                   // query sets
+    constexpr int kTilesPerGroup = (NW / QW) * WT;  // template tiles per N-group
+    static_assert(kBQ % WQL == 0 && NW % QW == 0 && kArows % NW == 0 && IRIS_BATCH_BQ % kBQ == 0, "geometry");
     constexpr int kAper = kArows / NW;  // compact A rows per wave and K-step
     // [stage][chunk pair][query][den h0, enc h0, den h1, enc h1][lane]: 2 x kGP x 16 KB
     __shared__ uint4 afrag[2][kGP][kBQ][4][64];
 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int qset = w % QW, tset = w / QW;  // this wave's queries qset * WQL + qi, tiles tset * WT + t
     const uint32_t qg = blockIdx.x % nqg, gi = blockIdx.x / nqg;
     const uint64_t ngroups = (ntiles + kTilesPerGroup - 1) / kTilesPerGroup;
     const uint32_t my_groups = gi < ngroups ? (uint32_t)((ngroups - gi + G - 1) / G) : 0;
@@ -421,7 +429,7 @@ __global__ void __launch_bounds__(64 * NW, 1)
     };
     auto b_row = [&](uint32_t s, int t) {  // tile t of this wave, chunk pair 0 of K-step s
         const uint32_t j = group_of(s), k = s % kSteps;
-        const uint64_t trel = (gi + (uint64_t)j * G) * kTilesPerGroup + w * WT + t;
+        const uint64_t trel = (gi + (uint64_t)j * G) * kTilesPerGroup + tset * WT + t;
         return db + (tile0 + (trel < ntiles ? trel : ntiles - 1)) * (uint64_t)kTileU4 + (k * kGP) * 64 + lane;
     };
     // compact A row -> fp4 den / encode fragments of both chunks (the expansion of batch_kernel)
@@ -458,17 +466,17 @@ __global__ void __launch_bounds__(64 * NW, 1)
 
     // running best per lane and query across the walk: (num | den << 16, N-group x tile << 5 | rotation);
     // den 0 = none yet
-    uint32_t run_nd[kBQ], run_jr[kBQ];
+    uint32_t run_nd[WQL], run_jr[WQL];
 #pragma unroll
-    for (int qi = 0; qi < kBQ; ++qi) {
+    for (int qi = 0; qi < WQL; ++qi) {
         run_nd[qi] = 1;  // (num 1, den 0): none
         run_jr[qi] = 0;
     }
     Partial wave_best;
-    v16f den[kBQ][WT], sacc[kBQ][WT];
+    v16f den[WQL][WT], sacc[WQL][WT];
     auto zero = [&] {
 #pragma unroll
-        for (int qi = 0; qi < kBQ; ++qi)
+        for (int qi = 0; qi < WQL; ++qi)
 #pragma unroll
             for (int t = 0; t < WT; ++t)
 #pragma unroll
@@ -514,12 +522,12 @@ __global__ void __launch_bounds__(64 * NW, 1)
             return form ? make_uint4(q.x & 0xAAAAAAAAu, q.y & 0xAAAAAAAAu, q.z & 0xAAAAAAAAu, q.w ^ qi)
                         : make_uint4(q.x & 0x22222222u, q.y & 0x11111111u, q.z & 0x22222222u, q.w & qi);
 #else
-            return st[b >> 1][qi][2 * (b & 1) + form][lane];
+            return st[b >> 1][qset * WQL + qi][2 * (b & 1) + form][lane];
 #endif
         };
-        uint4 fa[kBQ], fe[kBQ];
+        uint4 fa[WQL], fe[WQL];
 #pragma unroll
-        for (int qi = 0; qi < kBQ; ++qi) {
+        for (int qi = 0; qi < WQL; ++qi) {
             fa[qi] = frag(0, 0, qi);
             fe[qi] = frag(0, 1, qi);
         }
@@ -540,9 +548,9 @@ __global__ void __launch_bounds__(64 * NW, 1)
 #pragma unroll
                 for (int t = 0; t < WT; ++t) bq[t][b >> 1] = b_row(s1, t)[(b >> 1) * 64];
             }
-            uint4 na[kBQ], ne[kBQ];
+            uint4 na[WQL], ne[WQL];
 #pragma unroll
-            for (int qi = 0; qi < kBQ; ++qi) {
+            for (int qi = 0; qi < WQL; ++qi) {
                 if (!IRIS_BATCH2_ROLL) {
                     fa[qi] = frag(b, 0, qi);
                     fe[qi] = frag(b, 1, qi);
@@ -559,7 +567,7 @@ __global__ void __launch_bounds__(64 * NW, 1)
             __builtin_amdgcn_sched_barrier(0);
             if (nb && IRIS_BATCH2_ROLL) {
 #pragma unroll
-                for (int qi = 0; qi < kBQ; ++qi) {
+                for (int qi = 0; qi < WQL; ++qi) {
                     fa[qi] = na[qi];
                     fe[qi] = ne[qi];
                 }
@@ -576,11 +584,11 @@ __global__ void __launch_bounds__(64 * NW, 1)
             const int h = lane >> 5;
 #pragma unroll
             for (int t = 0; t < WT; ++t) {
-                const uint64_t trel = (gi + (uint64_t)j * G) * kTilesPerGroup + w * WT + t;
+                const uint64_t trel = (gi + (uint64_t)j * G) * kTilesPerGroup + tset * WT + t;
                 const uint64_t tg = (tile0 + trel) * 32 + (lane & 31);
                 const bool valid = live && trel < ntiles && tg >= first && tg < end;
 #pragma unroll
-                for (int qi = 0; qi < kBQ; ++qi) {
+                for (int qi = 0; qi < WQL; ++qi) {
                     // (bn, bd) = (1, 0) is "none": a row with den 0 (no jointly valid bit; also the
                     // zero row k = 31) is (0, 0) and never wins, n * 0 < 1 * d holds for any real
                     // candidate, so the scan needs no validity tests
@@ -616,11 +624,11 @@ __global__ void __launch_bounds__(64 * NW, 1)
     {
         Partial best = partial_none();
 #pragma unroll
-        for (int qi = 0; qi < kBQ; ++qi) {
+        for (int qi = 0; qi < WQL; ++qi) {
             Partial c = partial_none();
             if (run_nd[qi] >> 16) {
                 const uint32_t jt = run_jr[qi] >> 5, jj = jt / WT, t = jt - jj * WT;
-                const uint64_t trel = (gi + (uint64_t)jj * G) * kTilesPerGroup + w * WT + t;
+                const uint64_t trel = (gi + (uint64_t)jj * G) * kTilesPerGroup + tset * WT + t;
                 c.num = run_nd[qi] & 0xFFFFu;
                 c.den = run_nd[qi] >> 16;
                 c.rot = (int)(run_jr[qi] & 31u);
@@ -637,21 +645,27 @@ __global__ void __launch_bounds__(64 * NW, 1)
     }
 
     __syncthreads();
-    Partial *sP = (Partial *)&afrag[0][0][0][0][0];  // [wave][query]
-    if (lane < kBQ) sP[w * kBQ + lane] = wave_best;
+    Partial *sP = (Partial *)&afrag[0][0][0][0][0];  // [wave][query of the wave]
+    if (lane < WQL) sP[w * WQL + lane] = wave_best;
     __syncthreads();
-    if (tid < kBQ) {
-        Partial b = sP[tid];
-        for (int ww = 1; ww < NW; ++ww)
-            if (partial_better_dev(sP[ww * kBQ + tid], b)) b = sP[ww * kBQ + tid];
+    if (tid < kBQ) {  // query tid: the waves of its query set, one per tile set
+        const int qs = tid / WQL, qi = tid % WQL;
+        Partial b = sP[qs * WQL + qi];
+        for (int ww = qs + QW; ww < NW; ww += QW)
+            if (partial_better_dev(sP[ww * WQL + qi], b)) b = sP[ww * WQL + qi];
         partials[(uint64_t)(qg * kBQ + tid) * G + gi] = b;
     }
 }
 
-// 2 = batch_lds_kernel (default), 1 = batch_kernel; read per launch so tests can run both
+// IRIS_BATCH_KERNEL (read per launch, so tests run every form): 4 = batch_lds_kernel with
+// 2-query groups x 16-tile N-groups, 2 x 2 per wave (default: half the LDS fragment reads and
+// half the query-tile bytes per template of 2; 3.5 % faster, profiles/r03_batch_variants.txt);
+// 2 = batch_lds_kernel 4-query groups x 8 tiles, 4 x 1 per wave (round 2); 3 = 4-query groups,
+// 2 x 2 per wave; 1 = batch_kernel (LDS-DMA staged, round 1)
 static int batch_kernel_choice() {
     const char *e = getenv("IRIS_BATCH_KERNEL");
-    return e && atoi(e) == 1 ? 1 : 2;
+    const int k = e ? atoi(e) : 4;
+    return k >= 1 && k <= 4 ? k : 4;
 }
 
 uint32_t batch_query_group() { return BQ; }
@@ -661,8 +675,11 @@ BatchGeometry batch_geometry(LaunchRange r, uint32_t nq) {
     g.tile0 = r.first / 32;
     const uint64_t tile1 = (r.first + r.n + 31) / 32;
     g.ntiles = tile1 - g.tile0;
-    g.nqg = (nq + BQ - 1) / BQ;
-    const uint64_t ngroups = (g.ntiles + BT - 1) / BT;
+    const int kc = batch_kernel_choice();
+    g.qper = kc == 4 ? 2 : BQ;  // queries per query group
+    g.nqg = (nq + g.qper - 1) / g.qper;
+    const uint32_t tiles_per_group = kc == 1 ? BT : kc == 4 ? 16 : 8;
+    const uint64_t ngroups = (g.ntiles + tiles_per_group - 1) / tiles_per_group;
     // batch_kernel: ~2 workgroups per CU in total; batch_lds_kernel (one 128-KB-LDS workgroup
     // per CU): one round of workgroups
     const uint64_t want = batch_kernel_choice() >= 2 ? resident_blocks(1) : 512;
@@ -690,12 +707,20 @@ int launch_batch(void *stream, const void *db, const void *qtiles, LaunchRange r
         hipLaunchKernelGGL((batch_lds_kernel<8, 1>), dim3(g.nqg * g.G), dim3(64 * 8), 0, (hipStream_t)stream,
                            (const uint4 *)db, (const uint4 *)qtiles, g.tile0, g.ntiles, r.first, r.first + r.n, g.nqg,
                            g.G, partials);
+    else if (kc == 3)  // 2 queries x 2 tiles per wave: half the LDS fragment reads per MFMA
+        hipLaunchKernelGGL((batch_lds_kernel<8, 2, 2>), dim3(g.nqg * g.G), dim3(64 * 8), 0, (hipStream_t)stream,
+                           (const uint4 *)db, (const uint4 *)qtiles, g.tile0, g.ntiles, r.first, r.first + r.n, g.nqg,
+                           g.G, partials);
+    else if (kc == 4)  // 2-query groups x 16-tile N-groups: half the query-tile traffic beyond L2
+        hipLaunchKernelGGL((batch_lds_kernel<8, 2, 2, 2>), dim3(g.nqg * g.G), dim3(64 * 8), 0, (hipStream_t)stream,
+                           (const uint4 *)db, (const uint4 *)qtiles, g.tile0, g.ntiles, r.first, r.first + r.n, g.nqg,
+                           g.G, partials);
     else
         hipLaunchKernelGGL(batch_kernel, dim3(g.nqg * g.G), dim3(64 * NW), 0, (hipStream_t)stream, (const uint4 *)db,
                            (const uint4 *)qtiles, g.tile0, g.ntiles, r.first, r.first + r.n, g.nqg, g.G, g.xqg,
                            partials);
     if (hipGetLastError() != hipSuccess) return -1;
-    hipLaunchKernelGGL(batch_reduce_kernel, dim3(g.nqg * BQ), dim3(256), 0, (hipStream_t)stream, partials, g.G, out,
+    hipLaunchKernelGGL(batch_reduce_kernel, dim3(g.nqg * g.qper), dim3(256), 0, (hipStream_t)stream, partials, g.G, out,
                        idx_base);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -309,7 +309,8 @@ int launch_masks_resolve(void *stream, const void *db, const void *qfrag, Launch
 uint32_t resolver_partials(uint64_t n);
 struct BatchGeometry {
     uint64_t tile0, ntiles;
-    uint32_t nqg, G;  // query groups of 4, workgroups per query group
+    uint32_t nqg, G;  // query groups, workgroups per query group
+    uint32_t qper;    // queries per query group (nqg * qper results; at most the engine's padding)
     uint32_t xqg;     // > 0: XCD-aware grid, xqg query groups per XCD at a time (iris_batch.hip)
 };
 BatchGeometry batch_geometry(LaunchRange r, uint32_t nq);
