@@ -410,8 +410,10 @@ __global__ void __launch_bounds__(64 * NW, 1)
     // K-step at time s is s mod kSteps for every wave (the A fragments in LDS are shared); waves
     // 4..7 start their first group at s = off and the workgroup walks off extra steps, in which
     // the idle waves' MFMAs run on re-read rows and are discarded.
-    const uint32_t off = (IRIS_BATCH2_STAGGER && NW == 8 && w >= NW / 2) ? (uint32_t)(kSteps / 2) : 0u;
-    const uint32_t walk = total ? total + ((IRIS_BATCH2_STAGGER && NW == 8) ? (uint32_t)(kSteps / 2) : 0u) : 0u;
+    // (the 2 x 2 per-wave shape runs 2 % faster without it: profiles/r03_batch_variants.txt)
+    constexpr bool kStagger = IRIS_BATCH2_STAGGER && NW == 8 && WQL == 4;
+    const uint32_t off = (kStagger && w >= NW / 2) ? (uint32_t)(kSteps / 2) : 0u;
+    const uint32_t walk = total ? total + (kStagger ? (uint32_t)(kSteps / 2) : 0u) : 0u;
     auto group_of = [&](uint32_t s) {  // this wave's N-group at time s (clamped while idle)
         const uint32_t r = s >= off ? (s - off) / kSteps : 0u;
         return r < my_groups ? r : my_groups - 1;
