@@ -25,7 +25,7 @@
 #if defined(IRIS_SHIPPED_BUILD)
 #if (defined(IRIS_MFMA_DIAG) && IRIS_MFMA_DIAG) || (defined(IRIS_BATCH_DIAG) && IRIS_BATCH_DIAG) || \
     (defined(IRIS_BATCH2_DIAG) && IRIS_BATCH2_DIAG) || (defined(IRIS_STORE_DIAG) && IRIS_STORE_DIAG) || \
-    (defined(IRIS_TRITS_DIAG) && IRIS_TRITS_DIAG)
+    (defined(IRIS_TRITS_DIAG) && IRIS_TRITS_DIAG) || (defined(IRIS_PREP_DIAG) && IRIS_PREP_DIAG)
 #error "diagnostic knob in the shipped libiris_hip.so"
 #endif
 #endif
