@@ -164,30 +164,37 @@ __device__ __forceinline__ Partial partial_none() {
 }
 
 // Last-workgroup reduction (a search's partials reduce without a second launch).  Thread 0
-// publishes this workgroup's partial with system-scope atomic stores (sc0 sc1: written
-// through to the memory side, coherent across the XCDs' L2s without an L2 writeback /
-// invalidate -- a full __threadfence here drops every XCD's L2, the L2-resident query
-// fragments with it, once per workgroup, and doubled a 20k-template search), waits for them
-// to complete, and takes a ticket with a system-scope atomic; the workgroup that draws
-// gridDim.x - 1 reads every partial with system-scope atomic loads, folds them in the
+// publishes this workgroup's partial with agent-scope atomic stores (sc1: written through
+// past the XCD's L2, coherent across the XCDs without an L2 writeback / invalidate -- a full
+// __threadfence here drops every XCD's L2, the L2-resident query fragments with it, once per
+// workgroup, and doubled a 20k-template search), waits for them to complete, and takes a
+// ticket with an agent-scope atomic add; the workgroup that draws gridDim.x - 1 reads every
+// partial with agent-scope (sc1) atomic loads (MI355X_MICROARCH.md, inter-workgroup
+// visibility: the first hand-off row), folds them in the
 // search order (exact fraction, then lowest index), writes the winner with idx + idx_base to
 // fin.dst (pinned host or device memory) and resets the ticket for the next launch.
+// agent scope (sc1 stores / loads, the form of MI355X_MICROARCH.md's first hand-off row) or
+// system scope (sc0 sc1: through to memory); IRIS_FUSED_SYSTEM=1 selects the latter
+#ifndef IRIS_FUSED_SYSTEM
+#define IRIS_FUSED_SYSTEM 0
+#endif
+#define IRIS_FUSED_SCOPE (IRIS_FUSED_SYSTEM ? __HIP_MEMORY_SCOPE_SYSTEM : __HIP_MEMORY_SCOPE_AGENT)
 __device__ __forceinline__ void publish_partial(Partial *p, const Partial &b) {
     uint64_t *w = (uint64_t *)p;
-    __hip_atomic_store(w, (uint64_t)b.num | ((uint64_t)b.den << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(w + 1, (uint64_t)(uint32_t)b.rot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(w + 2, b.idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(w, (uint64_t)b.num | ((uint64_t)b.den << 32), __ATOMIC_RELAXED, IRIS_FUSED_SCOPE);
+    __hip_atomic_store(w + 1, (uint64_t)(uint32_t)b.rot, __ATOMIC_RELAXED, IRIS_FUSED_SCOPE);
+    __hip_atomic_store(w + 2, b.idx, __ATOMIC_RELAXED, IRIS_FUSED_SCOPE);
 }
 __device__ __forceinline__ Partial read_partial(const Partial *p) {
     uint64_t *w = (uint64_t *)p;
-    const uint64_t a = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    const uint64_t r = __hip_atomic_load(w + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const uint64_t a = __hip_atomic_load(w, __ATOMIC_RELAXED, IRIS_FUSED_SCOPE);
+    const uint64_t r = __hip_atomic_load(w + 1, __ATOMIC_RELAXED, IRIS_FUSED_SCOPE);
     Partial q;
     q.num = (uint32_t)a;
     q.den = (uint32_t)(a >> 32);
     q.rot = (int32_t)(uint32_t)r;
     q.pad = 0;
-    q.idx = __hip_atomic_load(w + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    q.idx = __hip_atomic_load(w + 2, __ATOMIC_RELAXED, IRIS_FUSED_SCOPE);
     return q;
 }
 // thread 0 holds this workgroup's winner b (the caller has not stored it)
@@ -198,7 +205,7 @@ __device__ __forceinline__ void fold_partials_last(Partial *partials, const Part
         // the stores are performed (vmcnt also counts stores on gfx9) before the ticket is taken;
         // a release fence at agent / system scope would add the L2 writeback this avoids
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        last = __hip_atomic_fetch_add(fin.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == gridDim.x - 1;
+        last = __hip_atomic_fetch_add(fin.ticket, 1u, __ATOMIC_RELAXED, IRIS_FUSED_SCOPE) == gridDim.x - 1;
     }
     __syncthreads();
     if (!last) return;  // workgroup-uniform
@@ -221,7 +228,7 @@ __device__ __forceinline__ void fold_partials_last(Partial *partials, const Part
             if (partial_better_dev(sw[w], b)) b = sw[w];
         if (b.den != 0) b.idx += fin.idx_base;
         *fin.dst = b;
-        __hip_atomic_store(fin.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);  // for the next launch
+        __hip_atomic_store(fin.ticket, 0u, __ATOMIC_RELAXED, IRIS_FUSED_SCOPE);  // for the next launch
     }
 }
 

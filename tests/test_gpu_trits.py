@@ -2,14 +2,24 @@
 2560 B per template, each position stored as one of the three states encode() tells
 apart (src/lib.rs:16-26).  Counts, distances and the argmin must equal the oracle's
 restatement of Template::distance (src/template.rs:43-64) bit for bit, and equal the
-lossless TILES layout; read-back returns pattern & mask (all the path reads)."""
+lossless TILES layout; read-back returns pattern & mask (all the path reads).
+
+Round 3: TRITS is retired from the default test and bench matrix.  It
+reads 20 % fewer bytes but is VALU-issue-bound on its table decode: 5.2-5.3 ms per 10M against
+TILES 4.72-4.79 ms, so it is not a speed path; the layout stays in the library
+for capacity (2560 B per template: 112M instead of 90M templates per GPU) and is still
+exercised end to end by tests/test_gpu_group.py.  IRIS_TEST_TRITS=1 runs this file."""
+import os
+
 import numpy as np
 import pytest
 
 import iris_hip as ih
 from oracle import oracle_c as oc
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(os.environ.get("IRIS_TEST_TRITS") != "1",
+                                 reason="TRITS is out of the default matrix (IRIS_TEST_TRITS=1 runs it)")]
 ROT = 31
 SEED = 42
 TRITS = ih.LAYOUT_TRITS
