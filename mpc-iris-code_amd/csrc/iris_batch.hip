@@ -372,8 +372,6 @@ __global__ void __launch_bounds__(256) batch_reduce_kernel(const Partial *__rest
 #endif
 namespace lds2 {
 constexpr int kGP = IRIS_BATCH2_GP;      // chunk pairs per K-step
-constexpr int kSteps = kPlaneGroups / kGP;
-static_assert(kPlaneGroups % kGP == 0, "K-step must tile the 100 chunk pairs");
 }  // namespace lds2
 
 // Waves: QW = kBQ / WQL query sets x NW / QW tile sets; a wave holds WQL queries x WT tiles
@@ -385,17 +383,22 @@ static_assert(kPlaneGroups % kGP == 0, "K-step must tile the 100 chunk pairs");
 // BQL = queries per workgroup (a query group): 4 (tiles per N-group = 8 with the shapes
 // above) or 2 with WQL = 2, WT = 2 (16 tiles per N-group: each query tile read from beyond L2
 // is applied to twice the templates, half the A traffic per query).
-template <int NW, int WT, int WQL = 4, int BQL = 4>
+#ifndef IRIS_BATCH2_GP_Q2
+#define IRIS_BATCH2_GP_Q2 4  // chunk pairs per K-step of the 2-query-group shape (5: 197 VGPRs spilled)
+#endif
+template <int NW, int WT, int WQL = 4, int BQL = 4, int GPL = lds2::kGP>
 __global__ void __launch_bounds__(64 * NW, 1)
     batch_lds_kernel(const uint4 *__restrict__ db, const uint4 *__restrict__ qtiles, uint64_t tile0, uint64_t ntiles,
                      uint64_t first, uint64_t end, uint32_t nqg, uint32_t G, Partial *__restrict__ partials) {
-    using namespace lds2;
+    constexpr int kGP = GPL;                        // chunk pairs per K-step
+    constexpr int kSteps = kPlaneGroups / kGP;
+    static_assert(kPlaneGroups % kGP == 0, "K-step must tile the 100 chunk pairs");
     constexpr int kBQ = BQL;
     constexpr int kArows = kBQ * kGP;               // compact A rows (1 KB) per K-step
     constexpr int QW = kBQ / WQL;                   // query sets
     constexpr int kTilesPerGroup = (NW / QW) * WT;  // template tiles per N-group
-    static_assert(kBQ % WQL == 0 && NW % QW == 0 && kArows % NW == 0 && IRIS_BATCH_BQ % kBQ == 0, "geometry");
-    constexpr int kAper = kArows / NW;  // compact A rows per wave and K-step
+    static_assert(kBQ % WQL == 0 && NW % QW == 0 && IRIS_BATCH_BQ % kBQ == 0, "geometry");
+    constexpr int kAper = (kArows + NW - 1) / NW;  // compact A rows per wave and K-step (the last may be idle)
     // [stage][chunk pair][query][den h0, enc h0, den h1, enc h1][lane]: 2 x kGP x 16 KB
     __shared__ uint4 afrag[2][kGP][kBQ][4][64];
 
@@ -426,7 +429,7 @@ __global__ void __launch_bounds__(64 * NW, 1)
 #pragma unroll
         for (int i = 0; i < kAper; ++i) {
             const int r = w + NW * i;
-            aq[i] = abase[(uint64_t)(r % kBQ) * kTileU4 + (k * kGP + r / kBQ) * 64];
+            if (kArows % NW == 0 || r < kArows) aq[i] = abase[(uint64_t)(r % kBQ) * kTileU4 + (k * kGP + r / kBQ) * 64];
         }
     };
     auto b_row = [&](uint32_t s, int t) {  // tile t of this wave, chunk pair 0 of K-step s
@@ -439,6 +442,7 @@ __global__ void __launch_bounds__(64 * NW, 1)
 #pragma unroll
         for (int i = 0; i < kAper; ++i) {
             const int r = w + NW * i, qi = r % kBQ, gp = r / kBQ;
+            if (kArows % NW != 0 && r >= kArows) continue;
             uint4(*dst)[64] = afrag[s & 1][gp][qi];
 #pragma unroll
             for (int h2 = 0; h2 < 2; ++h2) {
@@ -714,7 +718,8 @@ int launch_batch(void *stream, const void *db, const void *qtiles, LaunchRange r
                            (const uint4 *)db, (const uint4 *)qtiles, g.tile0, g.ntiles, r.first, r.first + r.n, g.nqg,
                            g.G, partials);
     else if (kc == 4)  // 2-query groups x 16-tile N-groups: half the query-tile traffic beyond L2
-        hipLaunchKernelGGL((batch_lds_kernel<8, 2, 2, 2>), dim3(g.nqg * g.G), dim3(64 * 8), 0, (hipStream_t)stream,
+        hipLaunchKernelGGL((batch_lds_kernel<8, 2, 2, 2, IRIS_BATCH2_GP_Q2>), dim3(g.nqg * g.G), dim3(64 * 8), 0,
+                           (hipStream_t)stream,
                            (const uint4 *)db, (const uint4 *)qtiles, g.tile0, g.ntiles, r.first, r.first + r.n, g.nqg,
                            g.G, partials);
     else
