@@ -451,6 +451,9 @@ class Ranks:
 
     def join_group(self, args):
         """The library device group of this run (None: single device, or the gloo rehearsal)."""
+        # one node (the bench contract): RCCL's bootstrap sockets over loopback; the data path is
+        # xGMI peer-to-peer either way (a caller's own setting wins)
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
         if args.single_process:
             self.group = ih.Group(list(range(args.gpus)))
         elif self.dist is not None and self.rccl:
