@@ -200,3 +200,38 @@ def test_group_single_rank_communicator():
             gdb.generate(SEED)
             best, idx = oracle_best(query, ref)
             assert same(gdb.search(query), best, idx) and idx == 1234
+
+
+def test_group_configs4_shape_on_one_gpu(group, device):
+    """configs[4]'s shape rehearsed on the one GPU: 8 logical shards as 8 GPUs would hold them
+    (10M templates, so that the single-device copy for the comparison fits beside it), an exact
+    tie between the last record of shard 0 and a record of the last shard (the lower global
+    index must win), then queries whose planted answers sit on both sides of every shard
+    boundary, searched pipelined through the group and compared with the single-device search
+    of the same records."""
+    n, spd = 10_000_000, 8
+    query = oc.gen_templates(SEED + 40, 0, 1)[0]
+    with ih.GroupDatabase(group, ih.KIND_TEMPLATES, n, shards_per_device=spd) as gdb, \
+            ih.Database(device, ih.KIND_TEMPLATES, n) as db:
+        gdb.generate(SEED)
+        db.generate(n, SEED)
+        firsts = [gdb.shard(i)[0] for i in range(spd)]
+        exact = planted(query, 3)
+        for site in (n - 2, firsts[1] - 1):
+            gdb.write(site, exact[None, :])
+            db.write(site, exact[None, :])
+        m = gdb.search(query)
+        assert m.index == firsts[1] - 1 and m.distance == 0.0 and m.rotation == 3
+        sites = [s for f in firsts[1:] for s in (f, f - 2)]
+        qs = [oc.gen_templates(SEED + 50 + k, 0, 1)[0] for k in range(len(sites))]
+        for k, (site, q) in enumerate(zip(sites, qs)):
+            rec = planted(q, (k % 31) - 15, 0x3 << (k % 60))
+            gdb.write(site, rec[None, :])
+            db.write(site, rec[None, :])
+        pend = [gdb.search_async(q) for q in qs]
+        for k, (q, p) in enumerate(zip(qs, pend)):
+            g = p.wait()
+            with ih.TemplateEngine(device, q) as eng:
+                s1 = eng.search(db)
+            assert (g.index, g.num, g.den, g.rotation) == (s1.index, s1.num, s1.den, s1.rotation), (k, g, s1)
+            assert g.index == sites[k]
