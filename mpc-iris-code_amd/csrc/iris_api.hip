@@ -72,33 +72,142 @@ int range_ok(const iris_db *db, uint64_t first, uint64_t n) {
     return 0;
 }
 
+constexpr uint64_t kU16Chunk = 4ull << 20;  // records per engine launch of the host-output forms
+
+// Enqueues the engine kernel over [first, first+n) of db (n <= kU16Chunk), [n][31] u16 rows to
+// the device buffer o, on `stream` (default: the device stream); a DistanceEngine's small-range
+// K-split uses ws (default: the device's shared workspace); nothing waits.
+int enqueue_u16_engine(iris_engine *e, const iris_db *db, uint64_t first, uint64_t n, uint16_t *o,
+                       hipStream_t stream = nullptr, DevBuf *ws = nullptr) {
+    iris_device *d = e->dev;
+    if (!stream) stream = d->stream;
+    if (!ws) ws = &d->out_b;
+    LaunchRange r{first, n};
+    const bool tiles = db->k.layout == IRIS_LAYOUT_TILES;
+    if (e->kind == IRIS_KIND_MASKS)
+        return timed(d, "masks", n, [&] {
+            return tiles ? launch_masks_mfma(stream, db->data, e->qfrag, r, o) : launch_masks(stream, db->data, e->qtab, r, o);
+        }, stream);
+    void *w = nullptr;  // K-split workspace of small ranges
+    if (tiles && shares_workspace_bytes(r)) {
+        CHK(ensure(*ws, shares_workspace_bytes(r)));
+        w = ws->p;
+    }
+    return timed(d, "shares", n, [&] {
+        return tiles ? launch_shares_mfma(stream, db->data, e->qfrag, r, o, w) : launch_shares(stream, db->data, e->qtab, r, o);
+    }, stream);
+}
+
 // Engine kernel over [first, first+n) of db, u16 [n][31] outputs to host.
 int run_u16_engine(iris_engine *e, const iris_db *db, uint64_t first, uint64_t n, uint16_t *out) {
     iris_device *d = e->dev;
-    const uint64_t ch = 4ull << 20;
-    CHK(ensure(d->out_a, std::min<uint64_t>(n, ch) * kRot * 2));
-    for (uint64_t done = 0; done < n; done += ch) {
-        const uint64_t m = std::min<uint64_t>(ch, n - done);
-        LaunchRange r{first + done, m};
-        const bool tiles = db->k.layout == IRIS_LAYOUT_TILES;
-        uint16_t *o = (uint16_t *)d->out_a.p;
-        if (e->kind == IRIS_KIND_MASKS)
-            CHK(timed(d, "masks", m, [&] {
-                return tiles ? launch_masks_mfma(d->stream, db->data, e->qfrag, r, o) : launch_masks(d->stream, db->data, e->qtab, r, o);
-            }));
-        else {
-            void *ws = nullptr;  // K-split workspace of small ranges
-            if (tiles && shares_workspace_bytes(r)) {
-                CHK(ensure(d->out_b, shares_workspace_bytes(r)));
-                ws = d->out_b.p;
-            }
-            CHK(timed(d, "shares", m, [&] {
-                return tiles ? launch_shares_mfma(d->stream, db->data, e->qfrag, r, o, ws) : launch_shares(d->stream, db->data, e->qtab, r, o);
-            }));
-        }
+    CHK(ensure(d->out_a, std::min<uint64_t>(n, kU16Chunk) * kRot * 2));
+    for (uint64_t done = 0; done < n; done += kU16Chunk) {
+        const uint64_t m = std::min<uint64_t>(kU16Chunk, n - done);
+        CHK(enqueue_u16_engine(e, db, first + done, m, (uint16_t *)d->out_a.p));
         HIPCHK(hipMemcpyAsync(out + done * kRot, d->out_a.p, m * kRot * 2, hipMemcpyDeviceToHost, d->stream));
         CHK(sync(d));
     }
+    return 0;
+}
+
+// ---- read-ahead of host-output engine calls (iris_handles.hpp, Readahead)
+
+// calls of at most this many records (62 MB of rows per buffer) go through the read-ahead
+constexpr uint64_t kReadaheadMax = 1ull << 20;
+
+// IRIS_READAHEAD=0 turns it off (tests run both forms)
+bool readahead_on() {
+    const char *f = getenv("IRIS_READAHEAD");
+    return !(f && f[0] == '0');
+}
+
+// Drops the engine's read-ahead: its kernels (side stream) and row copies (device stream) have
+// finished when this returns, so the buffers may be reused or freed.
+int ra_wait(iris_engine *e) {
+    Readahead &ra = e->ra;
+    if (!ra.computed[0]) return 0;
+    iris_device *d = e->dev;
+    ra.pending = false;
+    if (d->aux) HIPCHK(hipStreamSynchronize(d->aux));
+    HIPCHK(hipStreamSynchronize(d->stream));
+    if (d->profiling) fold_done(d);
+    return 0;
+}
+
+void ra_release(iris_engine *e) {
+    Readahead &ra = e->ra;
+    if (!ra.computed[0]) return;
+    (void)hipSetDevice(e->dev->ordinal);
+    (void)ra_wait(e);
+    for (int b = 0; b < 2; ++b) {
+        if (ra.rows[b]) (void)hipFree(ra.rows[b]);
+        (void)hipEventDestroy(ra.computed[b]);
+        (void)hipEventDestroy(ra.copied[b]);
+    }
+    if (ra.ws.p) (void)hipFree(ra.ws.p);
+    ra = Readahead{};
+}
+
+// Enqueues the engine kernel over [first, first+n) of db into rows[b] on the device's side
+// stream, after the last copy out of rows[b]; records computed[b].
+int ra_launch(iris_engine *e, const iris_db *a, uint64_t first, uint64_t n, int b) {
+    Readahead &ra = e->ra;
+    iris_device *d = e->dev;
+    CHK(ensure_aux(d));
+    if (!ra.computed[0])
+        for (int i = 0; i < 2; ++i) {
+            HIPCHK(hipEventCreateWithFlags(&ra.computed[i], hipEventDisableTiming));
+            HIPCHK(hipEventCreateWithFlags(&ra.copied[i], hipEventDisableTiming));
+            HIPCHK(hipEventRecord(ra.copied[i], d->stream));  // "no copy pending" for the first waits
+        }
+    const size_t bytes = (size_t)n * kRot * 2;
+    if (bytes > ra.cap) {
+        CHK(ra_wait(e));  // nothing in flight uses either buffer
+        for (int i = 0; i < 2; ++i) {
+            if (ra.rows[i]) HIPCHK(hipFree(ra.rows[i]));
+            ra.rows[i] = nullptr;
+        }
+        ra.cap = 0;
+        const size_t want = std::max(bytes, (size_t)4096);
+        for (int i = 0; i < 2; ++i) {
+            const hipError_t err = hipMalloc(&ra.rows[i], want);
+            if (err != hipSuccess) return fail(IRIS_E_NOMEM, std::string("read-ahead rows: ") + hipGetErrorString(err));
+        }
+        ra.cap = want;
+    }
+    HIPCHK(hipStreamWaitEvent(d->aux, ra.copied[b], 0));
+    CHK(enqueue_u16_engine(e, a, first, n, (uint16_t *)ra.rows[b], d->aux, &ra.ws));
+    HIPCHK(hipEventRecord(ra.computed[b], d->aux));
+    ra.db = a;
+    ra.version = a->version;
+    ra.first = first;
+    ra.n = n;
+    ra.cur = b;
+    ra.pending = true;
+    return 0;
+}
+
+// A host-output call on records [first, first+n) of db (records [0, end) exist).  Its rows come
+// from the read-ahead buffer when that holds exactly this range of this version of db, else they
+// are computed into the other buffer now; the next range of the same size is then launched on
+// the side stream into the other buffer -- it runs while this call's rows are copied into `out`
+// (the copy engines over the host link, ~1.24 MB per 20 000-record chunk) -- and the call returns
+// once its own copy is done.
+int readahead_u16_call(iris_engine *e, const iris_db *a, uint64_t first, uint64_t n, uint64_t end, uint16_t *out) {
+    Readahead &ra = e->ra;
+    iris_device *d = e->dev;
+    const bool hit = ra.pending && ra.db == a && ra.version == a->version && ra.first == first && ra.n == n;
+    if (!hit) CHK(ra_launch(e, a, first, n, ra.pending ? ra.cur ^ 1 : 0));
+    const int b = ra.cur;
+    HIPCHK(hipStreamWaitEvent(d->stream, ra.computed[b], 0));
+    ra.pending = false;
+    const uint64_t next = first + n;
+    if (next < end) CHK(ra_launch(e, a, next, std::min<uint64_t>(n, end - next), b ^ 1));
+    HIPCHK(hipMemcpyAsync(out, ra.rows[b], (size_t)n * kRot * 2, hipMemcpyDeviceToHost, d->stream));
+    HIPCHK(hipEventRecord(ra.copied[b], d->stream));
+    HIPCHK(hipEventSynchronize(ra.copied[b]));
+    if (d->profiling) fold_done(d);
     return 0;
 }
 
@@ -134,6 +243,7 @@ int qbuf_take(iris_device *d, size_t bytes, void **p, size_t *got) {
 void iris_api::engine_free(iris_engine *e) {
     if (!e) return;
     for (iris_engine *c : e->sub) engine_free(c);
+    ra_release(e);
     if (e->qbuf) {
         iris_device *d = e->dev;
         // later users of the buffer are ordered after this engine's kernels on the device stream
@@ -230,6 +340,7 @@ void device_teardown(iris_device *d) {
         }
         if (d->aux) (void)hipStreamDestroy(d->aux);
         if (d->host_result) (void)hipHostFree(d->host_result);
+        if (d->host_done) (void)hipHostFree(d->host_done);
         for (void *b : d->slot_blocks) (void)hipHostFree(b);
         for (auto &q : d->qpool) (void)hipFree(q.second);
         d->qpool.clear();
@@ -419,6 +530,7 @@ int iris_db_create_ex(iris_device_t *d, int kind, uint64_t capacity, int layout,
     std::lock_guard<std::recursive_mutex> g(d->mu);
     CHK(set_device(d));
     iris_db *db = new (std::nothrow) iris_db();
+    if (db) db->version = next_db_version();
     if (!db) return fail(IRIS_E_NOMEM, "out of host memory");
     db->dev = d;
     db->k = kind_info(kind, layout);
@@ -571,6 +683,7 @@ int iris_db_attach_host(iris_db_t *db, const void *host, uint64_t n, int upload)
     if (n == 0) return 0;
     db->host_base = (uintptr_t)host;
     db->host_n = n;
+    db->version = next_db_version();
     d->attached.push_back(db);
     return 0;
 }
@@ -666,6 +779,8 @@ int iris_engine_batch_process(iris_engine_t *e, const iris_db_t *db, uint64_t fi
     CHK(range_ok(db, first, n));
     if (n == 0) return 0;
     ARG(out, "out is NULL");
+    if (n <= kReadaheadMax && readahead_on()) return readahead_u16_call(e, db, first, n, db->len, out);
+    CHK(ra_wait(e));
     return run_u16_engine(e, db, first, n, out);
 }
 
@@ -717,6 +832,8 @@ int iris_engine_batch_process_host(iris_engine_t *e, const void *records, uint64
         if (a->k.kind != e->kind || p < a->host_base) continue;
         const uintptr_t off = p - a->host_base;
         if (off % k.rec_bytes != 0 || off / k.rec_bytes > a->host_n || n > a->host_n - off / k.rec_bytes) continue;
+        if (n <= kReadaheadMax && readahead_on()) return readahead_u16_call(e, a, off / k.rec_bytes, n, a->host_n, out);
+        CHK(ra_wait(e));
         return run_u16_engine(e, a, off / k.rec_bytes, n, out);
     }
     const uint64_t ch = std::min<uint64_t>(n, 1ull << 20 >> (e->kind == IRIS_KIND_SHARES ? 4 : 0));
@@ -778,8 +895,10 @@ int iris_template_counts(iris_engine_t *e, const iris_db_t *db, uint64_t first, 
 }  // extern "C"
 
 int iris_api::search_enqueue(iris_engine_t *e, const iris_db_t *db, uint64_t first, uint64_t n, double *dist_dev,
-                             Partial *dst, bool side, hipEvent_t done, uint64_t idx_base) {
+                             Partial *dst, bool side, hipEvent_t done, uint64_t idx_base, uint32_t *host_done,
+                             uint32_t seq, bool *flagged) {
     iris_device *d = e->dev;
+    if (flagged) *flagged = false;
     if (n == 0) return 0;
     LaunchRange r{first, n};
     const int layout = db->k.layout;
@@ -787,12 +906,13 @@ int iris_api::search_enqueue(iris_engine_t *e, const iris_db_t *db, uint64_t fir
         // small range: the kernel's last workgroup reduces and writes dst itself (no reduce launch)
         CHK(ensure_ticket(d));
         CHK(ensure(d->partials, (size_t)mfma_search_partials(r) * sizeof(Partial)));
-        const FusedFinish fin{(uint32_t *)d->ticket.p, dst, idx_base};
+        const FusedFinish fin{(uint32_t *)d->ticket.p, dst, idx_base, host_done, seq};
         uint32_t written = 0;
         CHK(timed(d, "template_search", n, [&] {
             return launch_template_mfma_search(d->stream, db->data, e->qfrag, r, dist_dev, (Partial *)d->partials.p,
                                                &written, &fin);
         }));
+        if (flagged) *flagged = host_done != nullptr;
         if (!side) return 0;
         // later side-stream work (a group's all-gather) and `done` follow the kernel
         CHK(ensure_aux(d));
@@ -846,9 +966,26 @@ static int search_locked(iris_engine_t *e, const iris_db_t *db, uint64_t first, 
                          double *dist_dev, iris_match_t *out) {
     iris_device *d = e->dev;
     CHK(ensure_host_result(d, sizeof(Partial)));
-    CHK(search_enqueue(e, db, first, n, dist_dev, (Partial *)d->host_result));
+    // Without a device distances output the caller needs only the winner: a small (fused)
+    // search publishes it with a sequence word in coherent host memory, and the call returns
+    // as soon as that word lands -- no wait for the kernel's retirement and completion signal
+    // (the kernel's tail is ordered before anything later enqueued on the stream).
+    uint32_t *done_word = nullptr, seq = 0;
+    if (!dist_dev) {
+        CHK(ensure_host_done(d));
+        done_word = d->host_done;
+        seq = ++d->done_seq;
+        if (seq == 0) seq = ++d->done_seq;  // 0 is the word's initial value
+    }
+    bool flagged = false;
+    CHK(search_enqueue(e, db, first, n, dist_dev, (Partial *)d->host_result, false, nullptr, 0, done_word, seq,
+                       &flagged));
     Partial res{};
-    CHK(sync(d));
+    if (flagged) {
+        CHK(wait_done(d, seq));
+        if (d->profiling) fold_done(d);  // the timing events of earlier searches
+    } else
+        CHK(sync(d));
     if (n > 0) memcpy(&res, d->host_result, sizeof(Partial));
     if (out) {
         if (n == 0 || res.den == 0) {

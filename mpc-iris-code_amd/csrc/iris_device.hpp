@@ -197,6 +197,8 @@ __device__ __forceinline__ Partial read_partial(const Partial *p) {
     q.idx = __hip_atomic_load(w + 2, __ATOMIC_RELAXED, IRIS_FUSED_SCOPE);
     return q;
 }
+constexpr uint32_t kTicketGroups = 8;    // sub-tickets of fold_partials_last
+constexpr uint32_t kTicketStride = 64;   // words between tickets (256 B: separate lines)
 // thread 0 holds this workgroup's winner b (the caller has not stored it)
 __device__ __forceinline__ void fold_partials_last(Partial *partials, const Partial &b0, const FusedFinish &fin) {
     __shared__ int last;
@@ -205,7 +207,17 @@ __device__ __forceinline__ void fold_partials_last(Partial *partials, const Part
         // the stores are performed (vmcnt also counts stores on gfx9) before the ticket is taken;
         // a release fence at agent / system scope would add the L2 writeback this avoids
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        last = __hip_atomic_fetch_add(fin.ticket, 1u, __ATOMIC_RELAXED, IRIS_FUSED_SCOPE) == gridDim.x - 1;
+        // two-level ticket: workgroup b counts at sub-ticket b % 8 (its own 256-B line), the last
+        // of each of those groups at the top word -- the same-address atomics of a launch are
+        // serialised where they are performed, ~6 ns each, so 625 on one word cost ~4 us of tail
+        const uint32_t c = blockIdx.x % kTicketGroups, groups = gridDim.x < kTicketGroups ? gridDim.x : kTicketGroups;
+        const uint32_t members = (gridDim.x - c + kTicketGroups - 1) / kTicketGroups;
+        uint32_t *sub = fin.ticket + kTicketStride * (1 + c);
+        last = 0;
+        if (__hip_atomic_fetch_add(sub, 1u, __ATOMIC_RELAXED, IRIS_FUSED_SCOPE) == members - 1) {
+            __hip_atomic_store(sub, 0u, __ATOMIC_RELAXED, IRIS_FUSED_SCOPE);  // for the next launch
+            last = __hip_atomic_fetch_add(fin.ticket, 1u, __ATOMIC_RELAXED, IRIS_FUSED_SCOPE) == groups - 1;
+        }
     }
     __syncthreads();
     if (!last) return;  // workgroup-uniform
@@ -227,8 +239,18 @@ __device__ __forceinline__ void fold_partials_last(Partial *partials, const Part
         for (uint32_t w = 1; w < (blockDim.x + 63) / 64; ++w)
             if (partial_better_dev(sw[w], b)) b = sw[w];
         if (b.den != 0) b.idx += fin.idx_base;
-        *fin.dst = b;
         __hip_atomic_store(fin.ticket, 0u, __ATOMIC_RELAXED, IRIS_FUSED_SCOPE);  // for the next launch
+        if (fin.done) {
+            // write-through to the host, completed, then the sequence word the host polls
+            uint64_t *w = (uint64_t *)fin.dst;
+            __hip_atomic_store(w, (uint64_t)b.num | ((uint64_t)b.den << 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(w + 1, (uint64_t)(uint32_t)b.rot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(w + 2, b.idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(fin.done, fin.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        } else {
+            *fin.dst = b;
+        }
     }
 }
 

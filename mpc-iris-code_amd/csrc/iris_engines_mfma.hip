@@ -258,6 +258,59 @@ __global__ void __launch_bounds__(256, kMasksBlocksPerCu)
     }
 }
 
+// Small ranges (up to kMasksSplitTiles tiles: the resolver's 20k-record chunks,
+// src/main.rs:511-516): one tile per workgroup of KS waves, wave w summing K-slice w
+// (kSteps / KS steps of 4 chunks).  Every load of the slice -- mask dwords from HBM,
+// query words from L2 (no LDS staging of the whole query per workgroup) -- is issued
+// up front, so the launch costs about one HBM round trip per wave instead of the
+// persistent kernel's ~25 dependent ones; the slices' counts (exact integers in f32)
+// meet in LDS and wave 0 writes the tile's rows.
+constexpr int kMasksSplitKS = 10;
+constexpr uint64_t kMasksSplitTiles = 1024;
+
+template <int KS>
+__global__ void __launch_bounds__(64 * KS)
+    masks_split_kernel(const uint4 *__restrict__ db, const uint4 *__restrict__ qfrag, uint64_t tile0,
+                       uint64_t first, uint64_t end, uint16_t *__restrict__ out) {
+    constexpr int kSteps = kMaskChunks / 4;  // 50
+    static_assert(kSteps % KS == 0, "K-split geometry");
+    constexpr int kG = kSteps / KS;
+    const int lane = threadIdx.x & 63;
+    const int slice = threadIdx.x >> 6;
+    const uint64_t tile = tile0 + blockIdx.x;
+    const uint4 *dp = db + tile * (uint64_t)kMaskTileUint4 + (uint64_t)slice * kG * 64 + lane;
+    const uint4 *qp = qfrag + (uint64_t)slice * kG * 64 + lane;
+    uint4 d[kG], w[kG];
+#pragma unroll
+    for (int g = 0; g < kG; ++g) d[g] = nt_load(dp + g * 64);
+#pragma unroll
+    for (int g = 0; g < kG; ++g) w[g] = qp[g * 64];
+    v16f acc;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+#pragma unroll
+    for (int g = 0; g < kG; ++g) {
+        mask_chunk(d[g].x, mask_a(w[g].x), acc);
+        mask_chunk(d[g].y, mask_a(w[g].y), acc);
+        mask_chunk(d[g].z, mask_a(w[g].z), acc);
+        mask_chunk(d[g].w, mask_a(w[g].w), acc);
+    }
+    __shared__ float red[KS - 1][16][64];
+    __shared__ __attribute__((aligned(16))) uint16_t sh_out[1024];
+    if (slice != 0) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) red[slice - 1][i][lane] = acc[i];
+    }
+    __syncthreads();
+    if (slice != 0) return;
+#pragma unroll
+    for (int k = 0; k < KS - 1; ++k)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[i] += red[k][i][lane];
+    store_tile_rows(out, sh_out, tile * kTile, first, end, true, lane,
+                    [&](int r) { return (uint16_t)(uint32_t)acc[r]; });
+}
+
 // Tiles per wave for a range of `ntiles` tiles: `big`, unless that leaves fewer waves
 // than the chip holds at two workgroups per CU — then one, for 8x / 4x / 2x the waves
 // (a participant-sized chunk of 20k records is only 625 tiles).  IRIS_TILES_PER_WAVE=1|4
@@ -269,7 +322,15 @@ static int tiles_per_wave(uint64_t ntiles, int big) {
 
 int launch_masks_mfma(void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *out) {
     if (r.n == 0) return 0;
-    const int tpw = tiles_per_wave(tiles_of(r, 1).ntiles, kMasksTiles);
+    const uint64_t ntiles = tiles_of(r, 1).ntiles;
+    // the K-split form for small ranges (IRIS_TILES_PER_WAVE pins the persistent kernel for tests)
+    if (ntiles <= kMasksSplitTiles && !getenv("IRIS_TILES_PER_WAVE")) {
+        hipLaunchKernelGGL(masks_split_kernel<kMasksSplitKS>, dim3((uint32_t)ntiles), dim3(64 * kMasksSplitKS), 0,
+                           (hipStream_t)stream, (const uint4 *)db, (const uint4 *)qfrag, tiles_of(r, 1).tile0,
+                           r.first, r.first + r.n, out);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
+    const int tpw = tiles_per_wave(ntiles, kMasksTiles);
     const Tiles t = tiles_of(r, tpw);
     const uint64_t grid = std::min<uint64_t>(t.grid, resident_blocks(kMasksBlocksPerCu));
     auto kern = tpw == 1 ? masks_mfma_kernel<MASKS_OUT, 1> : masks_mfma_kernel<MASKS_OUT>;

@@ -74,6 +74,10 @@ struct iris_device {
     // device-to-host copy between the last kernel and the stream sync)
     void *host_result = nullptr;
     size_t host_result_cap = 0;
+    // coherent pinned word a blocking small search's last workgroup stores its sequence
+    // number into after its result (iris::FusedFinish::done); the host spins on it
+    uint32_t *host_done = nullptr;
+    uint32_t done_seq = 0;
     // pinned result slots of asynchronous searches (iris_template_search_async)
     std::vector<iris::Partial *> free_slots;
     std::vector<void *> slot_blocks;
@@ -103,6 +107,33 @@ struct iris_db {
     // iris_db_attach_host: records [0, host_n) equal the host array at host_base
     uintptr_t host_base = 0;
     uint64_t host_n = 0;
+    // process-unique, renewed by every change of the records (db_detach) and every attachment:
+    // an engine's read-ahead rows are valid for one version of one database
+    uint64_t version = 0;
+};
+
+inline uint64_t next_db_version() {
+    static std::atomic<uint64_t> v{0};
+    return ++v;
+}
+
+// Read-ahead of a masks / distance engine's host-output calls (host slices of an attached
+// array, iris_engine_batch_process_host, or ranges of a resident database,
+// iris_engine_batch_process): the reference's participant and resolver walk their file in
+// consecutive 20 000-record chunks (src/main.rs:427-431, 511-516), so while the rows of chunk
+// [first, first + n) are copied to the caller, the engine already computes [first + n, first + 2n)
+// on the device's side stream into its other row buffer; the next call, if it asks for exactly
+// that range of the same version of the same database, only copies those rows out.
+struct Readahead {
+    const struct iris_db *db = nullptr;
+    uint64_t version = 0, first = 0, n = 0;  // the range in flight into rows[cur]
+    void *rows[2] = {nullptr, nullptr};      // device [n][31] u16 rows
+    size_t cap = 0;                          // bytes of each
+    hipEvent_t computed[2] = {nullptr, nullptr};  // side stream, after the kernel into rows[b]
+    hipEvent_t copied[2] = {nullptr, nullptr};    // device stream, after the copy out of rows[b]
+    int cur = 0;
+    bool pending = false;
+    DevBuf ws;  // the K-split workspace of read-ahead DistanceEngine launches (own: concurrent)
 };
 
 struct iris_engine {
@@ -115,6 +146,7 @@ struct iris_engine {
     void *qfrag_trits = nullptr;  // template engines: the TRITS kernel's query fragments
     uint32_t nq = 0;          // > 0: batched template engine (qfrag = nq padded query tiles)
     std::vector<iris_engine *> sub;  // streaming batched engine: one single-query engine per query
+    Readahead ra;             // masks / distance engines: host-slice calls on attached databases
 };
 
 // Up to this many queries a batch runs as streaming passes over the database —
@@ -150,10 +182,39 @@ inline int ensure_host_result(iris_device *d, size_t bytes) {
     d->host_result = nullptr;
     d->host_result_cap = 0;
     const size_t want = std::max(bytes, (size_t)4096);
-    hipError_t e = hipHostMalloc(&d->host_result, want, hipHostMallocDefault);
+    // coherent: a fused search writes its winner through to it and the host reads it
+    // while the kernel may still be retiring (search_locked)
+    hipError_t e = hipHostMalloc(&d->host_result, want, hipHostMallocCoherent | hipHostMallocMapped);
     if (e != hipSuccess) return fail(IRIS_E_NOMEM, std::string("hipHostMalloc result: ") + hipGetErrorString(e));
     d->host_result_cap = want;
     return 0;
+}
+
+inline int ensure_host_done(iris_device *d) {
+    if (d->host_done) return 0;
+    void *p = nullptr;
+    hipError_t e = hipHostMalloc(&p, 256, hipHostMallocCoherent | hipHostMallocMapped);
+    if (e != hipSuccess) return fail(IRIS_E_NOMEM, std::string("hipHostMalloc done word: ") + hipGetErrorString(e));
+    d->host_done = (uint32_t *)p;
+    __atomic_store_n(d->host_done, 0u, __ATOMIC_RELEASE);
+    return 0;
+}
+
+// Spins until the kernel enqueued last stores `seq` into d->host_done.  The stream is
+// queried every few thousand polls, so a failed launch is reported rather than waited on.
+inline int wait_done(iris_device *d, uint32_t seq) {
+    for (uint32_t spins = 1;; ++spins) {
+        if (__atomic_load_n(d->host_done, __ATOMIC_ACQUIRE) == seq) return 0;
+        if ((spins & 4095) == 0) {
+            const hipError_t q = hipStreamQuery(d->stream);
+            if (q == hipSuccess) {
+                if (__atomic_load_n(d->host_done, __ATOMIC_ACQUIRE) == seq) return 0;
+                return fail(IRIS_E_HIP, "search kernel completed without publishing its result");
+            }
+            if (q != hipErrorNotReady) return fail(IRIS_E_HIP, std::string("hipStreamQuery: ") + hipGetErrorString(q));
+        }
+        __builtin_ia32_pause();
+    }
 }
 
 // A pinned host slot for one asynchronous search result (blocks of 256 slots).
@@ -242,6 +303,7 @@ inline int check_kind(int kind) {
 
 // Any change to a database's records ends its host attachment (caller holds the device lock).
 inline void db_detach(iris_db *db) {
+    db->version = next_db_version();  // read-ahead rows of the old records no longer match
     if (!db->host_base) return;
     auto &v = db->dev->attached;
     v.erase(std::remove(v.begin(), v.end(), db), v.end());
@@ -251,8 +313,8 @@ inline void db_detach(iris_db *db) {
 
 inline int ensure_ticket(iris_device *d) {
     if (d->ticket.p) return 0;
-    CHK(ensure(d->ticket, 256));
-    HIPCHK(hipMemsetAsync(d->ticket.p, 0, 256, d->stream));
+    CHK(ensure(d->ticket, 4096));  // the top word + 8 sub-tickets 256 B apart (iris_device.hpp)
+    HIPCHK(hipMemsetAsync(d->ticket.p, 0, 4096, d->stream));
     return 0;
 }
 
@@ -271,8 +333,11 @@ int template_engine_locked(iris_device *d, const iris_template_t *query, iris_en
 // range-relative index + idx_base) lands in `dst` (pinned host or device memory); nothing
 // waits.  side = true: the reduce runs on the device's side stream over one of two
 // alternating partials buffers, and `done` (if given) is recorded there after it.
+// host_done / seq: the fused small-range form also stores seq into the coherent host word
+// host_done after writing dst; *flagged reports whether that form ran (else nothing is stored).
 int search_enqueue(iris_engine *e, const iris_db *db, uint64_t first, uint64_t n, double *dist_dev, iris::Partial *dst,
-                   bool side = false, hipEvent_t done = nullptr, uint64_t idx_base = 0);
+                   bool side = false, hipEvent_t done = nullptr, uint64_t idx_base = 0, uint32_t *host_done = nullptr,
+                   uint32_t seq = 0, bool *flagged = nullptr);
 // Partial (indices offset by base) -> iris_match_t; +inf / UINT64_MAX when none
 void match_from(const iris::Partial &r, bool any, uint64_t base, iris_match_t *out);
 

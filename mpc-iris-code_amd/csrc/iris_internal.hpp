@@ -271,11 +271,16 @@ int launch_template_mfma_counts(void *stream, const void *db, const void *qfrag,
                                 uint16_t *den_out);
 // Fused finish of a small search (grids of at most kFusedReduceMax workgroups): the last
 // workgroup to finish reduces the partials and writes the winner (idx + idx_base) to dst;
-// ticket is a zeroed device word that the kernel leaves zeroed.
+// ticket is a zeroed 4-KB device block (a two-level ticket) that the kernel leaves zeroed.  done != null (dst in
+// coherent host memory): dst is written through to host memory and, once those stores have
+// completed, seq is stored to *done (coherent host memory) -- a blocking caller spins on
+// that word instead of waiting for the end of the kernel and the runtime's completion signal.
 struct FusedFinish {
     uint32_t *ticket;
     Partial *dst;
     uint64_t idx_base;
+    uint32_t *done;
+    uint32_t seq;
 };
 constexpr uint32_t kFusedReduceMax = 4096;
 bool fused_search_ok(LaunchRange r);

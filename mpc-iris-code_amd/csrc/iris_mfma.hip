@@ -40,6 +40,16 @@ constexpr int kTileUint4 = kPlaneGroups * 64;  // 6400 uint4 = 102400 B per tile
 #endif
 constexpr int kMfmaTiles = IRIS_MFMA_TILES;    // tiles per wave (4: 128 templates)
 constexpr int kMfmaWgs = IRIS_MFMA_WGS;        // workgroups per CU the register budget allows
+#ifndef IRIS_SPLIT_STAGES
+#define IRIS_SPLIT_STAGES 6
+#endif
+constexpr int kSplitStages = IRIS_SPLIT_STAGES;  // load ring depth of the K-split (small-range) form
+#ifndef IRIS_SPLIT_T
+#define IRIS_SPLIT_T 2
+#endif
+// tiles per workgroup of the K-split form: every query-fragment load (2 per chunk pair and
+// wave, from L2) feeds this many tiles -- at 1 the query stream is twice the template stream
+constexpr int kSplitT = IRIS_SPLIT_T;
 
 __device__ __forceinline__ v16f mfma_fp4(const v8i &a, const v8i &b, const v16f &c) {
     // cbsz = blgp = 4: both operands e2m1; scales 127 = 2^0 (e8m0)
@@ -93,8 +103,8 @@ __device__ __forceinline__ uint4 stream_load(const uint4 *p) {
 
 enum { MF_COUNTS = 0, MF_SEARCH = 1 };
 
-// KS > 1 (small ranges, T = 1): the KS waves of a tile group split K -- wave w computes
-// chunk groups [w' * 100 / KS, +100 / KS) of tile blockIdx.x * (4 / KS) + w / KS (w' = w % KS)
+// KS > 1 (small ranges, T = kSplitT): the KS waves of a tile group split K -- wave w computes
+// chunk groups [w' * 100 / KS, +100 / KS) of tiles T * (blockIdx.x * (4 / KS) + w / KS) + t (w' = w % KS)
 // -- and the partial sums (exact integers in f32) meet in LDS before the epilogue, so a range of
 // a few hundred tiles still puts several waves on every SIMD.
 // FUSED (search, small grids): the last workgroup to finish folds every workgroup's
@@ -105,7 +115,7 @@ __global__ void __launch_bounds__(256, kMfmaWgs)
                          uint64_t ntiles, uint64_t first, uint64_t end, uint16_t *__restrict__ num_out,
                          uint16_t *__restrict__ den_out, double *__restrict__ dist_out,
                          Partial *__restrict__ partials, FusedFinish fin) {
-    static_assert(KS == 1 || (T == 1 && kWaveSlots % KS == 0 && kPlaneGroups % KS == 0), "K-split geometry");
+    static_assert(KS == 1 || (kWaveSlots % KS == 0 && kPlaneGroups % KS == 0), "K-split geometry");
     const int lane = threadIdx.x & 63;
     const int wslot = threadIdx.x >> 6;
     const int slice = wslot % KS;
@@ -158,41 +168,60 @@ __global__ void __launch_bounds__(256, kMfmaWgs)
 #pragma unroll
             for (int t = 0; t < T; ++t) chunk_step(st.d[t].z, st.d[t].w, f1, den[t], s[t]);
         };
-        Stage sa, sb, sc;
-        load(sa, 0);
-        load(sb, 1);
-        int g = 0;
+        if constexpr (KS > 1) {
+            // K-slice of kG = 25 steps, fully unrolled over a kSplitStages-deep ring: the wave
+            // keeps (kSplitStages - 1) steps of loads in flight instead of 2, so a range of a
+            // few hundred tiles -- one short slice per wave, nothing to overlap between
+            // slices -- is not bound by one HBM round trip per two steps
+            Stage st[kSplitStages];
+#pragma unroll
+            for (int i = 0; i < kSplitStages - 1; ++i) load(st[i], i);
+#pragma unroll
+            for (int g = 0; g < kG; ++g) {
+                if (g + kSplitStages - 1 < kG) load(st[(g + kSplitStages - 1) % kSplitStages], g + kSplitStages - 1);
+                compute(st[g % kSplitStages]);
+            }
+        } else {
+            Stage sa, sb, sc;
+            load(sa, 0);
+            load(sb, 1);
+            int g = 0;
 #pragma unroll 1
-        for (; g + 3 <= kG; g += 3) {
-            load(sc, g + 2);
-            compute(sa);
-            load(sa, g + 3);
-            compute(sb);
-            load(sb, g + 4);
-            compute(sc);
+            for (; g + 3 <= kG; g += 3) {
+                load(sc, g + 2);
+                compute(sa);
+                load(sa, g + 3);
+                compute(sb);
+                load(sb, g + 4);
+                compute(sc);
+            }
+            // kG = 3q + {1, 2} (100; 50): the remaining steps' data is in sa (, sb)
+            if constexpr (kG % 3 >= 1) compute(sa);
+            if constexpr (kG % 3 == 2) compute(sb);
         }
-        // kG = 3q + {1, 2} (100, 25; 50): the remaining steps' data is in sa (, sb)
-        if constexpr (kG % 3 >= 1) compute(sa);
-        if constexpr (kG % 3 == 2) compute(sb);
     }
     if constexpr (KS > 1) {  // the K-slices' partial sums -> slice 0's accumulators (exact)
-        __shared__ float red[kWaveSlots][32][64];
+        __shared__ float red[kWaveSlots][T][32][64];
         if (slice != 0) {
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                red[wslot][i][lane] = den[0][i];
-                red[wslot][16 + i][lane] = s[0][i];
-            }
+            for (int t = 0; t < T; ++t)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    red[wslot][t][i][lane] = den[t][i];
+                    red[wslot][t][16 + i][lane] = s[t][i];
+                }
         }
         __syncthreads();
         if (slice == 0) {
 #pragma unroll
             for (int k = 1; k < KS; ++k)
 #pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    den[0][i] += red[wslot + k][i][lane];
-                    s[0][i] += red[wslot + k][16 + i][lane];
-                }
+                for (int t = 0; t < T; ++t)
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) {
+                        den[t][i] += red[wslot + k][t][i][lane];
+                        s[t][i] += red[wslot + k][t][16 + i][lane];
+                    }
         }
     }
 
@@ -505,8 +534,8 @@ static TileRange tile_range(LaunchRange r) {
         t.ksplit = 1;
     }
     if (t.ksplit > 1) {
-        t.tiles_per_wave = 1;
-        t.grid = t.ntiles;  // one tile per workgroup
+        t.tiles_per_wave = kSplitT;
+        t.grid = (t.ntiles + kSplitT - 1) / kSplitT;  // kSplitT tiles per workgroup
         return t;
     }
     const uint64_t waves = (t.ntiles + t.tiles_per_wave - 1) / t.tiles_per_wave;
@@ -539,7 +568,7 @@ int launch_template_mfma_counts(void *stream, const void *db, const void *qfrag,
                                 uint16_t *den_out) {
     if (r.n == 0) return 0;
     const TileRange t = tile_range(r);
-    auto kern = t.ksplit > 1 ? template_mfma_kernel<MF_COUNTS, 1, 4>
+    auto kern = t.ksplit > 1 ? template_mfma_kernel<MF_COUNTS, kSplitT, 4>
                 : t.tiles_per_wave == 1 ? template_mfma_kernel<MF_COUNTS, 1> : template_mfma_kernel<MF_COUNTS>;
     hipLaunchKernelGGL(kern, dim3((uint32_t)t.grid), dim3(256), 0, (hipStream_t)stream,
                        (const uint4 *)db, (const uint4 *)qfrag, t.tile0, t.ntiles, r.first, r.first + r.n, num_out,
@@ -554,10 +583,10 @@ int launch_template_mfma_search(void *stream, const void *db, const void *qfrag,
     if (r.n == 0) return 0;
     const bool fused = fin && t.grid <= kFusedReduceMax;
     if (fin && !fused) return -1;  // the caller asks fused_search_ok() first
-    auto kern = fused ? (t.ksplit > 1 ? template_mfma_kernel<MF_SEARCH, 1, 4, true>
+    auto kern = fused ? (t.ksplit > 1 ? template_mfma_kernel<MF_SEARCH, kSplitT, 4, true>
                          : t.tiles_per_wave == 1 ? template_mfma_kernel<MF_SEARCH, 1, 1, true>
                                                  : template_mfma_kernel<MF_SEARCH, kMfmaTiles, 1, true>)
-                      : (t.ksplit > 1 ? template_mfma_kernel<MF_SEARCH, 1, 4>
+                      : (t.ksplit > 1 ? template_mfma_kernel<MF_SEARCH, kSplitT, 4>
                          : t.tiles_per_wave == 1 ? template_mfma_kernel<MF_SEARCH, 1> : template_mfma_kernel<MF_SEARCH>);
     hipLaunchKernelGGL(kern, dim3((uint32_t)t.grid), dim3(256), 0, (hipStream_t)stream,
                        (const uint4 *)db, (const uint4 *)qfrag, t.tile0, t.ntiles, r.first, r.first + r.n,

@@ -108,3 +108,96 @@ def test_attach_kind_and_alignment_rules(device):
         tdb.generate(10, 1)
         with pytest.raises(ih.IrisError):
             tdb.save_file("/tmp/never_written.templates")
+
+
+def launches(dev, name):
+    return dev.kernel_stats(name)[0]
+
+
+@pytest.mark.parametrize("kind", [ih.KIND_MASKS, ih.KIND_SHARES])
+@pytest.mark.parametrize("readahead", ["1", "0"])
+def test_attached_chunk_walk_readahead(device, monkeypatch, kind, readahead):
+    """The reference's loop (src/main.rs:427-431, 511-516): consecutive equal chunks of the
+    attached file, the last one short.  With readahead every chunk after the first comes from
+    the engine's read-ahead rows, computed once: one engine launch per chunk."""
+    monkeypatch.setenv("IRIS_READAHEAD", readahead)
+    n, chunk = (5003, 1000) if kind == ih.KIND_MASKS else (1301, 300)
+    host = oc.gen_masks(SEED + 5, 0, n) if kind == ih.KIND_MASKS else oc.gen_shares(SEED + 5, 0, n)
+    qt = oc.gen_templates(SEED + 6, 0, 1)[0]
+    if kind == ih.KIND_MASKS:
+        eng, want, kname = ih.MasksEngine(device, qt[200:]), oc.masks_batch(qt[200:], host), "masks"
+    else:
+        q = oc.encode(qt)
+        eng, want, kname = ih.DistanceEngine(device, q), oc.distance_batch(q, host), "shares"
+    with eng, ih.Database(device, kind, n) as db:
+        db.attach_host(host)
+        device.reset_stats()
+        device.set_profiling(True)
+        try:
+            for walk in range(2):  # the second walk starts with a miss (chunk 0 after the last)
+                for a in range(0, n, chunk):
+                    out = np.empty((min(chunk, n - a), 31), np.uint16)
+                    eng.batch_process(out, host[a:a + chunk])
+                    assert (out == want[a:a + chunk]).all(), (walk, a)
+            device.synchronize()
+            chunks = 2 * ((n + chunk - 1) // chunk)
+            assert launches(device, kname) == chunks  # no chunk computed twice
+            assert launches(device, "pack") == 0
+            # out of order: every call still returns its own rows (misses recompute)
+            for a, b in ((2000 % n, 2000 % n + 7), (0, chunk), (0, chunk), (n - 5, n), (chunk, 2 * chunk), (1, 2)):
+                out = np.empty((b - a, 31), np.uint16)
+                eng.batch_process(out, host[a:b])
+                assert (out == want[a:b]).all(), (a, b)
+        finally:
+            device.set_profiling(False)
+
+
+def test_readahead_dropped_when_attachment_changes(device):
+    """A read-ahead chunk belongs to one attachment: rewriting the database and re-attaching
+    the same host buffer with new contents (same address) must not serve the old rows."""
+    n, chunk = 4000, 1000
+    host = oc.gen_masks(SEED + 7, 0, n)
+    new = oc.gen_masks(SEED + 8, 0, n)
+    q = oc.gen_masks(SEED + 9, 0, 1)[0]
+    with ih.MasksEngine(device, q) as eng, ih.Database(device, ih.KIND_MASKS, n) as db:
+        db.attach_host(host)
+        out = np.empty((chunk, 31), np.uint16)
+        eng.batch_process(out, host[:chunk])  # chunk 1 is now read ahead from the old contents
+        assert (out == oc.masks_batch(q, host[:chunk])).all()
+        host[:] = new
+        db.write(0, host)  # detaches
+        db.attach_host(host, upload=False)  # same address, new attachment
+        eng.batch_process(out, host[chunk:2 * chunk])
+        assert (out == oc.masks_batch(q, new[chunk:2 * chunk])).all()
+        # and an engine destroyed with a read-ahead in flight releases it
+        eng.batch_process(out, host[2 * chunk:3 * chunk])
+    device.synchronize()
+
+
+def test_resident_range_walk_readahead(device):
+    """iris_engine_batch_process over consecutive ranges of a resident database (host output)
+    reads ahead too; a write into the database between two calls drops the read-ahead rows."""
+    n, chunk = 3500, 800
+    recs = oc.gen_masks(SEED + 10, 0, n)
+    q = oc.gen_masks(SEED + 11, 0, 1)[0]
+    with ih.MasksEngine(device, q) as eng, ih.Database(device, ih.KIND_MASKS, n) as db:
+        db.append(recs)
+        want = oc.masks_batch(q, recs)
+        device.reset_stats()
+        device.set_profiling(True)
+        try:
+            for a in range(0, n, chunk):
+                m = min(chunk, n - a)
+                out = np.empty((m, 31), np.uint16)
+                eng.batch_process(out, db, first=a, n=m)
+                assert (out == want[a:a + m]).all(), a
+            device.synchronize()
+            assert launches(device, "masks") == (n + chunk - 1) // chunk
+        finally:
+            device.set_profiling(False)
+        out = np.empty((chunk, 31), np.uint16)
+        eng.batch_process(out, db, first=0, n=chunk)  # [chunk, 2 chunk) is read ahead now
+        recs[chunk:2 * chunk] = oc.gen_masks(SEED + 12, 0, chunk)
+        db.write(chunk, recs[chunk:2 * chunk])
+        eng.batch_process(out, db, first=chunk, n=chunk)
+        assert (out == oc.masks_batch(q, recs[chunk:2 * chunk])).all()
