@@ -74,27 +74,20 @@ int range_ok(const iris_db *db, uint64_t first, uint64_t n) {
 
 constexpr uint64_t kU16Chunk = 4ull << 20;  // records per engine launch of the host-output forms
 
-// Enqueues the engine kernel over [first, first+n) of db (n <= kU16Chunk), [n][31] u16 rows to
-// the device buffer o, on `stream` (default: the device stream); a DistanceEngine's small-range
-// K-split uses ws (default: the device's shared workspace); nothing waits.
+// Enqueues the engine kernel over [first, first+n) of db, [n][31] u16 rows to the device buffer
+// o, on `stream` (default: the device stream); nothing waits.
 int enqueue_u16_engine(iris_engine *e, const iris_db *db, uint64_t first, uint64_t n, uint16_t *o,
-                       hipStream_t stream = nullptr, DevBuf *ws = nullptr) {
+                       hipStream_t stream = nullptr) {
     iris_device *d = e->dev;
     if (!stream) stream = d->stream;
-    if (!ws) ws = &d->out_b;
     LaunchRange r{first, n};
     const bool tiles = db->k.layout == IRIS_LAYOUT_TILES;
     if (e->kind == IRIS_KIND_MASKS)
         return timed(d, "masks", n, [&] {
             return tiles ? launch_masks_mfma(stream, db->data, e->qfrag, r, o) : launch_masks(stream, db->data, e->qtab, r, o);
         }, stream);
-    void *w = nullptr;  // K-split workspace of small ranges
-    if (tiles && shares_workspace_bytes(r)) {
-        CHK(ensure(*ws, shares_workspace_bytes(r)));
-        w = ws->p;
-    }
     return timed(d, "shares", n, [&] {
-        return tiles ? launch_shares_mfma(stream, db->data, e->qfrag, r, o, w) : launch_shares(stream, db->data, e->qtab, r, o);
+        return tiles ? launch_shares_mfma(stream, db->data, e->qfrag, r, o) : launch_shares(stream, db->data, e->qtab, r, o);
     }, stream);
 }
 
@@ -116,8 +109,13 @@ int run_u16_engine(iris_engine *e, const iris_db *db, uint64_t first, uint64_t n
 // calls of at most this many records (62 MB of rows per buffer) go through the read-ahead
 constexpr uint64_t kReadaheadMax = 1ull << 20;
 
-// IRIS_READAHEAD=0 turns it off (tests run both forms)
-bool readahead_on() {
+// Distance engines only: a masks call's 13-us kernel hides little behind its ~40-us row copy
+// (48-51 vs 57-60 us per 20k-record call), and in 4 of 6 bench runs a masks walk with read-ahead
+// fell into 275 us per call -- the copy behind a cross-stream dependency taking the runtime's
+// slow path (profiles/r03_readahead.txt) -- while a shares call (103-us kernel) gains 1.4x.
+// IRIS_READAHEAD=0 turns it off (tests run both forms).
+bool readahead_on(const iris_engine *e) {
+    if (e->kind != IRIS_KIND_SHARES) return false;
     const char *f = getenv("IRIS_READAHEAD");
     return !(f && f[0] == '0');
 }
@@ -145,7 +143,6 @@ void ra_release(iris_engine *e) {
         (void)hipEventDestroy(ra.computed[b]);
         (void)hipEventDestroy(ra.copied[b]);
     }
-    if (ra.ws.p) (void)hipFree(ra.ws.p);
     ra = Readahead{};
 }
 
@@ -177,7 +174,7 @@ int ra_launch(iris_engine *e, const iris_db *a, uint64_t first, uint64_t n, int 
         ra.cap = want;
     }
     HIPCHK(hipStreamWaitEvent(d->aux, ra.copied[b], 0));
-    CHK(enqueue_u16_engine(e, a, first, n, (uint16_t *)ra.rows[b], d->aux, &ra.ws));
+    CHK(enqueue_u16_engine(e, a, first, n, (uint16_t *)ra.rows[b], d->aux));
     HIPCHK(hipEventRecord(ra.computed[b], d->aux));
     ra.db = a;
     ra.version = a->version;
@@ -203,6 +200,8 @@ int readahead_u16_call(iris_engine *e, const iris_db *a, uint64_t first, uint64_
     HIPCHK(hipStreamWaitEvent(d->stream, ra.computed[b], 0));
     ra.pending = false;
     const uint64_t next = first + n;
+    // launched before the copy, so it overlaps it (launched after the copy's completion instead,
+    // a 20k-record masks call took 75 us rather than 51 us; tools/ra_diag.py, profiles/r03_readahead.txt)
     if (next < end) CHK(ra_launch(e, a, next, std::min<uint64_t>(n, end - next), b ^ 1));
     HIPCHK(hipMemcpyAsync(out, ra.rows[b], (size_t)n * kRot * 2, hipMemcpyDeviceToHost, d->stream));
     HIPCHK(hipEventRecord(ra.copied[b], d->stream));
@@ -779,7 +778,7 @@ int iris_engine_batch_process(iris_engine_t *e, const iris_db_t *db, uint64_t fi
     CHK(range_ok(db, first, n));
     if (n == 0) return 0;
     ARG(out, "out is NULL");
-    if (n <= kReadaheadMax && readahead_on()) return readahead_u16_call(e, db, first, n, db->len, out);
+    if (n <= kReadaheadMax && readahead_on(e)) return readahead_u16_call(e, db, first, n, db->len, out);
     CHK(ra_wait(e));
     return run_u16_engine(e, db, first, n, out);
 }
@@ -796,24 +795,7 @@ int iris_engine_batch_process_device(iris_engine_t *e, const iris_db_t *db, uint
     CHK(range_ok(db, first, n));
     if (n == 0) return 0;
     ARG(out_device, "out is NULL");
-    LaunchRange r{first, n};
-    const bool tiles = db->k.layout == IRIS_LAYOUT_TILES;
-    if (e->kind == IRIS_KIND_MASKS)
-        CHK(timed(d, "masks", n, [&] {
-            return tiles ? launch_masks_mfma(d->stream, db->data, e->qfrag, r, out_device)
-                         : launch_masks(d->stream, db->data, e->qtab, r, out_device);
-        }));
-    else {
-        void *ws = nullptr;  // K-split workspace of small ranges
-        if (tiles && shares_workspace_bytes(r)) {
-            CHK(ensure(d->out_b, shares_workspace_bytes(r)));
-            ws = d->out_b.p;
-        }
-        CHK(timed(d, "shares", n, [&] {
-            return tiles ? launch_shares_mfma(d->stream, db->data, e->qfrag, r, out_device, ws)
-                         : launch_shares(d->stream, db->data, e->qtab, r, out_device);
-        }));
-    }
+    CHK(enqueue_u16_engine(e, db, first, n, out_device));
     return sync(d);
 }
 
@@ -832,7 +814,7 @@ int iris_engine_batch_process_host(iris_engine_t *e, const void *records, uint64
         if (a->k.kind != e->kind || p < a->host_base) continue;
         const uintptr_t off = p - a->host_base;
         if (off % k.rec_bytes != 0 || off / k.rec_bytes > a->host_n || n > a->host_n - off / k.rec_bytes) continue;
-        if (n <= kReadaheadMax && readahead_on()) return readahead_u16_call(e, a, off / k.rec_bytes, n, a->host_n, out);
+        if (n <= kReadaheadMax && readahead_on(e)) return readahead_u16_call(e, a, off / k.rec_bytes, n, a->host_n, out);
         CHK(ra_wait(e));
         return run_u16_engine(e, a, off / k.rec_bytes, n, out);
     }

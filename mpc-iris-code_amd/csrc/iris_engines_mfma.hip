@@ -376,22 +376,14 @@ __device__ __forceinline__ v16i mfma_i8(const uint4 &a, const uint4 &b, const v1
     return __builtin_amdgcn_mfma_i32_32x32x32_i8(av, bv, c, 0, 0, 0);
 }
 
-// split > 1 (small ranges): wave w computes K-slice w % split of tile group
-// w / split and writes its partial rows to out + slice * slice_stride; the
-// partial dot products add up mod 2^16 (shares_combine_kernel).  Slice 0 carries
-// the query-sum bias terms; the 16384 * K_slice terms vanish (K_slice = 64 * steps).
 template <int T = kSharesTiles>
 __global__ void __launch_bounds__(256, 2)
     shares_mfma_kernel(const uint4 *__restrict__ db, const uint4 *__restrict__ qfrag, const int2 *__restrict__ qsum,
-                       uint64_t tile0, uint64_t ntiles, uint64_t first, uint64_t end, uint16_t *__restrict__ out,
-                       uint32_t split, uint64_t slice_stride) {
+                       uint64_t tile0, uint64_t ntiles, uint64_t first, uint64_t end, uint16_t *__restrict__ out) {
     const int lane = threadIdx.x & 63;
-    const uint64_t wave0 = (uint64_t)blockIdx.x * kWaveSlots + (threadIdx.x >> 6);
-    const uint32_t slice = (uint32_t)(wave0 % split);
-    const uint64_t wave = wave0 / split;
-    const int kSteps = kShareChunks / 2 / (int)split;  // steps of 2 chunks in this wave's K-slice
-    const int g0 = (int)slice * kSteps;
-    out += slice * slice_stride;
+    const uint64_t wave = (uint64_t)blockIdx.x * kWaveSlots + (threadIdx.x >> 6);
+    constexpr int kSteps = kShareChunks / 2;  // steps of 2 chunks
+    constexpr int g0 = 0;
     const uint64_t tw = wave * T;
     if (tw >= ntiles) return;
     v16i s1[T], s2[T];
@@ -466,8 +458,130 @@ __global__ void __launch_bounds__(256, 2)
         const int ehi = __shfl(s2[t][15], src) - elo;
         store_tile_rows(out, lds, (tile0 + tw + t) * kTile, first, end, tw + t < ntiles, lane, [&](int r) {
             const int k = (r & 3) + 8 * (r >> 2) + 4 * h;
-            const int2 qs = slice == 0 ? qsum[k < kRot ? k : 0] : make_int2(0, 0);  // (sum q'_lo, sum q'_hi) of row k
+            const int2 qs = qsum[k < kRot ? k : 0];  // (sum q'_lo, sum q'_hi) of row k
             // the 16384 * K terms vanish mod 2^16 (K = 12800)
+            const uint32_t lo = (uint32_t)s1[t][r] + 128u * (uint32_t)elo + 128u * (uint32_t)qs.x;
+            const uint32_t cross = (uint32_t)s2[t][r] + 128u * (uint32_t)ehi + 128u * (uint32_t)qs.x +
+                                   128u * (uint32_t)elo + 128u * (uint32_t)qs.y;
+            return (uint16_t)(lo + 256u * cross);
+        });
+    }
+}
+
+// Small ranges (the participant's 20 000-record chunks, src/main.rs:427-431): a workgroup of
+// KS waves owns T tiles and wave w sums K-slice w (kShareChunks / 2 / KS steps of 2 chunks);
+// the slices' i32 sums meet in LDS (exact mod 2^16 like every partial here) and wave 0 writes
+// the tiles' rows -- no workspace round trip through HBM and no second (combine) launch, and
+// each query-fragment load (L2) feeds T tiles.
+// shapes measured at 20k shares (one box, interleaved, profiles/r03_shares_split.txt): KS = 2 waves x
+// 1 tile 99 us per kernel, KS = 4: 102 us, KS = 8: 103 us, KS = 4 x 2 tiles: 108 us; the round-2
+// form (up to 10 slices through an HBM workspace + a combine launch) 109 + 4 us
+constexpr int kSharesSplitT = 1;
+constexpr int kSharesSplitKS = 2;
+constexpr uint64_t kSharesSplitTiles = 4096;
+
+template <int T, int KS>
+__global__ void __launch_bounds__(64 * KS, 2)
+    shares_split_kernel(const uint4 *__restrict__ db, const uint4 *__restrict__ qfrag, const int2 *__restrict__ qsum,
+                        uint64_t tile0, uint64_t ntiles, uint64_t first, uint64_t end, uint16_t *__restrict__ out) {
+    constexpr int kSteps = kShareChunks / 2 / KS;
+    static_assert(kShareChunks % (2 * KS) == 0, "K-split geometry");
+    const int lane = threadIdx.x & 63;
+    const int slice = threadIdx.x >> 6;
+    const uint64_t tw = (uint64_t)blockIdx.x * T;
+    const int g0 = slice * kSteps;
+    v16i s1[T], s2[T];
+#pragma unroll
+    for (int t = 0; t < T; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            s1[t][i] = 0;
+            s2[t][i] = 0;
+        }
+    const uint4 *dp[T];
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        const uint64_t rel = (tw + t < ntiles) ? tw + t : ntiles - 1;
+        dp[t] = db + (tile0 + rel) * (uint64_t)kShareTileUint4 + lane;
+    }
+    const uint4 *qp = qfrag + lane;
+    struct Stage {
+        uint4 lo[T][2], hi[T][2];
+        uint4 qlo[2], qhi[2];
+    };
+    auto load = [&](Stage &st, int g) {
+        g = g0 + (g < kSteps ? g : kSteps - 1);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int c = 2 * g + i;
+#pragma unroll
+            for (int t = 0; t < T; ++t) {
+                st.lo[t][i] = nt_load(dp[t] + (2 * c) * 64);
+                st.hi[t][i] = nt_load(dp[t] + (2 * c + 1) * 64);
+            }
+            st.qlo[i] = qp[(2 * c) * 64];
+            st.qhi[i] = qp[(2 * c + 1) * 64];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    auto compute = [&](const Stage &st) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int t = 0; t < T; ++t) {
+                s1[t] = mfma_i8(st.qlo[i], st.lo[t][i], s1[t]);
+                s2[t] = mfma_i8(st.qlo[i], st.hi[t][i], s2[t]);
+                s2[t] = mfma_i8(st.qhi[i], st.lo[t][i], s2[t]);
+            }
+    };
+    Stage sa, sb, sc;
+    load(sa, 0);
+    load(sb, 1);
+    int g = 0;
+#pragma unroll 1
+    for (; g + 3 <= kSteps; g += 3) {
+        load(sc, g + 2);
+        compute(sa);
+        load(sa, g + 3);
+        compute(sb);
+        load(sb, g + 4);
+        compute(sc);
+    }
+    if (g < kSteps) compute(sa);
+    if (g + 1 < kSteps) compute(sb);
+
+    __shared__ int red[KS - 1][T][2][16][64];
+    __shared__ __attribute__((aligned(16))) uint16_t sh_out[1024];
+    if (slice != 0) {
+#pragma unroll
+        for (int t = 0; t < T; ++t)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                red[slice - 1][t][0][i][lane] = s1[t][i];
+                red[slice - 1][t][1][i][lane] = s2[t][i];
+            }
+    }
+    __syncthreads();
+    if (slice != 0) return;
+#pragma unroll
+    for (int k = 0; k < KS - 1; ++k)
+#pragma unroll
+        for (int t = 0; t < T; ++t)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                s1[t][i] += red[k][t][0][i][lane];
+                s2[t][i] += red[k][t][1][i][lane];
+            }
+    // row 31 (lane t + 32, register 15) holds sum e'_lo in S1 and sum e'_hi + sum e'_lo in S2
+    const int h = lane >> 5;
+    const int src = (lane & 31) + 32;
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        const int elo = __shfl(s1[t][15], src);
+        const int ehi = __shfl(s2[t][15], src) - elo;
+        store_tile_rows(out, sh_out, (tile0 + tw + t) * kTile, first, end, tw + t < ntiles, lane, [&](int r) {
+            const int k = (r & 3) + 8 * (r >> 2) + 4 * h;
+            const int2 qs = qsum[k < kRot ? k : 0];  // (sum q'_lo, sum q'_hi) of row k
             const uint32_t lo = (uint32_t)s1[t][r] + 128u * (uint32_t)elo + 128u * (uint32_t)qs.x;
             const uint32_t cross = (uint32_t)s2[t][r] + 128u * (uint32_t)ehi + 128u * (uint32_t)qs.x +
                                    128u * (uint32_t)elo + 128u * (uint32_t)qs.y;
@@ -478,60 +592,27 @@ __global__ void __launch_bounds__(256, 2)
 
 // K-slices for a range (1 = no split): enough one-tile waves to fill the chip, a
 // divisor of the 200 steps, at most 10.
-static uint32_t shares_split(LaunchRange r) {
-    const uint64_t ntiles = tiles_of(r, 1).ntiles;
-    if (tiles_per_wave(ntiles, kSharesTiles) != 1 || getenv("IRIS_TILES_PER_WAVE")) return 1;
-    const uint64_t waves = (uint64_t)resident_blocks(2) * kWaveSlots;
-    for (uint32_t s : {1u, 2u, 4u, 5u, 8u, 10u})
-        if (ntiles * s >= waves) return s;
-    return 10;
+static bool shares_lds_split(uint64_t ntiles) {
+    return ntiles <= kSharesSplitTiles && !getenv("IRIS_TILES_PER_WAVE");
 }
 
-size_t shares_workspace_bytes(LaunchRange r) {
-    const uint32_t s = r.n ? shares_split(r) : 1;
-    return s > 1 ? (size_t)s * ((r.n * kRot + 7) / 8 * 8) * 2 : 0;  // 16-B aligned slices
-}
-
-// sum of `split` partial [n][31] u16 slices, mod 2^16
-__global__ void __launch_bounds__(256) shares_combine_kernel(const uint16_t *__restrict__ ws, uint64_t count,
-                                                             uint64_t stride, uint32_t split,
-                                                             uint16_t *__restrict__ out) {
-    typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (8 * i + 8 <= count && (((uintptr_t)out & 15) == 0)) {
-        u16x8 v = *(const u16x8 *)(ws + 8 * i);
-        for (uint32_t s = 1; s < split; ++s) v += *(const u16x8 *)(ws + s * stride + 8 * i);
-        *(u16x8 *)(out + 8 * i) = v;
-    } else {
-        for (uint64_t e = 8 * i; e < count && e < 8 * i + 8; ++e) {
-            uint16_t v = 0;
-            for (uint32_t s = 0; s < split; ++s) v = (uint16_t)(v + ws[s * stride + e]);
-            out[e] = v;
-        }
-    }
-}
-
-// ws: shares_workspace_bytes(r) bytes of device memory (16-B aligned), or null when that is 0
-int launch_shares_mfma(void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *out, void *ws) {
+int launch_shares_mfma(void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *out) {
     if (r.n == 0) return 0;
-    const int tpw = tiles_per_wave(tiles_of(r, 1).ntiles, kSharesTiles);
-    const uint32_t split = ws ? shares_split(r) : 1;
-    const Tiles t = tiles_of(r, tpw);
     const int2 *qsum = (const int2 *)((const uint4 *)qfrag + kShareFragUint4);
-    const uint64_t waves = (t.ntiles + tpw - 1) / tpw * split;
-    const uint64_t grid = (waves + kWaveSlots - 1) / kWaveSlots;
-    const uint64_t count = r.n * kRot, stride = (count + 7) / 8 * 8;
-    auto kern = tpw == 1 ? shares_mfma_kernel<1> : shares_mfma_kernel<>;
-    hipLaunchKernelGGL(kern, dim3((uint32_t)grid), dim3(256), 0, (hipStream_t)stream,
-                       (const uint4 *)db, (const uint4 *)qfrag, qsum, t.tile0, t.ntiles, r.first, r.first + r.n,
-                       split > 1 ? (uint16_t *)ws : out, split, split > 1 ? stride : 0);
-    if (hipGetLastError() != hipSuccess) return -1;
-    if (split > 1) {
-        hipLaunchKernelGGL(shares_combine_kernel, dim3((uint32_t)((count + 8 * 256 - 1) / (8 * 256))), dim3(256), 0,
-                           (hipStream_t)stream, (const uint16_t *)ws, count, stride, split, out);
-        if (hipGetLastError() != hipSuccess) return -1;
+    if (shares_lds_split(tiles_of(r, 1).ntiles)) {
+        const Tiles t = tiles_of(r, 1);
+        hipLaunchKernelGGL((shares_split_kernel<kSharesSplitT, kSharesSplitKS>),
+                           dim3((uint32_t)((t.ntiles + kSharesSplitT - 1) / kSharesSplitT)), dim3(64 * kSharesSplitKS), 0,
+                           (hipStream_t)stream, (const uint4 *)db, (const uint4 *)qfrag, qsum, t.tile0, t.ntiles, r.first,
+                           r.first + r.n, out);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
     }
-    return 0;
+    const int tpw = tiles_per_wave(tiles_of(r, 1).ntiles, kSharesTiles);
+    const Tiles t = tiles_of(r, tpw);
+    auto kern = tpw == 1 ? shares_mfma_kernel<1> : shares_mfma_kernel<>;
+    hipLaunchKernelGGL(kern, dim3((uint32_t)t.grid), dim3(256), 0, (hipStream_t)stream, (const uint4 *)db,
+                       (const uint4 *)qfrag, qsum, t.tile0, t.ntiles, r.first, r.first + r.n, out);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 // ------------------------------------------------------------------ TILES plumbing (masks, shares)

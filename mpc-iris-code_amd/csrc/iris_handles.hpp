@@ -133,7 +133,6 @@ struct Readahead {
     hipEvent_t copied[2] = {nullptr, nullptr};    // device stream, after the copy out of rows[b]
     int cur = 0;
     bool pending = false;
-    DevBuf ws;  // the K-split workspace of read-ahead DistanceEngine launches (own: concurrent)
 };
 
 struct iris_engine {

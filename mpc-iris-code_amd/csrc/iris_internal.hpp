@@ -324,8 +324,7 @@ int launch_batch(void *stream, const void *db, const void *qtiles, LaunchRange r
                  Partial *partials, Partial *out, uint64_t idx_base = 0);
 int launch_resolver(void *stream, const uint16_t *const *shares, uint32_t parts, const uint16_t *denoms, uint64_t n,
                     double *dist_out, Partial *partials);
-size_t shares_workspace_bytes(LaunchRange r);  // > 0: launch_shares_mfma splits K over slices
-int launch_shares_mfma(void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *out, void *ws);
+int launch_shares_mfma(void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *out);
 int launch_template_search(void *stream, const void *db, const void *qtab, LaunchRange r, double *dist_out,
                            Partial *partials, uint32_t *n_partials);
 // consumes partials; the winner's idx (range-relative) is offset by idx_base

@@ -181,6 +181,38 @@ int main() {
         (void)hipStreamSynchronize(s);
         std::memcpy(pageable.data(), pinned, rows);
     }, 1000);
+    // the same D2H after a kernel on the same stream, and behind a cross-stream event while the
+    // other stream runs a kernel (the read-ahead's shape)
+    void *dev2 = nullptr;
+    CK(hipMalloc(&dev2, rows));
+    hipStream_t s2;
+    CK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+    hipEvent_t e1, e2;
+    CK(hipEventCreateWithFlags(&e1, hipEventDisableTiming));
+    CK(hipEventCreateWithFlags(&e2, hipEventDisableTiming));
+    timeit("kern+d2h", [&] {
+        hipLaunchKernelGGL(k_rows_plain<0>, dim3(304), dim3(256), 0, s, (const uint4 *)dev, (uint4 *)dev2, rows / 16);
+        (void)hipMemcpyAsync(pageable.data(), dev2, rows, hipMemcpyDeviceToHost, s);
+        (void)hipStreamSynchronize(s);
+    }, 1000);
+    timeit("xwait+d2h", [&] {
+        hipLaunchKernelGGL(k_rows_plain<0>, dim3(304), dim3(256), 0, s2, (const uint4 *)dev, (uint4 *)dev2, rows / 16);
+        (void)hipEventRecord(e1, s2);
+        (void)hipStreamWaitEvent(s, e1, 0);
+        (void)hipMemcpyAsync(pageable.data(), dev2, rows, hipMemcpyDeviceToHost, s);
+        (void)hipEventRecord(e2, s);
+        (void)hipEventSynchronize(e2);
+    }, 1000);
+    timeit("xwait+d2h+k", [&] {  // + the next kernel on s2 while the copy runs
+        hipLaunchKernelGGL(k_rows_plain<0>, dim3(304), dim3(256), 0, s2, (const uint4 *)dev, (uint4 *)dev2, rows / 16);
+        (void)hipEventRecord(e1, s2);
+        (void)hipStreamWaitEvent(s, e1, 0);
+        hipLaunchKernelGGL(k_rows_plain<0>, dim3(304), dim3(256), 0, s2, (const uint4 *)dev, (uint4 *)pinned, rows / 16);
+        (void)hipMemcpyAsync(pageable.data(), dev2, rows, hipMemcpyDeviceToHost, s);
+        (void)hipEventRecord(e2, s);
+        (void)hipEventSynchronize(e2);
+    }, 1000);
+    CK(hipStreamSynchronize(s2));
     timeit("kern-to-coh", [&] {
         hipLaunchKernelGGL(k_rows, dim3(625), dim3(256), 0, s, (const uint4 *)dev, (uint4 *)pinned_c,
                            rows / 16, ticket, flag, ++seq);
