@@ -109,26 +109,20 @@ int run_u16_engine(iris_engine *e, const iris_db *db, uint64_t first, uint64_t n
 // calls of at most this many records (62 MB of rows per buffer) go through the read-ahead
 constexpr uint64_t kReadaheadMax = 1ull << 20;
 
-// Distance engines only: a masks call's 13-us kernel hides little behind its ~40-us row copy
-// (48-51 vs 57-60 us per 20k-record call), and in 4 of 6 bench runs a masks walk with read-ahead
-// fell into 275 us per call -- the copy behind a cross-stream dependency taking the runtime's
-// slow path (profiles/r03_readahead.txt) -- while a shares call (103-us kernel) gains 1.4x.
-// IRIS_READAHEAD=0 turns it off (tests run both forms).
-bool readahead_on(const iris_engine *e) {
-    if (e->kind != IRIS_KIND_SHARES) return false;
+// IRIS_READAHEAD=0 turns it off (tests run both forms)
+bool readahead_on() {
     const char *f = getenv("IRIS_READAHEAD");
     return !(f && f[0] == '0');
 }
 
-// Drops the engine's read-ahead: its kernels (side stream) and row copies (device stream) have
-// finished when this returns, so the buffers may be reused or freed.
+// Drops the engine's read-ahead: its kernels (side stream) have finished when this returns, so
+// the row buffers may be reused or freed.
 int ra_wait(iris_engine *e) {
     Readahead &ra = e->ra;
     if (!ra.computed[0]) return 0;
     iris_device *d = e->dev;
     ra.pending = false;
     if (d->aux) HIPCHK(hipStreamSynchronize(d->aux));
-    HIPCHK(hipStreamSynchronize(d->stream));
     if (d->profiling) fold_done(d);
     return 0;
 }
@@ -139,41 +133,36 @@ void ra_release(iris_engine *e) {
     (void)hipSetDevice(e->dev->ordinal);
     (void)ra_wait(e);
     for (int b = 0; b < 2; ++b) {
-        if (ra.rows[b]) (void)hipFree(ra.rows[b]);
+        if (ra.rows[b]) (void)hipHostFree(ra.rows[b]);
         (void)hipEventDestroy(ra.computed[b]);
-        (void)hipEventDestroy(ra.copied[b]);
     }
     ra = Readahead{};
 }
 
-// Enqueues the engine kernel over [first, first+n) of db into rows[b] on the device's side
-// stream, after the last copy out of rows[b]; records computed[b].
+// Enqueues the engine kernel over [first, first+n) of db on the device's side stream; it stores
+// the rows straight into the pinned buffer rows[b] (over the host link, no copy-engine DMA);
+// records computed[b].  rows[b] is not being read: the host copies out synchronously.
 int ra_launch(iris_engine *e, const iris_db *a, uint64_t first, uint64_t n, int b) {
     Readahead &ra = e->ra;
     iris_device *d = e->dev;
     CHK(ensure_aux(d));
     if (!ra.computed[0])
-        for (int i = 0; i < 2; ++i) {
-            HIPCHK(hipEventCreateWithFlags(&ra.computed[i], hipEventDisableTiming));
-            HIPCHK(hipEventCreateWithFlags(&ra.copied[i], hipEventDisableTiming));
-            HIPCHK(hipEventRecord(ra.copied[i], d->stream));  // "no copy pending" for the first waits
-        }
+        for (int i = 0; i < 2; ++i) HIPCHK(hipEventCreateWithFlags(&ra.computed[i], hipEventDisableTiming));
     const size_t bytes = (size_t)n * kRot * 2;
     if (bytes > ra.cap) {
-        CHK(ra_wait(e));  // nothing in flight uses either buffer
+        CHK(ra_wait(e));  // no kernel in flight writes either buffer
         for (int i = 0; i < 2; ++i) {
-            if (ra.rows[i]) HIPCHK(hipFree(ra.rows[i]));
+            if (ra.rows[i]) HIPCHK(hipHostFree(ra.rows[i]));
             ra.rows[i] = nullptr;
         }
         ra.cap = 0;
         const size_t want = std::max(bytes, (size_t)4096);
         for (int i = 0; i < 2; ++i) {
-            const hipError_t err = hipMalloc(&ra.rows[i], want);
+            const hipError_t err = hipHostMalloc(&ra.rows[i], want, hipHostMallocDefault);
             if (err != hipSuccess) return fail(IRIS_E_NOMEM, std::string("read-ahead rows: ") + hipGetErrorString(err));
         }
         ra.cap = want;
     }
-    HIPCHK(hipStreamWaitEvent(d->aux, ra.copied[b], 0));
     CHK(enqueue_u16_engine(e, a, first, n, (uint16_t *)ra.rows[b], d->aux));
     HIPCHK(hipEventRecord(ra.computed[b], d->aux));
     ra.db = a;
@@ -187,25 +176,21 @@ int ra_launch(iris_engine *e, const iris_db *a, uint64_t first, uint64_t n, int 
 
 // A host-output call on records [first, first+n) of db (records [0, end) exist).  Its rows come
 // from the read-ahead buffer when that holds exactly this range of this version of db, else they
-// are computed into the other buffer now; the next range of the same size is then launched on
-// the side stream into the other buffer -- it runs while this call's rows are copied into `out`
-// (the copy engines over the host link, ~1.24 MB per 20 000-record chunk) -- and the call returns
-// once its own copy is done.
+// are computed into the other buffer now; the next range of the same size is launched into the
+// other buffer before this call's rows are copied out, so the kernel overlaps the copy; the copy
+// (CPU, split over helper threads) lands the rows in `out` whatever its page size -- the copy
+// engines' DMA into a 4-KB-page pageable buffer runs at ~8 GB/s (profiles/r03_host_rows.txt).
 int readahead_u16_call(iris_engine *e, const iris_db *a, uint64_t first, uint64_t n, uint64_t end, uint16_t *out) {
     Readahead &ra = e->ra;
     iris_device *d = e->dev;
     const bool hit = ra.pending && ra.db == a && ra.version == a->version && ra.first == first && ra.n == n;
     if (!hit) CHK(ra_launch(e, a, first, n, ra.pending ? ra.cur ^ 1 : 0));
     const int b = ra.cur;
-    HIPCHK(hipStreamWaitEvent(d->stream, ra.computed[b], 0));
     ra.pending = false;
     const uint64_t next = first + n;
-    // launched before the copy, so it overlaps it (launched after the copy's completion instead,
-    // a 20k-record masks call took 75 us rather than 51 us; tools/ra_diag.py, profiles/r03_readahead.txt)
     if (next < end) CHK(ra_launch(e, a, next, std::min<uint64_t>(n, end - next), b ^ 1));
-    HIPCHK(hipMemcpyAsync(out, ra.rows[b], (size_t)n * kRot * 2, hipMemcpyDeviceToHost, d->stream));
-    HIPCHK(hipEventRecord(ra.copied[b], d->stream));
-    HIPCHK(hipEventSynchronize(ra.copied[b]));
+    HIPCHK(hipEventSynchronize(ra.computed[b]));
+    parallel_copy(out, ra.rows[b], (size_t)n * kRot * 2);
     if (d->profiling) fold_done(d);
     return 0;
 }
@@ -778,7 +763,7 @@ int iris_engine_batch_process(iris_engine_t *e, const iris_db_t *db, uint64_t fi
     CHK(range_ok(db, first, n));
     if (n == 0) return 0;
     ARG(out, "out is NULL");
-    if (n <= kReadaheadMax && readahead_on(e)) return readahead_u16_call(e, db, first, n, db->len, out);
+    if (n <= kReadaheadMax && readahead_on()) return readahead_u16_call(e, db, first, n, db->len, out);
     CHK(ra_wait(e));
     return run_u16_engine(e, db, first, n, out);
 }
@@ -814,7 +799,7 @@ int iris_engine_batch_process_host(iris_engine_t *e, const void *records, uint64
         if (a->k.kind != e->kind || p < a->host_base) continue;
         const uintptr_t off = p - a->host_base;
         if (off % k.rec_bytes != 0 || off / k.rec_bytes > a->host_n || n > a->host_n - off / k.rec_bytes) continue;
-        if (n <= kReadaheadMax && readahead_on(e)) return readahead_u16_call(e, a, off / k.rec_bytes, n, a->host_n, out);
+        if (n <= kReadaheadMax && readahead_on()) return readahead_u16_call(e, a, off / k.rec_bytes, n, a->host_n, out);
         CHK(ra_wait(e));
         return run_u16_engine(e, a, off / k.rec_bytes, n, out);
     }

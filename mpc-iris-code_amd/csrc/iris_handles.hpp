@@ -122,15 +122,15 @@ inline uint64_t next_db_version() {
 // iris_engine_batch_process): the reference's participant and resolver walk their file in
 // consecutive 20 000-record chunks (src/main.rs:427-431, 511-516), so while the rows of chunk
 // [first, first + n) are copied to the caller, the engine already computes [first + n, first + 2n)
-// on the device's side stream into its other row buffer; the next call, if it asks for exactly
-// that range of the same version of the same database, only copies those rows out.
+// on the device's side stream, its kernel storing the rows straight into the other of two pinned
+// host buffers; the next call, if it asks for exactly that range of the same version of the same
+// database, only copies those rows out.
 struct Readahead {
     const struct iris_db *db = nullptr;
     uint64_t version = 0, first = 0, n = 0;  // the range in flight into rows[cur]
-    void *rows[2] = {nullptr, nullptr};      // device [n][31] u16 rows
+    void *rows[2] = {nullptr, nullptr};      // pinned host [n][31] u16 rows
     size_t cap = 0;                          // bytes of each
     hipEvent_t computed[2] = {nullptr, nullptr};  // side stream, after the kernel into rows[b]
-    hipEvent_t copied[2] = {nullptr, nullptr};    // device stream, after the copy out of rows[b]
     int cur = 0;
     bool pending = false;
 };

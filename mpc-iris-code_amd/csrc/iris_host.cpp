@@ -208,3 +208,103 @@ void build_query_tile(const iris_template_t *q, uint32_t *tile) {
 }
 
 }  // namespace iris
+
+// ------------------------------------------------------------------ parallel host copies
+
+#include <atomic>
+#include <condition_variable>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include <unistd.h>
+
+namespace iris {
+
+namespace {
+
+// Helper threads for copying an engine call's rows out of pinned memory into the caller's
+// buffer (read-ahead, iris_api.hip): one core reads ~25 GB/s from DRAM, so a 1.24-MB
+// participant-sized chunk costs ~45 us on one thread.  The helpers spin for a while after each
+// job (calls of a chunk walk arrive every few tens of us) and then block.
+class CopyPool {
+   public:
+    explicit CopyPool(int helpers) : pid_(getpid()) {
+        for (int i = 0; i < helpers; ++i) threads_.emplace_back([this, i] { worker(i + 1); });
+        for (auto &t : threads_) t.detach();  // never joined: the pool lives as long as the process
+    }
+    pid_t pid() const { return pid_; }
+    int parts() const { return (int)threads_.size() + 1; }
+
+    void run(char *dst, const char *src, size_t bytes) {
+        std::lock_guard<std::mutex> one(run_mu_);  // one copy at a time (devices may call concurrently)
+        dst_ = dst;
+        src_ = src;
+        bytes_ = bytes;
+        remaining_.store(parts() - 1, std::memory_order_relaxed);
+        {
+            std::lock_guard<std::mutex> l(mu_);
+            gen_.fetch_add(1, std::memory_order_release);
+        }
+        cv_.notify_all();
+        part(0);
+        while (remaining_.load(std::memory_order_acquire) != 0) __builtin_ia32_pause();
+    }
+
+   private:
+    void part(int id) {
+        const size_t per = ((bytes_ + parts() - 1) / parts() + 63) & ~(size_t)63;
+        const size_t a = std::min(bytes_, (size_t)id * per), b = std::min(bytes_, a + per);
+        if (a < b) memcpy(dst_ + a, src_ + a, b - a);
+    }
+    void worker(int id) {
+        uint64_t seen = 0;
+        for (;;) {
+            uint64_t g;
+            for (int spins = 0; (g = gen_.load(std::memory_order_acquire)) == seen;) {
+                if (++spins < (1 << 16)) {
+                    __builtin_ia32_pause();
+                } else {
+                    std::unique_lock<std::mutex> l(mu_);
+                    cv_.wait(l, [&] { return gen_.load(std::memory_order_acquire) != seen; });
+                    spins = 0;
+                }
+            }
+            seen = g;
+            part(id);
+            remaining_.fetch_sub(1, std::memory_order_release);
+        }
+    }
+    pid_t pid_;
+    std::vector<std::thread> threads_;
+    std::mutex run_mu_, mu_;
+    std::condition_variable cv_;
+    std::atomic<uint64_t> gen_{0};
+    std::atomic<int> remaining_{0};
+    char *dst_ = nullptr;
+    const char *src_ = nullptr;
+    size_t bytes_ = 0;
+};
+
+constexpr int kCopyHelpers = 3;
+constexpr size_t kParallelCopyMin = 256 << 10;
+
+}  // namespace
+
+void parallel_copy(void *dst, const void *src, size_t bytes) {
+    static std::mutex create_mu;
+    static CopyPool *pool = nullptr;  // leaked on purpose (detached helpers)
+    if (bytes < kParallelCopyMin) {
+        memcpy(dst, src, bytes);
+        return;
+    }
+    CopyPool *p;
+    {
+        std::lock_guard<std::mutex> l(create_mu);
+        if (!pool || pool->pid() != getpid()) pool = new CopyPool(kCopyHelpers);  // a forked child gets its own
+        p = pool;
+    }
+    p->run((char *)dst, (const char *)src, bytes);
+}
+
+}  // namespace iris

@@ -201,3 +201,23 @@ def test_resident_range_walk_readahead(device):
         db.write(chunk, recs[chunk:2 * chunk])
         eng.batch_process(out, db, first=chunk, n=chunk)
         assert (out == oc.masks_batch(q, recs[chunk:2 * chunk])).all()
+
+
+@pytest.mark.parametrize("kind", [ih.KIND_MASKS, ih.KIND_SHARES])
+def test_participant_sized_chunks(device, kind):
+    """20 000-record chunks (1.24 MB of rows each: the read-ahead's helper-thread copy path),
+    consecutive and then repeated, against the oracle."""
+    n, chunk = (45_000, 20_000) if kind == ih.KIND_MASKS else (25_000, 20_000)
+    host = oc.gen_masks(SEED + 13, 0, n) if kind == ih.KIND_MASKS else oc.gen_shares(SEED + 13, 0, n)
+    qt = oc.gen_templates(SEED + 14, 0, 1)[0]
+    if kind == ih.KIND_MASKS:
+        eng, want = ih.MasksEngine(device, qt[200:]), oc.masks_batch(qt[200:], host)
+    else:
+        q = oc.encode(qt)
+        eng, want = ih.DistanceEngine(device, q), oc.distance_batch(q, host)
+    with eng, ih.Database(device, kind, n) as db:
+        db.attach_host(host)
+        for a in list(range(0, n, chunk)) + [0, 0, chunk]:
+            out = np.empty((min(chunk, n - a), 31), np.uint16)
+            eng.batch_process(out, host[a:a + chunk])
+            assert (out == want[a:a + chunk]).all(), a

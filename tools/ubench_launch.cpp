@@ -11,6 +11,9 @@
 #include <chrono>
 #include <cstdio>
 #include <cstring>
+#include <sys/mman.h>
+
+#include <thread>
 #include <vector>
 
 #define CK(x)                                                                    \
@@ -181,6 +184,48 @@ int main() {
         (void)hipStreamSynchronize(s);
         std::memcpy(pageable.data(), pinned, rows);
     }, 1000);
+    // destination page size: a 2-MB-aligned buffer advised to huge pages vs one forced to 4-KB pages
+    char *thp = (char *)mmap(nullptr, 8 << 20, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    char *small = (char *)mmap(nullptr, 8 << 20, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    char *thp_al = (char *)(((uintptr_t)thp + (2 << 20) - 1) & ~(uintptr_t)((2 << 20) - 1));
+    madvise(thp_al, 4 << 20, MADV_HUGEPAGE);
+    madvise(small, 8 << 20, MADV_NOHUGEPAGE);
+    std::memset(thp_al, 0, 4 << 20);
+    std::memset(small, 0, 8 << 20);
+    timeit("d2h-thp", [&] {
+        (void)hipMemcpyAsync(thp_al, dev, rows, hipMemcpyDeviceToHost, s);
+        (void)hipStreamSynchronize(s);
+    }, 1000);
+    timeit("d2h-4k", [&] {
+        (void)hipMemcpyAsync(small, dev, rows, hipMemcpyDeviceToHost, s);
+        (void)hipStreamSynchronize(s);
+    }, 1000);
+    timeit("reg+d2h-4k", [&] {  // page-lock the destination for this call only
+        (void)hipHostRegister(small, rows, hipHostRegisterDefault);
+        (void)hipMemcpyAsync(small, dev, rows, hipMemcpyDeviceToHost, s);
+        (void)hipStreamSynchronize(s);
+        (void)hipHostUnregister(small);
+    }, 300);
+    auto mt_copy = [&](char *dst, const char *src, size_t bytes, int nt) {
+        std::vector<std::thread> th;
+        const size_t per = (bytes / nt + 63) & ~(size_t)63;
+        for (int i = 0; i < nt; ++i) {
+            const size_t a = i * per, b = std::min(bytes, a + per);
+            if (a < b) th.emplace_back([=] { std::memcpy(dst + a, src + a, b - a); });
+        }
+        for (auto &t : th) t.join();
+    };
+    for (int nt : {1, 4}) {
+        char name[32];
+        std::snprintf(name, sizeof name, "kpin+cp%d-4k", nt);
+        timeit(name, [&] {
+            hipLaunchKernelGGL(k_rows_plain<0>, dim3(304), dim3(256), 0, s, (const uint4 *)dev, (uint4 *)pinned, rows / 16);
+            (void)hipStreamSynchronize(s);
+            mt_copy(small, (const char *)pinned, rows, nt);
+        }, 1000);
+    }
+    munmap(thp, 8 << 20);
+    munmap(small, 8 << 20);
     // the same D2H after a kernel on the same stream, and behind a cross-stream event while the
     // other stream runs a kernel (the read-ahead's shape)
     void *dev2 = nullptr;
