@@ -370,12 +370,6 @@ __global__ void __launch_bounds__(256) batch_reduce_kernel(const Partial *__rest
 #ifndef IRIS_BATCH2_ROLL
 #define IRIS_BATCH2_ROLL 1
 #endif
-// 1: the query-tile (A) rows are read with nontemporal loads (a workgroup's A is private to it and
-// re-read per N-group from the Infinity Cache anyway; the template tiles it would evict from the
-// XCD's L2 are shared by the XCD's 32 workgroups)
-#ifndef IRIS_BATCH2_A_NT
-#define IRIS_BATCH2_A_NT 0
-#endif
 namespace lds2 {
 constexpr int kGP = IRIS_BATCH2_GP;      // chunk pairs per K-step
 }  // namespace lds2
@@ -435,16 +429,9 @@ __global__ void __launch_bounds__(64 * NW, 1)
 #pragma unroll
         for (int i = 0; i < kAper; ++i) {
             const int r = w + NW * i;
-            if (kArows % NW == 0 || r < kArows) {
-                const uint4 *src = abase + (uint64_t)(r % kBQ) * kTileU4 + (k * kGP + r / kBQ) * 64;
-                if constexpr (IRIS_BATCH2_A_NT) {
-                    typedef unsigned int u32x4_a __attribute__((ext_vector_type(4)));
-                    const u32x4_a v = __builtin_nontemporal_load((const u32x4_a *)src);
-                    aq[i] = make_uint4(v.x, v.y, v.z, v.w);
-                } else {
-                    aq[i] = *src;
-                }
-            }
+            // plain loads: nontemporal ones (to keep the shared template tiles in L2) measured 5 %
+            // slower with more bytes from beyond L2 (4.64 vs 2.94 TB, profiles/r03_batch_a_nt.txt)
+            if (kArows % NW == 0 || r < kArows) aq[i] = abase[(uint64_t)(r % kBQ) * kTileU4 + (k * kGP + r / kBQ) * 64];
         }
     };
     auto b_row = [&](uint32_t s, int t) {  // tile t of this wave, chunk pair 0 of K-step s
