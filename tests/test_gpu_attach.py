@@ -221,3 +221,37 @@ def test_participant_sized_chunks(device, kind):
             out = np.empty((min(chunk, n - a), 31), np.uint16)
             eng.batch_process(out, host[a:a + chunk])
             assert (out == want[a:a + chunk]).all(), a
+
+
+def test_concurrent_chunk_walks(device):
+    """The participant and the resolver run their loops in worker threads (src/main.rs:425, 510):
+    two threads, each with its own engine, walk one attached array in 20 000-record chunks at the
+    same time (read-ahead kernels interleave on the side stream, copies share the helper pool)."""
+    import threading
+
+    n, chunk = 60_000, 20_000
+    host = oc.gen_masks(SEED + 15, 0, n)
+    qs = oc.gen_masks(SEED + 16, 0, 2)
+    wants = [oc.masks_batch(q, host) for q in qs]
+    errors = []
+    with ih.Database(device, ih.KIND_MASKS, n) as db:
+        db.attach_host(host)
+
+        def walk(i):
+            try:
+                with ih.MasksEngine(device, qs[i]) as eng:
+                    for rep in range(3):
+                        for a in range(0, n, chunk):
+                            out = np.empty((chunk, 31), np.uint16)
+                            eng.batch_process(out, host[a:a + chunk])
+                            if not (out == wants[i][a:a + chunk]).all():
+                                errors.append((i, rep, a))
+            except Exception as ex:  # reported below
+                errors.append((i, repr(ex)))
+
+        threads = [threading.Thread(target=walk, args=(i,)) for i in range(2)]
+        for th in threads:
+            th.start()
+        for th in threads:
+            th.join()
+    assert not errors, errors
