@@ -127,13 +127,38 @@ int ra_wait(iris_engine *e) {
     return 0;
 }
 
+constexpr size_t kRowsPoolMax = 8;
+
+// A pinned row buffer of at least `bytes` from the device's pool (at most twice the size), else new.
+int rows_take(iris_device *d, size_t bytes, void **p, size_t *got) {
+    for (size_t i = 0; i < d->rows_pool.size(); ++i) {
+        const size_t b = d->rows_pool[i].first;
+        if (b >= bytes && b <= 2 * bytes) {
+            *p = d->rows_pool[i].second;
+            *got = b;
+            d->rows_pool.erase(d->rows_pool.begin() + i);
+            return 0;
+        }
+    }
+    const hipError_t err = hipHostMalloc(p, bytes, hipHostMallocDefault);
+    if (err != hipSuccess) return fail(IRIS_E_NOMEM, std::string("read-ahead rows: ") + hipGetErrorString(err));
+    *got = bytes;
+    return 0;
+}
+
+void rows_give(iris_device *d, void *p, size_t bytes) {
+    if (!p) return;
+    if (d->rows_pool.size() < kRowsPoolMax) d->rows_pool.emplace_back(bytes, p);
+    else (void)hipHostFree(p);
+}
+
 void ra_release(iris_engine *e) {
     Readahead &ra = e->ra;
     if (!ra.computed[0]) return;
     (void)hipSetDevice(e->dev->ordinal);
-    (void)ra_wait(e);
+    (void)ra_wait(e);  // no kernel writes the buffers any more: they go back to the pool
     for (int b = 0; b < 2; ++b) {
-        if (ra.rows[b]) (void)hipHostFree(ra.rows[b]);
+        rows_give(e->dev, ra.rows[b], ra.cap);
         (void)hipEventDestroy(ra.computed[b]);
     }
     ra = Readahead{};
@@ -151,17 +176,13 @@ int ra_launch(iris_engine *e, const iris_db *a, uint64_t first, uint64_t n, int 
     const size_t bytes = (size_t)n * kRot * 2;
     if (bytes > ra.cap) {
         CHK(ra_wait(e));  // no kernel in flight writes either buffer
-        for (int i = 0; i < 2; ++i) {
-            if (ra.rows[i]) HIPCHK(hipHostFree(ra.rows[i]));
-            ra.rows[i] = nullptr;
-        }
+        for (int i = 0; i < 2; ++i) rows_give(d, ra.rows[i], ra.cap);
+        ra.rows[0] = ra.rows[1] = nullptr;
         ra.cap = 0;
         const size_t want = std::max(bytes, (size_t)4096);
-        for (int i = 0; i < 2; ++i) {
-            const hipError_t err = hipHostMalloc(&ra.rows[i], want, hipHostMallocDefault);
-            if (err != hipSuccess) return fail(IRIS_E_NOMEM, std::string("read-ahead rows: ") + hipGetErrorString(err));
-        }
-        ra.cap = want;
+        size_t got[2] = {0, 0};
+        for (int i = 0; i < 2; ++i) CHK(rows_take(d, want, &ra.rows[i], &got[i]));
+        ra.cap = std::min(got[0], got[1]);
     }
     CHK(enqueue_u16_engine(e, a, first, n, (uint16_t *)ra.rows[b], d->aux));
     HIPCHK(hipEventRecord(ra.computed[b], d->aux));
@@ -177,9 +198,10 @@ int ra_launch(iris_engine *e, const iris_db *a, uint64_t first, uint64_t n, int 
 // A host-output call on records [first, first+n) of db (records [0, end) exist).  Its rows come
 // from the read-ahead buffer when that holds exactly this range of this version of db, else they
 // are computed into the other buffer now; the next range of the same size is launched into the
-// other buffer before this call's rows are copied out, so the kernel overlaps the copy; the copy
-// (CPU, split over helper threads) lands the rows in `out` whatever its page size -- the copy
-// engines' DMA into a 4-KB-page pageable buffer runs at ~8 GB/s (profiles/r03_host_rows.txt).
+// other buffer before this call's rows are copied out, so the kernel overlaps the copy.  The copy
+// is the CPU's, split over helper threads: the copy engines' D2H of these 1.24 MB took 31 us on
+// one box and 150-275 us (8 GB/s) on others, and queued behind the side stream's event it fell
+// into the slow form on boxes that had the fast one (profiles/r03_host_rows.txt, r03_readahead.txt).
 int readahead_u16_call(iris_engine *e, const iris_db *a, uint64_t first, uint64_t n, uint64_t end, uint16_t *out) {
     Readahead &ra = e->ra;
     iris_device *d = e->dev;
@@ -328,6 +350,8 @@ void device_teardown(iris_device *d) {
         for (void *b : d->slot_blocks) (void)hipHostFree(b);
         for (auto &q : d->qpool) (void)hipFree(q.second);
         d->qpool.clear();
+        for (auto &q : d->rows_pool) (void)hipHostFree(q.second);
+        d->rows_pool.clear();
         for (auto &p : d->pending) {
             (void)hipEventDestroy(p.a);
             (void)hipEventDestroy(p.b);

@@ -94,6 +94,8 @@ struct iris_device {
     std::atomic<int> refs{1};
     // freed engines' query buffers, reused by later engines (stream-ordered)
     std::vector<std::pair<size_t, void *>> qpool;
+    // freed engines' pinned read-ahead row buffers (the participant builds an engine per request)
+    std::vector<std::pair<size_t, void *>> rows_pool;
     // databases attached to a host array (iris_db_attach_host): host-slice engine calls
     // on a range inside one of them run on the resident copy
     std::vector<struct iris_db *> attached;
