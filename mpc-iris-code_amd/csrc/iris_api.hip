@@ -109,8 +109,11 @@ int run_u16_engine(iris_engine *e, const iris_db *db, uint64_t first, uint64_t n
 // calls of at most this many records (62 MB of rows per buffer) go through the read-ahead
 constexpr uint64_t kReadaheadMax = 1ull << 20;
 
-// IRIS_READAHEAD=0 turns it off (tests run both forms)
-bool readahead_on() {
+// TILES databases only: their kernels store the rows as 16-B runs (store_tile_rows), which the
+// host link takes well; the LANES kernels' 2-byte stores would each be a host-link write.
+// IRIS_READAHEAD=0 turns it off (tests run both forms).
+bool readahead_ok(const iris_db *db, uint64_t n) {
+    if (n > kReadaheadMax || db->k.layout != IRIS_LAYOUT_TILES) return false;
     const char *f = getenv("IRIS_READAHEAD");
     return !(f && f[0] == '0');
 }
@@ -787,7 +790,7 @@ int iris_engine_batch_process(iris_engine_t *e, const iris_db_t *db, uint64_t fi
     CHK(range_ok(db, first, n));
     if (n == 0) return 0;
     ARG(out, "out is NULL");
-    if (n <= kReadaheadMax && readahead_on()) return readahead_u16_call(e, db, first, n, db->len, out);
+    if (readahead_ok(db, n)) return readahead_u16_call(e, db, first, n, db->len, out);
     CHK(ra_wait(e));
     return run_u16_engine(e, db, first, n, out);
 }
@@ -823,7 +826,7 @@ int iris_engine_batch_process_host(iris_engine_t *e, const void *records, uint64
         if (a->k.kind != e->kind || p < a->host_base) continue;
         const uintptr_t off = p - a->host_base;
         if (off % k.rec_bytes != 0 || off / k.rec_bytes > a->host_n || n > a->host_n - off / k.rec_bytes) continue;
-        if (n <= kReadaheadMax && readahead_on()) return readahead_u16_call(e, a, off / k.rec_bytes, n, a->host_n, out);
+        if (readahead_ok(a, n)) return readahead_u16_call(e, a, off / k.rec_bytes, n, a->host_n, out);
         CHK(ra_wait(e));
         return run_u16_engine(e, a, off / k.rec_bytes, n, out);
     }
