@@ -600,6 +600,8 @@ __global__ void __launch_bounds__(64 * NW, 1)
                     // (bn, bd) = (1, 0) is "none": a row with den 0 (no jointly valid bit; also the
                     // zero row k = 31) is (0, 0) and never wins, n * 0 < 1 * d holds for any real
                     // candidate, so the scan needs no validity tests
+                    // (the selects stay compare + v_cndmask: bit-field inserts under a sign mask,
+                    // forced with inline asm, measured 1.5 % slower, profiles/r03_batch_epilogue_bfi.txt)
                     uint32_t bn = 1, bd = 0, br = 0;
 #pragma unroll
                     for (int r = 0; r < 16; ++r) {
