@@ -187,6 +187,11 @@ int ra_launch(iris_engine *e, const iris_db *a, uint64_t first, uint64_t n, int 
         for (int i = 0; i < 2; ++i) CHK(rows_take(d, want, &ra.rows[i], &got[i]));
         ra.cap = std::min(got[0], got[1]);
     }
+    // ordered after everything enqueued on the device stream so far: the engine's query tables
+    // (built there when the engine was created) and any write to the database
+    if (!d->ra_order) HIPCHK(hipEventCreateWithFlags(&d->ra_order, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(d->ra_order, d->stream));
+    HIPCHK(hipStreamWaitEvent(d->aux, d->ra_order, 0));
     CHK(enqueue_u16_engine(e, a, first, n, (uint16_t *)ra.rows[b], d->aux));
     HIPCHK(hipEventRecord(ra.computed[b], d->aux));
     ra.db = a;
@@ -355,6 +360,7 @@ void device_teardown(iris_device *d) {
         d->qpool.clear();
         for (auto &q : d->rows_pool) (void)hipHostFree(q.second);
         d->rows_pool.clear();
+        if (d->ra_order) (void)hipEventDestroy(d->ra_order);
         for (auto &p : d->pending) {
             (void)hipEventDestroy(p.a);
             (void)hipEventDestroy(p.b);
@@ -584,6 +590,7 @@ int iris_db_destroy(iris_db_t *db) {
         std::lock_guard<std::recursive_mutex> g(d->mu);
         (void)hipSetDevice(d->ordinal);
         (void)hipStreamSynchronize(d->stream);
+        if (d->aux) (void)hipStreamSynchronize(d->aux);  // a read-ahead kernel may still read it
         db_detach(db);
         if (db->data) (void)hipFree(db->data);
     }

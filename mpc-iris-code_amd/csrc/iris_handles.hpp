@@ -96,6 +96,10 @@ struct iris_device {
     std::vector<std::pair<size_t, void *>> qpool;
     // freed engines' pinned read-ahead row buffers (the participant builds an engine per request)
     std::vector<std::pair<size_t, void *>> rows_pool;
+    // recorded on the device stream before every read-ahead launch and waited for by the side
+    // stream: the launch follows whatever the device stream holds (the engine's query build,
+    // writes to the database)
+    hipEvent_t ra_order = nullptr;
     // databases attached to a host array (iris_db_attach_host): host-slice engine calls
     // on a range inside one of them run on the resident copy
     std::vector<struct iris_db *> attached;

@@ -255,3 +255,32 @@ def test_concurrent_chunk_walks(device):
         for th in threads:
             th.join()
     assert not errors, errors
+
+
+@pytest.mark.parametrize("kind", [ih.KIND_MASKS, ih.KIND_SHARES])
+def test_fresh_engine_first_call(device, kind):
+    """An engine's query tables are built on the device stream when it is created, and a database
+    is written there too; the read-ahead kernels run on the side stream, so the first call of a
+    fresh engine must be ordered after both (engines reuse pooled query buffers: a call that ran
+    early would see the previous engine's query)."""
+    n = 3000 if kind == ih.KIND_MASKS else 600
+    rng = np.random.default_rng(77)
+    for it in range(6):
+        host = (oc.gen_masks(SEED + 20 + it, 0, n) if kind == ih.KIND_MASKS
+                else oc.gen_shares(SEED + 20 + it, 0, n))
+        qt = oc.gen_templates(SEED + 40 + it, 0, 1)[0]
+        with ih.Database(device, kind, n) as db:
+            db.append(host)
+            if kind == ih.KIND_MASKS:
+                eng, want = ih.MasksEngine(device, qt[200:]), oc.masks_batch(qt[200:], host)
+            else:
+                q = oc.encode(qt)
+                eng, want = ih.DistanceEngine(device, q), oc.distance_batch(q, host)
+            with eng:
+                out = np.empty((n, 31), np.uint16)
+                eng.batch_process(out, db)
+                assert (out == want).all(), it
+                a = int(rng.integers(0, n - 10))
+                out2 = np.empty((10, 31), np.uint16)
+                eng.batch_process(out2, db, first=a, n=10)
+                assert (out2 == want[a:a + 10]).all(), it
