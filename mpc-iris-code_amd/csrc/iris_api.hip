@@ -188,10 +188,16 @@ int ra_launch(iris_engine *e, const iris_db *a, uint64_t first, uint64_t n, int 
         ra.cap = std::min(got[0], got[1]);
     }
     // ordered after everything enqueued on the device stream so far: the engine's query tables
-    // (built there when the engine was created) and any write to the database
-    if (!d->ra_order) HIPCHK(hipEventCreateWithFlags(&d->ra_order, hipEventDisableTiming));
-    HIPCHK(hipEventRecord(d->ra_order, d->stream));
-    HIPCHK(hipStreamWaitEvent(d->aux, d->ra_order, 0));
+    // (built there when the engine was created) and any write to the database.  An idle device
+    // stream (the steady state of a chunk walk: its work is all on the side stream) needs no
+    // event -- the cross-stream wait costs ~10 us per launch (profiles/r03_readahead.txt)
+    const hipError_t idle = hipStreamQuery(d->stream);
+    if (idle != hipSuccess) {
+        if (idle != hipErrorNotReady) return fail(IRIS_E_HIP, std::string("hipStreamQuery: ") + hipGetErrorString(idle));
+        if (!d->ra_order) HIPCHK(hipEventCreateWithFlags(&d->ra_order, hipEventDisableTiming));
+        HIPCHK(hipEventRecord(d->ra_order, d->stream));
+        HIPCHK(hipStreamWaitEvent(d->aux, d->ra_order, 0));
+    }
     CHK(enqueue_u16_engine(e, a, first, n, (uint16_t *)ra.rows[b], d->aux));
     HIPCHK(hipEventRecord(ra.computed[b], d->aux));
     ra.db = a;
