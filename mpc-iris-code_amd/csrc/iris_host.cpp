@@ -289,6 +289,13 @@ class CopyPool {
 constexpr int kCopyHelpers = 3;
 constexpr size_t kParallelCopyMin = 256 << 10;
 
+int copy_helpers() {  // IRIS_COPY_HELPERS (0..15) overrides, read when the pool is created
+    const char *e = getenv("IRIS_COPY_HELPERS");
+    if (!e || !*e) return kCopyHelpers;
+    const int v = atoi(e);
+    return v < 0 ? 0 : v > 15 ? 15 : v;
+}
+
 }  // namespace
 
 void parallel_copy(void *dst, const void *src, size_t bytes) {
@@ -301,7 +308,7 @@ void parallel_copy(void *dst, const void *src, size_t bytes) {
     CopyPool *p;
     {
         std::lock_guard<std::mutex> l(create_mu);
-        if (!pool || pool->pid() != getpid()) pool = new CopyPool(kCopyHelpers);  // a forked child gets its own
+        if (!pool || pool->pid() != getpid()) pool = new CopyPool(copy_helpers());  // a forked child gets its own
         p = pool;
     }
     p->run((char *)dst, (const char *)src, bytes);
