@@ -359,7 +359,8 @@ __global__ void __launch_bounds__(256) batch_reduce_kernel(const Partial *__rest
 // Diagnostic builds (tools/, never the shipped library; results wrong by design):
 // IRIS_BATCH2_DIAG = 1 no s_barrier, 2 no LDS fragment reads (the B operands stand in),
 // 3 no B loads after the first step, 4 no A loads / expansion after the first step,
-// 5 no MFMAs (a VALU fold keeps the operands live)
+// 5 no MFMAs (a VALU fold keeps the operands live), 6 the template (B) operands expanded for chunk pair 0
+// only and reused for the K-step's other pairs (their loads still consumed)
 #ifndef IRIS_BATCH2_DIAG
 #define IRIS_BATCH2_DIAG 0
 #endif
@@ -539,6 +540,7 @@ __global__ void __launch_bounds__(64 * NW, 1)
             fa[qi] = frag(0, 0, qi);
             fe[qi] = frag(0, 1, qi);
         }
+        v8i sd[2][WT], se[2][WT];  // IRIS_BATCH2_DIAG 6: chunk pair 0's expansions, reused
 #pragma unroll
         for (int b = 0; b < 2 * kGP; ++b) {
             const bool nb = b + 1 < 2 * kGP;
@@ -546,11 +548,21 @@ __global__ void __launch_bounds__(64 * NW, 1)
 #pragma unroll
             for (int t = 0; t < WT; ++t) {
                 const uint4 q = bq[t][b >> 1];
+                if (IRIS_BATCH2_DIAG == 6 && b >= 2) {  // the load is consumed where the shipped kernel expands it
+                    asm volatile("" ::"v"(q.x), "v"(q.y), "v"(q.z), "v"(q.w));
+                    bd[t] = sd[b & 1][t];
+                    be[t] = se[b & 1][t];
+                    continue;
+                }
                 const uint32_t bx = (b & 1) ? q.z : q.x, by = (b & 1) ? q.w : q.y;
                 bd[t] = v8i{(int)(bx & 0x22222222u), (int)(bx & 0x11111111u), (int)(by & 0x22222222u),
                             (int)(by & 0x11111111u), 0, 0, 0, 0};
                 be[t] = v8i{(int)(bx & 0xAAAAAAAAu), (int)((bx << 1) & 0xAAAAAAAAu), (int)(by & 0xAAAAAAAAu),
                             (int)((by << 1) & 0xAAAAAAAAu), 0, 0, 0, 0};
+                if (IRIS_BATCH2_DIAG == 6) {
+                    sd[b & 1][t] = bd[t];
+                    se[b & 1][t] = be[t];
+                }
             }
             if ((b & 1) && (IRIS_BATCH2_DIAG != 3 || s == 0)) {  // both chunks of chunk pair b >> 1 expanded: its registers take step s + 1's
 #pragma unroll
