@@ -17,6 +17,8 @@
  *    reference's synchronous `batch_process` (src/lib.rs:42,69).
  *  - Handles are thread-safe: calls on one device are serialised internally
  *    (the reference engines are `Sync` and shared by rayon workers).
+ *  - Calls switch to their handle's device internally and leave the calling
+ *    thread's current HIP device as they found it.
  *  - Record layouts are the reference's in-memory / on-disk layouts
  *    (bytemuck views, little-endian):
  *      Bits        = uint64_t[200]            (src/bits.rs:13-15)      1600 B

@@ -422,6 +422,7 @@ int iris_device_count(int *count) {
 }
 
 int iris_device_open(int ordinal, iris_device_t **out) {
+    IRIS_KEEP_DEVICE();
     ARG(out, "out is NULL");
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(IRIS_E_NODEV, "no HIP device visible");
@@ -453,12 +454,14 @@ int iris_device_open(int ordinal, iris_device_t **out) {
 }
 
 int iris_device_close(iris_device_t *d) {
+    IRIS_KEEP_DEVICE();
     if (!d) return 0;
     device_release(d);  // torn down now, or when its last database / engine is destroyed
     return 0;
 }
 
 int iris_device_synchronize(iris_device_t *d) {
+    IRIS_KEEP_DEVICE();
     ARG(d, "device is NULL");
     std::lock_guard<std::recursive_mutex> g(d->mu);
     CHK(set_device(d));
@@ -472,6 +475,7 @@ int iris_device_stream(iris_device_t *d, void **stream) {
 }
 
 int iris_device_memory(iris_device_t *d, size_t *free_bytes, size_t *total_bytes) {
+    IRIS_KEEP_DEVICE();
     ARG(d && free_bytes && total_bytes, "NULL argument");
     std::lock_guard<std::recursive_mutex> g(d->mu);
     CHK(set_device(d));
@@ -480,6 +484,7 @@ int iris_device_memory(iris_device_t *d, size_t *free_bytes, size_t *total_bytes
 }
 
 int iris_device_set_profiling(iris_device_t *d, int enabled) {
+    IRIS_KEEP_DEVICE();
     ARG(d, "device is NULL");
     std::lock_guard<std::recursive_mutex> g(d->mu);
     d->profiling = enabled != 0;
@@ -488,6 +493,7 @@ int iris_device_set_profiling(iris_device_t *d, int enabled) {
 
 int iris_device_kernel_stats(iris_device_t *d, const char *kernel, uint64_t *launches, double *total_ms,
                              uint64_t *items) {
+    IRIS_KEEP_DEVICE();
     ARG(d && kernel, "NULL argument");
     std::lock_guard<std::recursive_mutex> g(d->mu);
     auto it = d->stats.find(kernel);
@@ -499,6 +505,7 @@ int iris_device_kernel_stats(iris_device_t *d, const char *kernel, uint64_t *lau
 }
 
 int iris_device_reset_stats(iris_device_t *d) {
+    IRIS_KEEP_DEVICE();
     ARG(d, "device is NULL");
     std::lock_guard<std::recursive_mutex> g(d->mu);
     d->stats.clear();
@@ -506,6 +513,7 @@ int iris_device_reset_stats(iris_device_t *d) {
 }
 
 int iris_device_alloc(iris_device_t *d, size_t bytes, void **ptr) {
+    IRIS_KEEP_DEVICE();
     ARG(d && ptr, "NULL argument");
     std::lock_guard<std::recursive_mutex> g(d->mu);
     CHK(set_device(d));
@@ -515,6 +523,7 @@ int iris_device_alloc(iris_device_t *d, size_t bytes, void **ptr) {
 }
 
 int iris_device_free(iris_device_t *d, void *ptr) {
+    IRIS_KEEP_DEVICE();
     ARG(d, "device is NULL");
     std::lock_guard<std::recursive_mutex> g(d->mu);
     CHK(set_device(d));
@@ -523,6 +532,7 @@ int iris_device_free(iris_device_t *d, void *ptr) {
 }
 
 int iris_memcpy_d2h(iris_device_t *d, void *host, const void *device, size_t bytes) {
+    IRIS_KEEP_DEVICE();
     ARG(d && (bytes == 0 || (host && device)), "NULL argument");
     std::lock_guard<std::recursive_mutex> g(d->mu);
     CHK(set_device(d));
@@ -531,6 +541,7 @@ int iris_memcpy_d2h(iris_device_t *d, void *host, const void *device, size_t byt
 }
 
 int iris_memcpy_h2d(iris_device_t *d, void *device, const void *host, size_t bytes) {
+    IRIS_KEEP_DEVICE();
     ARG(d && (bytes == 0 || (host && device)), "NULL argument");
     std::lock_guard<std::recursive_mutex> g(d->mu);
     CHK(set_device(d));
@@ -545,6 +556,7 @@ int iris_db_create(iris_device_t *d, int kind, uint64_t capacity, iris_db_t **ou
 }
 
 int iris_db_create_ex(iris_device_t *d, int kind, uint64_t capacity, int layout, iris_db_t **out) {
+    IRIS_KEEP_DEVICE();
     ARG(d && out, "NULL argument");
     CHK(check_kind(kind));
     if (layout == IRIS_LAYOUT_DEFAULT) layout = IRIS_LAYOUT_TILES;
@@ -590,6 +602,7 @@ int iris_db_layout(const iris_db_t *db, int *layout) {
 }
 
 int iris_db_destroy(iris_db_t *db) {
+    IRIS_KEEP_DEVICE();
     if (!db) return 0;
     iris_device *d = db->dev;
     {
@@ -624,6 +637,7 @@ int iris_db_kind(const iris_db_t *db, int *kind) {
 }
 
 int iris_db_append(iris_db_t *db, const void *records, uint64_t n) {
+    IRIS_KEEP_DEVICE();
     ARG(db, "database is NULL");
     std::lock_guard<std::recursive_mutex> g(db->dev->mu);
     CHK(set_device(db->dev));
@@ -631,6 +645,7 @@ int iris_db_append(iris_db_t *db, const void *records, uint64_t n) {
 }
 
 int iris_db_write(iris_db_t *db, uint64_t index, const void *records, uint64_t n) {
+    IRIS_KEEP_DEVICE();
     ARG(db, "database is NULL");
     std::lock_guard<std::recursive_mutex> g(db->dev->mu);
     CHK(set_device(db->dev));
@@ -638,6 +653,7 @@ int iris_db_write(iris_db_t *db, uint64_t index, const void *records, uint64_t n
 }
 
 int iris_db_read(const iris_db_t *db, uint64_t first, uint64_t n, void *records) {
+    IRIS_KEEP_DEVICE();
     ARG(db, "database is NULL");
     iris_device *d = db->dev;
     std::lock_guard<std::recursive_mutex> g(d->mu);
@@ -659,6 +675,7 @@ int iris_db_read(const iris_db_t *db, uint64_t first, uint64_t n, void *records)
 }
 
 int iris_db_generate(iris_db_t *db, uint64_t n, uint64_t seed, uint64_t global_index0) {
+    IRIS_KEEP_DEVICE();
     ARG(db, "database is NULL");
     iris_device *d = db->dev;
     std::lock_guard<std::recursive_mutex> g(d->mu);
@@ -673,6 +690,7 @@ int iris_db_generate(iris_db_t *db, uint64_t n, uint64_t seed, uint64_t global_i
 }
 
 int iris_db_truncate(iris_db_t *db, uint64_t len) {
+    IRIS_KEEP_DEVICE();
     ARG(db, "database is NULL");
     std::lock_guard<std::recursive_mutex> g(db->dev->mu);
     if (len > db->len) return fail(IRIS_E_RANGE, "iris_db_truncate: len beyond the current length");
@@ -682,6 +700,7 @@ int iris_db_truncate(iris_db_t *db, uint64_t len) {
 }
 
 int iris_db_attach_host(iris_db_t *db, const void *host, uint64_t n, int upload) {
+    IRIS_KEEP_DEVICE();
     ARG(db && (host || n == 0), "NULL argument");
     ARG(db->k.layout != IRIS_LAYOUT_TRITS, "a TRITS database does not hold the records exactly (search-only layout)");
     iris_device *d = db->dev;
@@ -713,6 +732,7 @@ int iris_db_attach_host(iris_db_t *db, const void *host, uint64_t n, int upload)
 }
 
 int iris_db_detach_host(iris_db_t *db) {
+    IRIS_KEEP_DEVICE();
     ARG(db, "database is NULL");
     std::lock_guard<std::recursive_mutex> g(db->dev->mu);
     db_detach(db);
@@ -720,6 +740,7 @@ int iris_db_detach_host(iris_db_t *db) {
 }
 
 int iris_db_clear(iris_db_t *db) {
+    IRIS_KEEP_DEVICE();
     ARG(db, "database is NULL");
     std::lock_guard<std::recursive_mutex> g(db->dev->mu);
     CHK(set_device(db->dev));
@@ -734,6 +755,7 @@ int iris_db_clear(iris_db_t *db) {
 // ------------------------------------------------------------------ engines
 
 int iris_masks_engine_new(iris_device_t *d, const uint64_t query_mask[IRIS_LIMBS], iris_engine_t **out) {
+    IRIS_KEEP_DEVICE();
     ARG(d && query_mask && out, "NULL argument");
     std::lock_guard<std::recursive_mutex> g(d->mu);
     CHK(set_device(d));
@@ -744,6 +766,7 @@ int iris_masks_engine_new(iris_device_t *d, const uint64_t query_mask[IRIS_LIMBS
 }
 
 int iris_distance_engine_new(iris_device_t *d, const uint16_t query[IRIS_BITS], iris_engine_t **out) {
+    IRIS_KEEP_DEVICE();
     ARG(d && query && out, "NULL argument");
     std::lock_guard<std::recursive_mutex> g(d->mu);
     CHK(set_device(d));
@@ -774,6 +797,7 @@ int iris_api::template_engine_locked(iris_device *d, const iris_template_t *quer
 extern "C" {
 
 int iris_template_engine_new(iris_device_t *d, const iris_template_t *query, iris_engine_t **out) {
+    IRIS_KEEP_DEVICE();
     ARG(d && query && out, "NULL argument");
     std::lock_guard<std::recursive_mutex> g(d->mu);
     CHK(set_device(d));
@@ -783,6 +807,7 @@ int iris_template_engine_new(iris_device_t *d, const iris_template_t *query, iri
 }
 
 int iris_engine_destroy(iris_engine_t *e) {
+    IRIS_KEEP_DEVICE();
     if (!e) return 0;
     iris_device *d = e->dev;
     {
@@ -794,6 +819,7 @@ int iris_engine_destroy(iris_engine_t *e) {
 }
 
 int iris_engine_batch_process(iris_engine_t *e, const iris_db_t *db, uint64_t first, uint64_t n, uint16_t *out) {
+    IRIS_KEEP_DEVICE();
     ARG(e && db, "NULL argument");
     ARG(e->kind == IRIS_KIND_MASKS || e->kind == IRIS_KIND_SHARES, "batch_process needs a masks or distance engine");
     ARG(db->k.kind == e->kind, "engine kind does not match the database kind");
@@ -810,6 +836,7 @@ int iris_engine_batch_process(iris_engine_t *e, const iris_db_t *db, uint64_t fi
 
 int iris_engine_batch_process_device(iris_engine_t *e, const iris_db_t *db, uint64_t first, uint64_t n,
                                      uint16_t *out_device) {
+    IRIS_KEEP_DEVICE();
     ARG(e && db, "NULL argument");
     ARG(e->kind == IRIS_KIND_MASKS || e->kind == IRIS_KIND_SHARES, "batch_process needs a masks or distance engine");
     ARG(db->k.kind == e->kind, "engine kind does not match the database kind");
@@ -825,6 +852,7 @@ int iris_engine_batch_process_device(iris_engine_t *e, const iris_db_t *db, uint
 }
 
 int iris_engine_batch_process_host(iris_engine_t *e, const void *records, uint64_t n, uint16_t *out) {
+    IRIS_KEEP_DEVICE();
     ARG(e, "engine is NULL");
     ARG(e->kind == IRIS_KIND_MASKS || e->kind == IRIS_KIND_SHARES, "batch_process needs a masks or distance engine");
     iris_device *d = e->dev;
@@ -865,6 +893,7 @@ static int template_args(iris_engine_t *e, const iris_db_t *db) {
 
 int iris_template_counts(iris_engine_t *e, const iris_db_t *db, uint64_t first, uint64_t n, uint16_t *num_out,
                          uint16_t *den_out) {
+    IRIS_KEEP_DEVICE();
     CHK(template_args(e, db));
     iris_device *d = e->dev;
     std::lock_guard<std::recursive_mutex> g(d->mu);
@@ -1062,6 +1091,7 @@ static int pair_search_locked(iris_engine_t *a, iris_engine_t *b, const iris_db_
 
 int iris_template_search(iris_engine_t *e, const iris_db_t *db, uint64_t first, uint64_t n, uint64_t index_base,
                          double *dist_out_device, iris_match_t *out) {
+    IRIS_KEEP_DEVICE();
     CHK(template_args(e, db));
     std::lock_guard<std::recursive_mutex> g(e->dev->mu);
     CHK(set_device(e->dev));
@@ -1100,6 +1130,7 @@ struct iris_pending {
 
 int iris_template_search_async(iris_engine_t *e, const iris_db_t *db, uint64_t first, uint64_t n,
                                uint64_t index_base, iris_pending_t **out) {
+    IRIS_KEEP_DEVICE();
     CHK(template_args(e, db));
     ARG(out, "out is NULL");
     iris_device *d = e->dev;
@@ -1129,6 +1160,7 @@ int iris_template_search_async(iris_engine_t *e, const iris_db_t *db, uint64_t f
 }
 
 int iris_pending_wait(iris_pending_t *p, iris_match_t *out) {
+    IRIS_KEEP_DEVICE();
     ARG(p, "pending is NULL");
     iris_device *d = p->dev;
     hipError_t err = hipSuccess;
@@ -1150,6 +1182,7 @@ int iris_pending_wait(iris_pending_t *p, iris_match_t *out) {
 }
 
 int iris_template_distances(iris_engine_t *e, const iris_db_t *db, uint64_t first, uint64_t n, double *out) {
+    IRIS_KEEP_DEVICE();
     CHK(template_args(e, db));
     iris_device *d = e->dev;
     std::lock_guard<std::recursive_mutex> g(d->mu);
@@ -1172,6 +1205,7 @@ int iris_template_distances(iris_engine_t *e, const iris_db_t *db, uint64_t firs
 // ------------------------------------------------------------------ batched queries
 
 int iris_template_batch_engine_new(iris_device_t *d, const iris_template_t *queries, uint32_t nq, iris_engine_t **out) {
+    IRIS_KEEP_DEVICE();
     ARG(d && out && (nq == 0 || queries), "NULL argument");
     ARG(nq > 0, "a batch needs at least one query");
     std::lock_guard<std::recursive_mutex> g(d->mu);
@@ -1209,6 +1243,7 @@ int iris_template_batch_engine_new(iris_device_t *d, const iris_template_t *quer
 
 int iris_template_batch_search(iris_engine_t *e, const iris_db_t *db, uint64_t first, uint64_t n, uint64_t index_base,
                                iris_match_t *out) {
+    IRIS_KEEP_DEVICE();
     ARG(e && db && out, "NULL argument");
     ARG(e->kind == IRIS_KIND_TEMPLATES && e->nq > 0, "not a batched template engine");
     ARG(db->k.kind == IRIS_KIND_TEMPLATES, "database does not hold templates");
@@ -1278,6 +1313,7 @@ static int resolver_finish(iris_device *d, uint32_t np, Partial *res) {
 // host calls merge the per-chunk winners on the host in chunk order.
 int iris_resolver_search(iris_device_t *d, const uint16_t *const *shares, uint32_t parts, const uint16_t *denoms,
                          uint64_t n, uint64_t index_base, double *dist_out_device, iris_match_t *out) {
+    IRIS_KEEP_DEVICE();
     ARG(d && out, "NULL argument");
     ARG(parts >= 1 && parts <= 8, "parts must be 1..8");
     ARG(n == 0 || (shares && denoms), "NULL argument");
@@ -1302,6 +1338,7 @@ int iris_resolver_search(iris_device_t *d, const uint16_t *const *shares, uint32
 int iris_resolver_search_masks(iris_engine_t *e, const iris_db_t *db, uint64_t first, uint64_t n,
                                const uint16_t *const *shares_device, uint32_t parts, uint64_t index_base,
                                double *dist_out_device, iris_match_t *out) {
+    IRIS_KEEP_DEVICE();
     ARG(e && db && out, "NULL argument");
     ARG(parts >= 1 && parts <= 8, "parts must be 1..8");
     ARG(e->kind == IRIS_KIND_MASKS && db->k.kind == IRIS_KIND_MASKS, "needs a masks engine and a masks database");
@@ -1339,6 +1376,7 @@ int iris_resolver_search_masks(iris_engine_t *e, const iris_db_t *db, uint64_t f
 
 int iris_resolver_search_host(iris_device_t *d, const uint16_t *const *shares, uint32_t parts, const uint16_t *denoms,
                               uint64_t n, uint64_t index_base, iris_match_t *out) {
+    IRIS_KEEP_DEVICE();
     ARG(d && out, "NULL argument");
     ARG(parts >= 1 && parts <= 8, "parts must be 1..8");
     ARG(n == 0 || (shares && denoms), "NULL argument");
@@ -1372,6 +1410,7 @@ int iris_resolver_search_host(iris_device_t *d, const uint16_t *const *shares, u
 
 int iris_dot_bool_batch(iris_device_t *d, const uint64_t *a, uint64_t na, const uint64_t *b, uint64_t nb,
                         uint16_t *out) {
+    IRIS_KEEP_DEVICE();
     ARG(d, "device is NULL");
     std::lock_guard<std::recursive_mutex> g(d->mu);
     CHK(set_device(d));
@@ -1402,6 +1441,7 @@ int iris_dot_bool_batch(iris_device_t *d, const uint64_t *a, uint64_t na, const 
 
 int iris_dot_u16_batch(iris_device_t *d, const uint16_t *a, uint64_t na, const uint16_t *b, uint64_t nb,
                        uint16_t *out) {
+    IRIS_KEEP_DEVICE();
     ARG(d, "device is NULL");
     std::lock_guard<std::recursive_mutex> g(d->mu);
     CHK(set_device(d));
@@ -1489,6 +1529,7 @@ int iris_query_table_sizes(int kind, uint32_t nq, size_t *tab_bytes, size_t *fra
 }
 
 int iris_engine_query_tables(const iris_engine_t *e, void *tab, size_t tab_bytes, void *frag, size_t frag_bytes) {
+    IRIS_KEEP_DEVICE();
     ARG(e, "engine is NULL");
     ARG(e->sub.empty(), "a streamed batch engine (<= 3 queries) holds one engine per query");
     size_t tb = 0, fb = 0;

@@ -175,6 +175,7 @@ int iris_group_unique_id(uint8_t id[IRIS_GROUP_ID_BYTES]) {
 }
 
 int iris_group_create(const int *ordinals, uint32_t n, iris_group_t **out) {
+    IRIS_KEEP_DEVICE();
     ARG(ordinals && out && n > 0, "a group needs at least one device");
     iris_group *g = new (std::nothrow) iris_group();
     if (!g) return fail(IRIS_E_NOMEM, "out of host memory");
@@ -200,6 +201,7 @@ int iris_group_create(const int *ordinals, uint32_t n, iris_group_t **out) {
 
 int iris_group_create_rank(int ordinal, uint32_t nranks, uint32_t rank, const uint8_t id[IRIS_GROUP_ID_BYTES],
                            iris_group_t **out) {
+    IRIS_KEEP_DEVICE();
     ARG(id && out, "NULL argument");
     ARG(nranks > 0 && rank < nranks, "rank must be below nranks");
     iris_group *g = new (std::nothrow) iris_group();
@@ -227,6 +229,7 @@ int iris_group_create_rank(int ordinal, uint32_t nranks, uint32_t rank, const ui
 }
 
 int iris_group_destroy(iris_group_t *g) {
+    IRIS_KEEP_DEVICE();
     if (!g) return 0;
     group_release(g);  // torn down now, or with its last database / pending search
     return 0;
@@ -248,6 +251,7 @@ int iris_group_device(const iris_group_t *g, uint32_t i, iris_device_t **dev) {
 }
 
 int iris_group_db_destroy(iris_group_db_t *gdb) {
+    IRIS_KEEP_DEVICE();
     if (!gdb) return 0;
     iris_group *g = gdb->g;
     {
@@ -259,6 +263,7 @@ int iris_group_db_destroy(iris_group_db_t *gdb) {
 }
 
 int iris_group_db_create(iris_group_t *g, int kind, uint64_t total, int layout, uint32_t spd, iris_group_db_t **out) {
+    IRIS_KEEP_DEVICE();
     ARG(g && out, "NULL argument");
     ARG(spd >= 1, "shards_per_device must be at least 1");
     CHK(check_kind(kind));
@@ -325,6 +330,7 @@ int iris_group_db_shard(const iris_group_db_t *gdb, uint32_t i, iris_db_t **db, 
 }
 
 int iris_group_db_generate(iris_group_db_t *gdb, uint64_t seed) {
+    IRIS_KEEP_DEVICE();
     ARG(gdb, "NULL argument");
     iris_group *g = gdb->g;
     std::lock_guard<std::mutex> gl(g->mu);
@@ -342,6 +348,7 @@ int iris_group_db_generate(iris_group_db_t *gdb, uint64_t seed) {
 }
 
 int iris_group_db_write(iris_group_db_t *gdb, uint64_t index, const void *records, uint64_t n) {
+    IRIS_KEEP_DEVICE();
     ARG(gdb, "NULL argument");
     if (index > gdb->total || n > gdb->total - index) return fail(IRIS_E_RANGE, "record range outside the group database");
     if (n == 0) return 0;
@@ -357,6 +364,7 @@ int iris_group_db_write(iris_group_db_t *gdb, uint64_t index, const void *record
 }
 
 int iris_group_db_read(const iris_group_db_t *gdb, uint64_t index, uint64_t n, void *records) {
+    IRIS_KEEP_DEVICE();
     ARG(gdb, "NULL argument");
     if (index > gdb->total || n > gdb->total - index) return fail(IRIS_E_RANGE, "record range outside the group database");
     if (n == 0) return 0;
@@ -376,6 +384,7 @@ int iris_group_db_read(const iris_group_db_t *gdb, uint64_t index, uint64_t n, v
 }
 
 int iris_group_db_load_file(iris_group_db_t *gdb, const char *path, uint64_t first) {
+    IRIS_KEEP_DEVICE();
     ARG(gdb && path, "NULL argument");
     iris_group *g = gdb->g;
     std::lock_guard<std::mutex> gl(g->mu);
@@ -398,6 +407,7 @@ int iris_group_db_load_file(iris_group_db_t *gdb, const char *path, uint64_t fir
 }
 
 int iris_group_template_search_async(iris_group_db_t *gdb, const iris_template_t *query, iris_group_pending_t **out) {
+    IRIS_KEEP_DEVICE();
     CHK(search_args(gdb));
     ARG(query && out, "NULL argument");
     iris_group *g = gdb->g;
@@ -469,6 +479,7 @@ int iris_group_template_search_async(iris_group_db_t *gdb, const iris_template_t
 }
 
 int iris_group_pending_wait(iris_group_pending_t *p, iris_match_t *out) {
+    IRIS_KEEP_DEVICE();
     ARG(p, "pending is NULL");
     iris_group *g = p->g;
     const size_t L = g->devs.size();
@@ -496,6 +507,7 @@ int iris_group_pending_wait(iris_group_pending_t *p, iris_match_t *out) {
 }
 
 int iris_group_template_search(iris_group_db_t *gdb, const iris_template_t *query, iris_match_t *out) {
+    IRIS_KEEP_DEVICE();
     ARG(out, "out is NULL");
     iris_group_pending *p = nullptr;
     CHK(iris_group_template_search_async(gdb, query, &p));
@@ -504,6 +516,7 @@ int iris_group_template_search(iris_group_db_t *gdb, const iris_template_t *quer
 
 int iris_group_template_batch_search(iris_group_db_t *gdb, const iris_template_t *queries, uint32_t nq,
                                      iris_match_t *out) {
+    IRIS_KEEP_DEVICE();
     CHK(search_args(gdb));
     ARG(queries && out, "NULL argument");
     ARG(nq > 0, "a batch needs at least one query");

@@ -168,6 +168,22 @@ inline int set_device(iris_device *d) {
     return 0;
 }
 
+// The library switches to a handle's device for its own HIP calls; every entry point that may do so
+// declares IRIS_KEEP_DEVICE() first, which puts the calling thread back on its own current device
+// when the call returns (a C caller's or a framework's device choice is left as it was).
+struct KeepDevice {
+    int prev = -1;
+    KeepDevice() {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    }
+    ~KeepDevice() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+    KeepDevice(const KeepDevice &) = delete;
+    KeepDevice &operator=(const KeepDevice &) = delete;
+};
+#define IRIS_KEEP_DEVICE() iris_api::KeepDevice keep_device_
+
 inline int ensure(DevBuf &b, size_t bytes) {
     if (bytes <= b.cap) return 0;
     if (b.p) HIPCHK(hipFree(b.p));

@@ -98,6 +98,7 @@ const char *kind_name(int kind) {
 extern "C" {
 
 int iris_db_load_file(iris_db_t *db, const char *path, uint64_t first, uint64_t count, uint64_t *loaded) {
+    IRIS_KEEP_DEVICE();
     ARG(db && path, "NULL argument");
     if (loaded) *loaded = 0;
     iris_device *d = db->dev;
@@ -226,6 +227,7 @@ int iris_db_load_file(iris_db_t *db, const char *path, uint64_t first, uint64_t 
 }
 
 int iris_db_save_file(const iris_db_t *db, const char *path, uint64_t first, uint64_t n) {
+    IRIS_KEEP_DEVICE();
     ARG(db && path, "NULL argument");
     // TRITS keeps pattern & mask only: a saved file would silently differ from what was loaded
     if (db->k.layout == IRIS_LAYOUT_TRITS)

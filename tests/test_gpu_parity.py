@@ -701,3 +701,45 @@ def test_concurrent_callers(device):
     for (wm, wo), (gm, go) in zip(want, got):
         assert gm.index == wm.index and bits_eq(gm.distance, wm.distance)
         assert (go == wo).all()
+
+
+def test_calls_keep_the_callers_current_device(device):
+    """Every entry point that switches to its handle's device puts the calling thread back on
+    its own current device (include/iris_hip.h); with one GPU only the path is exercised (the
+    before / after devices are equal by construction), from a fresh thread and from this one."""
+    import ctypes
+    import threading
+
+    # by soname: the HIP runtime instance libiris_hip.so is bound to (torch's copy, if torch came first)
+    hip = ctypes.CDLL("libamdhip64.so.7")
+    cur = ctypes.c_int(-1)
+
+    def current():
+        assert hip.hipGetDevice(ctypes.byref(cur)) == 0
+        return cur.value
+
+    t = oc.gen_templates(5, 0, 700)
+
+    def calls():
+        before = current()
+        db = ih.Database(device, ih.KIND_TEMPLATES, len(t))
+        db.append(t)
+        with ih.TemplateEngine(device, t[3]) as te:
+            m = te.search(db)
+        db.close()
+        assert m.index == 3 and m.distance == 0.0
+        assert current() == before
+
+    calls()
+    errors = []
+
+    def in_thread():
+        try:
+            calls()
+        except Exception as ex:  # reported below
+            errors.append(ex)
+
+    th = threading.Thread(target=in_thread)
+    th.start()
+    th.join()
+    assert not errors
