@@ -812,7 +812,10 @@ int iris_engine_destroy(iris_engine_t *e) {
     iris_device *d = e->dev;
     {
         std::lock_guard<std::recursive_mutex> g(d->mu);
-        engine_free(e);  // no wait: the buffers go back to the device's pool, reuse is stream-ordered
+        // no wait on the device stream: the query buffer goes back to the device's pool and its
+        // reuse is stream-ordered; an engine that read ahead waits for its side-stream kernels
+        // before its pinned row buffers go back (ra_release)
+        engine_free(e);
     }
     device_release(d);
     return 0;
