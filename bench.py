@@ -54,7 +54,6 @@ FP4_DENSE_PEAK_MACS = 10e15 / 2            # MI355X_MICROARCH.md: ~10 PF dense f
 MFMA_MACS_PER_TEMPLATE = 2 * 12800 * 31    # algorithmic: den + enc products of the 31 rotations
 MFMA_MACS_ISSUED_PER_TEMPLATE = 2 * 12800 * 32  # issued: the 32x32 tile carries a zero 32nd row
 BYTES_PER_TEMPLATE = 3200    # pattern + mask planes, read once per query
-TRITS_BYTES_PER_TEMPLATE = 2560  # --layout trits: 12800 three-state positions, five per byte
 VALU_OPS_PER_TEMPLATE = 400 * 31 * 4   # words x rotations x (and, bitop3, 2x bcnt)
 ROT = 31
 SEED = 20251015
@@ -80,7 +79,7 @@ def parse():
                     help="seconds of untimed steps before the warmup steps (the GPU reaches its steady "
                          "streaming rate after ~0.5-1 s of load)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--layout", choices=["tiles", "lanes", "trits"], default="tiles",
+    ap.add_argument("--layout", choices=["tiles", "lanes"], default="tiles",
                     help="tiles = MFMA kernels (default), lanes = VALU kernels")
     ap.add_argument("--queries", type=int, default=1024, help="queries per batch (workload batch)")
     ap.add_argument("--workload", choices=list(GPU_WORKLOADS + AUX_WORKLOADS), default="search",
@@ -806,11 +805,9 @@ def main():
         if world_gpus > 1:
             raise SystemExit(f"workload {args.workload} is a single-GPU line (run without --gpus / torchrun)")
         return run_aux(args, ih.Device(0))
-    if args.layout == "trits" and args.workload != "search":
-        raise SystemExit("--layout trits is the search-only template layout (--workload search)")
     if args.single_process and args.workload not in ("search", "batch"):
         raise SystemExit("--single-process runs the group search (--workload search / batch)")
-    layout = {"tiles": ih.LAYOUT_TILES, "lanes": ih.LAYOUT_LANES, "trits": ih.LAYOUT_TRITS}[args.layout]
+    layout = {"tiles": ih.LAYOUT_TILES, "lanes": ih.LAYOUT_LANES}[args.layout]
     kind = {"search": ih.KIND_TEMPLATES, "batch": ih.KIND_TEMPLATES, "masks": ih.KIND_MASKS,
             "shares": ih.KIND_SHARES}[args.workload]
     nq = args.queries if args.workload == "batch" else 1
@@ -995,7 +992,7 @@ def main():
         unprofiled_ms = ranks.max_over_ranks(time.perf_counter() - t1) / args.steps * 1e3
 
     kname = {"search": "template_search", "batch": "template_batch", "masks": "masks", "shares": "shares"}[args.workload]
-    rec_bytes = {"search": BYTES_PER_TEMPLATE if args.layout != "trits" else TRITS_BYTES_PER_TEMPLATE,
+    rec_bytes = {"search": BYTES_PER_TEMPLATE,
                  "batch": BYTES_PER_TEMPLATE, "masks": 1600, "shares": 25600}[args.workload]
     if args.workload in ("search", "batch"):
         results = [m] if args.workload == "search" else m
@@ -1100,7 +1097,6 @@ def main():
                          ("masks", "lanes"): "masks_kernel (VALU popcount)",
                          ("shares", "tiles"): "shares_mfma_kernel (i8 MFMA)",
                          ("shares", "lanes"): "shares_kernel (VALU v_pk_mad_u16)",
-                         ("search", "trits"): "trits_mfma_kernel<TR_SEARCH> (fp4 MFMA, 3-state bytes decoded via LDS table)",
                          ("batch", "tiles"): "batch_lds_kernel<8,2,2,2> (fp4 MFMA GEMM: 2-query groups x 16-tile N-groups, 2 x 2 per wave, LDS query-fragment ring)"}[(args.workload, args.layout)],
                 "avg_ms": avg_ms, "launches": launches, "per_device_avg_ms": per_dev_ms,
                 "reduce_avg_ms": rms / max(1, launches),

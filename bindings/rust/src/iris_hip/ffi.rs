@@ -36,8 +36,6 @@ pub const IRIS_KIND_TEMPLATES: c_int = 3;
 pub const IRIS_LAYOUT_DEFAULT: c_int = 0;
 pub const IRIS_LAYOUT_LANES: c_int = 1;
 pub const IRIS_LAYOUT_TILES: c_int = 2;
-/// Search-only template layout: 2560 B per template (pattern & mask read back).
-pub const IRIS_LAYOUT_TRITS: c_int = 3;
 
 /// Bytes of a device group's RCCL id (`iris_group_unique_id`).
 pub const IRIS_GROUP_ID_BYTES: usize = 128;

@@ -159,8 +159,7 @@ impl Database {
     }
 
     /// As `new` with an explicit device layout (`ffi::IRIS_LAYOUT_*`): e.g.
-    /// `IRIS_LAYOUT_TRITS` for a search-only template database of 2560 B per template
-    /// (read-back returns `pattern & mask`).
+    /// `IRIS_LAYOUT_LANES` for the VALU popcount kernels.
     pub fn with_layout<T: Record>(device: &Device, capacity: u64, layout: c_int) -> Result<Self> {
         let mut raw = ptr::null_mut();
         check(unsafe { ffi::iris_db_create_ex(device.raw(), T::KIND, capacity, layout, &mut raw) })?;

@@ -64,13 +64,7 @@ extern "C" {
 #define IRIS_LAYOUT_DEFAULT 0 /* TILES                                          */
 #define IRIS_LAYOUT_LANES 1   /* record-per-lane blocks of 64 (VALU kernels)   */
 #define IRIS_LAYOUT_TILES 2   /* 32-record MFMA tiles (fp4 / i8 kernels)        */
-/* Search-only template layout: each bit position as one of the three states
- * encode() distinguishes (masked out, +1, -1), five per byte: 2560 B per
- * template instead of 3200.  Search, counts and distances are identical to
- * TILES; the pattern bits under a zero mask are not stored, so iris_db_read
- * returns pattern & mask (which is all src/template.rs:49-64 and encode()
- * read).  IRIS_KIND_TEMPLATES only; batched engines of up to 3 queries. */
-#define IRIS_LAYOUT_TRITS 3
+/* (3 was the search-only TRITS template layout of rounds 2-3; removed, refused as unknown) */
 
 typedef struct iris_template {
     uint64_t pattern[IRIS_LIMBS];
@@ -162,7 +156,7 @@ int iris_db_truncate(iris_db_t *db, uint64_t len);
  * the resident copy and uploads nothing; other slices still upload.  The host
  * array must stay unchanged while attached; any write to the database
  * (append, write, generate, clear, truncate, load, prepare) or its
- * destruction detaches it.  TILES / LANES databases (not TRITS). */
+ * destruction detaches it. */
 int iris_db_attach_host(iris_db_t *db, const void *host, uint64_t n, int upload);
 int iris_db_detach_host(iris_db_t *db);
 
@@ -183,8 +177,7 @@ int iris_db_detach_host(iris_db_t *db);
  * try_cast_slice does ("Share file … invalid.", src/main.rs:390-393,459-462). */
 int iris_db_load_file(iris_db_t *db, const char *path, uint64_t first, uint64_t count, uint64_t *loaded);
 /* Writes records [first, first+n) of db to `path` (created / truncated) in
- * the same raw format.  A TRITS database is refused (IRIS_E_ARG): it keeps only
- * pattern & mask, so the file would differ from what was loaded. */
+ * the same raw format. */
 int iris_db_save_file(const iris_db_t *db, const char *path, uint64_t first, uint64_t n);
 /* JSON template files: a top-level array of {"pattern": hex, "mask": hex}
  * objects, each Bits the hex of its 1600 LE bytes (serde form of Template,

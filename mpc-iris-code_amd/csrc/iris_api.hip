@@ -560,8 +560,7 @@ int iris_db_create_ex(iris_device_t *d, int kind, uint64_t capacity, int layout,
     ARG(d && out, "NULL argument");
     CHK(check_kind(kind));
     if (layout == IRIS_LAYOUT_DEFAULT) layout = IRIS_LAYOUT_TILES;
-    ARG(layout == IRIS_LAYOUT_LANES || layout == IRIS_LAYOUT_TILES || layout == IRIS_LAYOUT_TRITS, "unknown layout");
-    ARG(layout != IRIS_LAYOUT_TRITS || kind == IRIS_KIND_TEMPLATES, "the TRITS layout holds templates only");
+    ARG(layout == IRIS_LAYOUT_LANES || layout == IRIS_LAYOUT_TILES, "unknown layout");
     std::lock_guard<std::recursive_mutex> g(d->mu);
     CHK(set_device(d));
     iris_db *db = new (std::nothrow) iris_db();
@@ -702,7 +701,6 @@ int iris_db_truncate(iris_db_t *db, uint64_t len) {
 int iris_db_attach_host(iris_db_t *db, const void *host, uint64_t n, int upload) {
     IRIS_KEEP_DEVICE();
     ARG(db && (host || n == 0), "NULL argument");
-    ARG(db->k.layout != IRIS_LAYOUT_TRITS, "a TRITS database does not hold the records exactly (search-only layout)");
     iris_device *d = db->dev;
     std::lock_guard<std::recursive_mutex> g(d->mu);
     CHK(set_device(d));
@@ -779,19 +777,9 @@ int iris_distance_engine_new(iris_device_t *d, const uint16_t query[IRIS_BITS], 
 }  // extern "C"
 
 int iris_api::template_engine_locked(iris_device *d, const iris_template_t *query, iris_engine **out) {
-    // [LANES table | TILES fragments | TRITS fragments], all built by one launch
-    iris_engine *e = nullptr;
-    void *tfrag = nullptr;
-    CHK(engine_alloc(d, IRIS_KIND_TEMPLATES, (size_t)kPlaneDwords * kTemplateTabStride * 4, kTemplateFragDwords * 4,
-                     kTemplateFragDwords * 4, &e, &tfrag));
-    e->qfrag_trits = tfrag;
-    if (launch_query_template(d->stream, query, (uint32_t *)e->qtab, (uint32_t *)e->qfrag, (uint32_t *)tfrag) != 0) {
-        const hipError_t err = hipGetLastError();
-        engine_free(e);
-        return fail(IRIS_E_HIP, std::string("build query tables: ") + hipGetErrorString(err));
-    }
-    *out = e;
-    return 0;
+    // [LANES table | TILES fragments], both built by one launch
+    return engine_from_host_query(d, IRIS_KIND_TEMPLATES, query, (size_t)kPlaneDwords * kTemplateTabStride * 4,
+                                  kTemplateFragDwords * 4, out, launch_query_template);
 }
 
 extern "C" {
@@ -913,7 +901,6 @@ int iris_template_counts(iris_engine_t *e, const iris_db_t *db, uint64_t first, 
         uint16_t *na = num_out ? (uint16_t *)d->out_a.p : nullptr;
         uint16_t *da = den_out ? (uint16_t *)d->out_b.p : nullptr;
         CHK(timed(d, "template_counts", m, [&] {
-            if (db->k.layout == IRIS_LAYOUT_TRITS) return launch_trits_counts(d->stream, db->data, e->qfrag_trits, r, na, da);
             return db->k.layout == IRIS_LAYOUT_TILES
                        ? launch_template_mfma_counts(d->stream, db->data, e->qfrag, r, na, da)
                        : launch_template_counts(d->stream, db->data, e->qtab, r, na, da);
@@ -963,9 +950,7 @@ int iris_api::search_enqueue(iris_engine_t *e, const iris_db_t *db, uint64_t fir
         if (done) HIPCHK(hipEventRecord(done, d->aux));
         return 0;
     }
-    const uint32_t np = layout == IRIS_LAYOUT_TILES   ? mfma_search_partials(r)
-                        : layout == IRIS_LAYOUT_TRITS ? trits_search_partials(r)
-                                                      : search_partials(r);
+    const uint32_t np = layout == IRIS_LAYOUT_TILES ? mfma_search_partials(r) : search_partials(r);
     const size_t pbytes = (size_t)std::max<uint32_t>(np, 1) * sizeof(Partial);
     DevBuf *buf = &d->partials;
     int b = 0;
@@ -985,8 +970,6 @@ int iris_api::search_enqueue(iris_engine_t *e, const iris_db_t *db, uint64_t fir
     CHK(timed(d, "template_search", n, [&] {
         if (layout == IRIS_LAYOUT_TILES)
             return launch_template_mfma_search(d->stream, db->data, e->qfrag, r, dist_dev, part, &written);
-        if (layout == IRIS_LAYOUT_TRITS)
-            return launch_trits_search(d->stream, db->data, e->qfrag_trits, r, dist_dev, part, &written);
         return launch_template_search(d->stream, db->data, e->qtab, r, dist_dev, part, &written);
     }));
     if (!side)  // the reduce writes the winner straight into pinned host memory: no copy before the wait

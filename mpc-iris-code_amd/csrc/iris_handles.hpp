@@ -148,7 +148,6 @@ struct iris_engine {
     size_t qbuf_bytes = 0;
     void *qtab = nullptr;     // SGPR rotated-query table (LANES kernels)
     void *qfrag = nullptr;    // MFMA query fragments (TILES kernels)
-    void *qfrag_trits = nullptr;  // template engines: the TRITS kernel's query fragments
     uint32_t nq = 0;          // > 0: batched template engine (qfrag = nq padded query tiles)
     std::vector<iris_engine *> sub;  // streaming batched engine: one single-query engine per query
     Readahead ra;             // masks / distance engines: host-slice calls on attached databases

@@ -25,7 +25,7 @@
 #if defined(IRIS_SHIPPED_BUILD)
 #if (defined(IRIS_MFMA_DIAG) && IRIS_MFMA_DIAG) || (defined(IRIS_BATCH_DIAG) && IRIS_BATCH_DIAG) || \
     (defined(IRIS_BATCH2_DIAG) && IRIS_BATCH2_DIAG) || (defined(IRIS_STORE_DIAG) && IRIS_STORE_DIAG) || \
-    (defined(IRIS_TRITS_DIAG) && IRIS_TRITS_DIAG) || (defined(IRIS_PREP_DIAG) && IRIS_PREP_DIAG)
+    (defined(IRIS_PREP_DIAG) && IRIS_PREP_DIAG)
 #error "diagnostic knob in the shipped libiris_hip.so"
 #endif
 #endif
@@ -68,7 +68,6 @@ inline KindInfo kind_info(int kind, int layout = IRIS_LAYOUT_LANES) {
     switch (kind) {
     case IRIS_KIND_TEMPLATES:
         if (layout == IRIS_LAYOUT_TILES) return {kind, layout, 32, kPlaneGroups, 2, 2 * kPlaneDwords, {kPlaneDwords, 0}, 3200};
-        if (layout == IRIS_LAYOUT_TRITS) return {kind, layout, 32, 80, 2, 2 * kPlaneDwords, {kPlaneDwords, 0}, 3200};
         return {kind, IRIS_LAYOUT_LANES, 64, 2 * kPlaneGroups, 2, 2 * kPlaneDwords, {kPlaneDwords, 0}, 3200};
     case IRIS_KIND_MASKS:
         if (layout == IRIS_LAYOUT_TILES) return {kind, layout, 32, kPlaneGroups / 2, 1, kPlaneDwords, {0, 0}, 1600};
@@ -80,67 +79,7 @@ inline KindInfo kind_info(int kind, int layout = IRIS_LAYOUT_LANES) {
     }
 }
 
-//  TRITS (TEMPLATES only, search-only; iris_trits.hip): tiles of 32 records,
-//    2560 B per record.  Position x of a template is one of three states
-//    (0: mask 0, 1: mask 1 pattern 0, 2: mask 1 pattern 1), five per byte,
-//    digit i of byte v weighing 3^i.  For 5-chunk group G (positions
-//    [320G, 320G+320)) lane L = t + 32h owns the 160 positions
-//    [320G + 160h, +160) = plane dwords 10G + 5h .. +4 (window position x =
-//    bit x & 31 of plane dword 10G + 5h + (x >> 5)).  Half-stage s = 0, 1 of the
-//    group is bytes 16s .. 16s+15: uint4 [(2G + s) * 64 + L] of the tile; digit k
-//    of its byte jj is window position trit_pos(s, jj, k) (the decode's byte roles,
-//    iris_trits.hip).
-constexpr int kTritGroups = 40;                      // 5-chunk groups per template
-constexpr int kTritTileUint4 = kTritGroups * 2 * 64; // 5120 uint4 = 81920 B per tile
-constexpr size_t kTritRecBytes = 2560;
-
-inline size_t block_bytes(const KindInfo &k) {
-    return (size_t)k.block * (k.layout == IRIS_LAYOUT_TRITS ? kTritRecBytes : k.rec_bytes);
-}
-
-// 5 mask / pattern bits (bit i = digit i) -> the TRITS byte
-IRIS_HD inline uint32_t trit_byte(uint32_t m5, uint32_t p5) {
-    uint32_t v = 0;
-    for (int i = 4; i >= 0; --i) v = 3 * v + (((m5 >> i) & 1u) ? 1u + ((p5 >> i) & 1u) : 0u);
-    return v;
-}
-// Window position (0..159) of digit k of byte jj of half-stage s.  Every 8 bytes
-// cover 40 positions, five decoded dwords of 8: bytes 0..3 (W_j) positions
-// 8j .. 8j+4, bytes 4..7 (S_j) positions 8j+5 .. 8j+7 (digits 0..2) and 32+2j,
-// 33+2j (digits 3, 4).
-IRIS_HD inline int trit_pos(int s, int jj, int k) {
-    const int base = 80 * s + 40 * (jj >> 3), b = jj & 7;
-    if (b < 4) return base + 8 * b + k;
-    const int j = b - 4;
-    return k < 3 ? base + 8 * j + 5 + k : base + 32 + 2 * j + (k - 3);
-}
-// its inverse: window position x -> (half-stage, byte, digit)
-IRIS_HD inline void trit_slot(int x, int &s, int &jj, int &k) {
-    s = x / 80;
-    const int r = x % 80, q = r / 40, n = r % 40;
-    int slot;
-    if (n < 32) {
-        const int j = n >> 3, o = n & 7;
-        slot = o < 5 ? j : 4 + j;
-        k = o < 5 ? o : o - 5;
-    } else {
-        slot = 4 + ((n - 32) >> 1);
-        k = 3 + ((n - 32) & 1);
-    }
-    jj = 8 * q + slot;
-}
-// TRITS byte -> the fp4 e2m1 encode() values of its 5 positions, nibble i =
-// 0 (masked out), 0x2 (+1.0: pattern 0) or 0xA (-1.0: pattern 1).  Bytes
-// >= 243 never occur.
-IRIS_HD inline uint32_t trit_decode(uint32_t v) {
-    uint32_t x = 0;
-    for (int i = 0; i < 5; ++i) {
-        const uint32_t d = v % 3;
-        v /= 3;
-        x |= (d == 0 ? 0u : d == 1 ? 0x2u : 0xAu) << (4 * i);
-    }
-    return x;
-}
+inline size_t block_bytes(const KindInfo &k) { return (size_t)k.block * k.rec_bytes; }
 
 // TILES interleave of 16 mask bits and 16 pattern bits into one dword:
 //   nibble p: bit0 = em[2p+1], bit1 = em[2p], bit2 = ep[2p+1], bit3 = ep[2p]
@@ -199,9 +138,6 @@ constexpr size_t kMaskFragUint4 = (size_t)(kMaskChunks / 4) * 64;
 constexpr size_t kShareFragUint4 = (size_t)kShareChunks * 64 * 2;  // + 32 int2 row constants after it
 IRIS_HD inline int mask_frag_bit(int j) { return 4 * (j & 7) + (j >> 3); }
 constexpr size_t kTemplateFragDwords = (size_t)(kPlaneDwords / 2) * 64 * kFragDwords;  // 200 chunks
-// TRITS query fragments (same size): for chunk C = 5G + c and lane L = k + 32h,
-// uint4 [C * 64 + L] = fp4 encode() of rotation k's plane dword 10G + 5h + c,
-// K index j <-> bit j (nibble j & 7 of dword j >> 3).
 
 // Rotated-query tables (built once per engine, on the device by iris_query.hip;
 // the host builders below are their reference):
@@ -247,8 +183,8 @@ struct LaunchRange {
 
 int launch_pack(void *stream, const KindInfo &k, const void *staging, void *db, uint64_t t_first, uint64_t n);
 // per-engine query tables built on the device from the query (iris_query.hip)
-// q, qmask: host; tfrag (may be NULL): the TRITS fragments, kTemplateFragDwords dwords
-int launch_query_template(void *stream, const void *q, uint32_t *tab, uint32_t *frag, uint32_t *tfrag);
+// q, qmask: host
+int launch_query_template(void *stream, const void *q, uint32_t *tab, uint32_t *frag);
 int launch_query_masks(void *stream, const void *qmask, uint32_t *tab, uint32_t *frag);
 int launch_query_shares(void *stream, const void *q, uint32_t *tab, uint32_t *frag);
 int launch_query_tiles(void *stream, const void *queries, uint32_t nq, uint32_t nqp, uint32_t *tiles);
@@ -298,15 +234,6 @@ int launch_pack_tiles_kind(void *stream, int kind, const void *staging, void *db
 int launch_unpack_tiles_kind(void *stream, int kind, const void *db, void *staging, uint64_t t_first, uint64_t n);
 int launch_generate_tiles_kind(void *stream, int kind, void *db, uint64_t t_first, uint64_t n, uint64_t seed,
                                uint64_t global_index0);
-// TRITS layout (iris_trits.hip); qfrag = the engine's TRITS query fragments
-int launch_pack_trits(void *stream, const void *staging, void *db, uint64_t t_first, uint64_t n);
-int launch_unpack_trits(void *stream, const void *db, void *staging, uint64_t t_first, uint64_t n);
-int launch_generate_trits(void *stream, void *db, uint64_t t_first, uint64_t n, uint64_t seed, uint64_t global_index0);
-uint32_t trits_search_partials(LaunchRange r);
-int launch_trits_search(void *stream, const void *db, const void *qfrag, LaunchRange r, double *dist_out,
-                        Partial *partials, uint32_t *n_partials);
-int launch_trits_counts(void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *num_out,
-                        uint16_t *den_out);
 int launch_masks_mfma(void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *out);
 uint32_t masks_resolve_partials(LaunchRange r);
 int launch_masks_resolve(void *stream, const void *db, const void *qfrag, LaunchRange r,

@@ -229,9 +229,6 @@ int iris_db_load_file(iris_db_t *db, const char *path, uint64_t first, uint64_t 
 int iris_db_save_file(const iris_db_t *db, const char *path, uint64_t first, uint64_t n) {
     IRIS_KEEP_DEVICE();
     ARG(db && path, "NULL argument");
-    // TRITS keeps pattern & mask only: a saved file would silently differ from what was loaded
-    if (db->k.layout == IRIS_LAYOUT_TRITS)
-        return fail(IRIS_E_ARG, "iris_db_save_file: a TRITS database is a search-only layout (pattern bits under a zero mask are not stored)");
     iris_device *d = db->dev;
     std::lock_guard<std::recursive_mutex> g(d->mu);
     CHK(set_device(d));

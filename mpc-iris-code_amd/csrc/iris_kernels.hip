@@ -448,7 +448,6 @@ static int check_launch() { return hipGetLastError() == hipSuccess ? 0 : -1; }
 int launch_pack(void *stream, const KindInfo &k, const void *staging, void *db, uint64_t t_first, uint64_t n) {
     if (n == 0) return 0;
     if (k.layout == IRIS_LAYOUT_TILES) return launch_pack_tiles_kind(stream, k.kind, staging, db, t_first, n);
-    if (k.layout == IRIS_LAYOUT_TRITS) return launch_pack_trits(stream, staging, db, t_first, n);
     hipLaunchKernelGGL(pack_kernel, dim3(grid_stride_blocks(n * k.groups)), dim3(256), 0, (hipStream_t)stream,
                        (const uint4 *)staging, (uint4 *)db, t_first, n, pack_params(k));
     return check_launch();
@@ -457,7 +456,6 @@ int launch_pack(void *stream, const KindInfo &k, const void *staging, void *db, 
 int launch_unpack(void *stream, const KindInfo &k, const void *db, void *staging, uint64_t t_first, uint64_t n) {
     if (n == 0) return 0;
     if (k.layout == IRIS_LAYOUT_TILES) return launch_unpack_tiles_kind(stream, k.kind, db, staging, t_first, n);
-    if (k.layout == IRIS_LAYOUT_TRITS) return launch_unpack_trits(stream, db, staging, t_first, n);
     hipLaunchKernelGGL(unpack_kernel, dim3(grid_stride_blocks(n * k.groups)), dim3(256), 0, (hipStream_t)stream,
                        (const uint4 *)db, (uint4 *)staging, t_first, n, pack_params(k));
     return check_launch();
@@ -468,7 +466,6 @@ int launch_generate(void *stream, const KindInfo &k, void *db, uint64_t t_first,
     if (n == 0) return 0;
     if (k.layout == IRIS_LAYOUT_TILES)
         return launch_generate_tiles_kind(stream, k.kind, db, t_first, n, seed, global_index0);
-    if (k.layout == IRIS_LAYOUT_TRITS) return launch_generate_trits(stream, db, t_first, n, seed, global_index0);
     const uint64_t key = gen_key(seed, k.kind == IRIS_KIND_SHARES ? 1 : 0);
     hipLaunchKernelGGL(generate_kernel, dim3(grid_stride_blocks(n * k.groups)), dim3(256), 0, (hipStream_t)stream,
                        (uint4 *)db, t_first, n, k.kind, k.groups, key, global_index0);

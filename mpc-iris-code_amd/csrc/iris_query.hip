@@ -50,7 +50,7 @@ struct MaskArg {
 };
 
 __global__ void __launch_bounds__(256) query_template_kernel(const TemplateArg q, uint32_t *__restrict__ tab,
-                                                             uint4 *__restrict__ frag, uint4 *__restrict__ tfrag) {
+                                                             uint4 *__restrict__ frag) {
     __shared__ uint32_t sp[kPlaneDwords], sm[kPlaneDwords];
     for (int i = threadIdx.x; i < kPlaneDwords; i += blockDim.x) {
         sp[i] = q.pattern[i];
@@ -75,16 +75,6 @@ __global__ void __launch_bounds__(256) query_template_kernel(const TemplateArg q
     }
     const int c = w >> 1, h = w & 1;
     frag[c * 64 + k + 32 * h] = make_uint4(f[0], f[1], f[2], f[3]);
-    if (tfrag) {  // TRITS: plane dword w = 10G + 5h' + c' is chunk 5G + c' of lane k + 32h', bit j = K index j
-        uint32_t t[4] = {0, 0, 0, 0};
-#pragma unroll
-        for (int j = 0; j < 32; ++j) {
-            const uint32_t code = ((mw >> j) & 1u) ? (((pw >> j) & 1u) ? 0xAu : 0x2u) : 0u;
-            t[j >> 3] |= code << (4 * (j & 7));
-        }
-        const int G = w / 10, r = w - 10 * G;
-        tfrag[(5 * G + r % 5) * 64 + k + 32 * (r / 5)] = make_uint4(t[0], t[1], t[2], t[3]);
-    }
 }
 
 // MASKS: table [w*32 + k] = mask_k dword w; compact fragments dword
@@ -203,12 +193,12 @@ __global__ void __launch_bounds__(256) query_tiles_kernel(const iris_template_t 
 }
 
 // q / qmask: HOST pointers (copied into the kernel arguments at launch)
-int launch_query_template(void *stream, const void *q, uint32_t *tab, uint32_t *frag, uint32_t *tfrag) {
+int launch_query_template(void *stream, const void *q, uint32_t *tab, uint32_t *frag) {
     TemplateArg a;
     memcpy(a.pattern, ((const iris_template_t *)q)->pattern, sizeof(a.pattern));
     memcpy(a.mask, ((const iris_template_t *)q)->mask, sizeof(a.mask));
     hipLaunchKernelGGL(query_template_kernel, dim3(kPlaneDwords * 32 / 256), dim3(256), 0, (hipStream_t)stream, a,
-                       tab, (uint4 *)frag, (uint4 *)tfrag);
+                       tab, (uint4 *)frag);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

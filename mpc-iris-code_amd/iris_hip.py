@@ -32,7 +32,7 @@ LIB_PATH = pathlib.Path(os.environ.get("IRIS_HIP_LIB", HERE / "libiris_hip.so"))
 
 COLS, ROWS, BITS, LIMBS, ROTATIONS = 200, 64, 12800, 200, 31
 KIND_MASKS, KIND_SHARES, KIND_TEMPLATES = 1, 2, 3
-LAYOUT_DEFAULT, LAYOUT_LANES, LAYOUT_TILES, LAYOUT_TRITS = 0, 1, 2, 3
+LAYOUT_DEFAULT, LAYOUT_LANES, LAYOUT_TILES = 0, 1, 2
 _REC_DTYPE = {KIND_MASKS: (np.uint64, LIMBS), KIND_SHARES: (np.uint16, BITS), KIND_TEMPLATES: (np.uint64, 2 * LIMBS)}
 
 
@@ -628,7 +628,7 @@ class Database:
         return got.value
 
     def save_file(self, path, first=0, n=None):
-        """Writes records [first, first+n) to a raw record file (refused for TRITS databases)."""
+        """Writes records [first, first+n) to a raw record file."""
         if n is None:
             n = len(self) - int(first)
         _check(load_library().iris_db_save_file(self.handle, os.fsencode(path), int(first), int(n)))
@@ -1144,6 +1144,6 @@ __all__ = [
     "DistanceEngine", "TemplateEngine", "TemplateBatchEngine", "Device", "Database", "Match", "merge_matches", "dot_bool", "dot_u16",
     "Group", "GroupDatabase", "GroupPendingSearch",
     "dot_bool_batch", "dot_u16_batch", "IrisError", "load_library", "KIND_MASKS", "KIND_SHARES", "KIND_TEMPLATES",
-    "LAYOUT_DEFAULT", "LAYOUT_LANES", "LAYOUT_TILES", "LAYOUT_TRITS",
+    "LAYOUT_DEFAULT", "LAYOUT_LANES", "LAYOUT_TILES",
     "ROTATIONS", "BITS", "LIMBS", "COLS", "ROWS",
 ]

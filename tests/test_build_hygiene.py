@@ -17,7 +17,7 @@ def _make(*args):
 
 
 def test_shipped_target_refuses_diag_knobs(tmp_path):
-    for knob in ("-DIRIS_MFMA_DIAG=1", "-DIRIS_STORE_DIAG", "-DIRIS_BATCH2_DIAG=5", "-DIRIS_TRITS_DIAG=2"):
+    for knob in ("-DIRIS_MFMA_DIAG=1", "-DIRIS_STORE_DIAG", "-DIRIS_BATCH2_DIAG=5", "-DIRIS_PREP_DIAG=2"):
         r = _make("-n", f"BUILD={tmp_path}/b", f"HIPFLAGS=-O3 --offload-arch=gfx950 {knob}")
         assert r.returncode != 0 and "refusing to build the shipped libiris_hip.so" in r.stderr, (knob, r.stderr)
 

@@ -102,12 +102,8 @@ def test_attach_kind_and_alignment_rules(device):
             assert pack_launches(device) > 0
         finally:
             device.set_profiling(False)
-    with ih.Database(device, ih.KIND_TEMPLATES, 10, ih.LAYOUT_TRITS) as tdb:
-        with pytest.raises(ih.IrisError):
-            tdb.attach_host(oc.gen_templates(1, 0, 10))  # search-only layout: not exact records
-        tdb.generate(10, 1)
-        with pytest.raises(ih.IrisError):
-            tdb.save_file("/tmp/never_written.templates")
+    with pytest.raises(ih.IrisError):  # layout 3 (the removed TRITS layout) is unknown
+        ih.Database(device, ih.KIND_TEMPLATES, 10, 3)
 
 
 def launches(dev, name):

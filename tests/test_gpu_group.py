@@ -121,7 +121,7 @@ def test_group_async_out_of_order(group):
             assert same(got[k], best, idx) and idx == 1000 + 3700 * k
 
 
-@pytest.mark.parametrize("layout", [ih.LAYOUT_LANES, ih.LAYOUT_TRITS])
+@pytest.mark.parametrize("layout", [ih.LAYOUT_LANES])
 def test_group_other_layouts(group, layout):
     n = 3001
     ref = oc.gen_templates(SEED, 0, n)

@@ -44,13 +44,11 @@ def per_launch(dirname, name, kernel):
 
 def main(round_tag="r02"):
     for w, (kernel, n, alg) in KERNELS.items():
-        for suffix, lay in (("", "tiles"), ("_lanes", "lanes"), ("_trits", "trits")):
+        for suffix, lay in (("", "tiles"), ("_lanes", "lanes")):
             fdir, wdir = f"{w}_FETCH_SIZE{suffix}", f"{w}_WRITE_SIZE{suffix}"
             if not (PMC / fdir).exists():
                 continue
-            k = {"tiles": kernel, "lanes": "template_kernel<1>", "trits": "trits_mfma_kernel<1"}[lay]
-            if lay == "trits":
-                alg = 2560
+            k = {"tiles": kernel, "lanes": "template_kernel<1>"}[lay]
             fetch = per_launch(fdir, "FETCH_SIZE", k)
             write = per_launch(wdir, "WRITE_SIZE", k)
             if fetch is None or write is None:

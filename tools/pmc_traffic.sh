@@ -24,7 +24,3 @@ if [ -z "$NO_LANES" ]; then
     pass search FETCH_SIZE _lanes --steps 3 --warmup 1 --layout lanes || exit 1
     pass search WRITE_SIZE _lanes --steps 3 --warmup 1 --layout lanes || exit 1
 fi
-if [ -n "$TRITS" ]; then
-    pass search FETCH_SIZE _trits --steps 3 --warmup 1 --layout trits || exit 1
-    pass search WRITE_SIZE _trits --steps 3 --warmup 1 --layout trits || exit 1
-fi
