@@ -97,6 +97,7 @@ extern "C" {
     // errors
     pub fn iris_last_error() -> *const c_char;
     pub fn iris_version() -> *const c_char;
+    pub fn iris_config(dev: *const IrisDevice, buf: *mut c_char, len: usize, needed: *mut usize) -> c_int;
 
     // devices
     pub fn iris_device_count(count: *mut c_int) -> c_int;
@@ -323,6 +324,7 @@ extern "C" {
         out: *mut *mut IrisGroup,
     ) -> c_int;
     pub fn iris_group_destroy(group: *mut IrisGroup) -> c_int;
+    pub fn iris_group_set_timeout(group: *mut IrisGroup, ms: u32) -> c_int;
     pub fn iris_group_info(
         group: *const IrisGroup,
         local_devices: *mut u32,

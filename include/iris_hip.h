@@ -90,6 +90,16 @@ typedef struct iris_pending iris_pending_t;
 /* ---------------------------------------------------------------- errors */
 const char *iris_last_error(void);
 const char *iris_version(void);
+/* Runtime configuration, read from the environment once when a device opens:
+ * "key=value ..." into buf (NUL-terminated, truncated to len); *needed (may be
+ * NULL) receives the full length without the NUL.  dev == NULL: what a device
+ * opened now would use.  Production knobs: IRIS_READAHEAD, IRIS_GROUP_TIMEOUT_MS,
+ * IRIS_COPY_HELPERS (process-wide).  Test-only hooks (IRIS_TILES_PER_WAVE,
+ * IRIS_FUSED_REDUCE, IRIS_BATCH_KERNEL, IRIS_BATCH_XQG, IRIS_SCHEDULE,
+ * IRIS_LOAD_PREAD, IRIS_GROUP_DELAY_US, IRIS_GROUP_STALL, IRIS_GROUP_UNORDERED)
+ * take effect only with IRIS_TEST_HOOKS=1; otherwise they are ignored and listed
+ * as "ignored=...". */
+int iris_config(const iris_device_t *dev, char *buf, size_t len, size_t *needed);
 
 /* --------------------------------------------------------------- devices */
 int iris_device_count(int *count);
@@ -351,7 +361,16 @@ int iris_match_merge(const iris_match_t *records, uint64_t count, iris_match_t *
  *    rank (any side channel); each rank then calls iris_group_create_rank with
  *    the same id (ncclCommInitRank).  Every rank makes the same group calls
  *    (SPMD); each holds and fills only its own shards.
- * Group calls are blocking and serialised per group, like the device calls. */
+ * Group calls are blocking and serialised per group, like the device calls.
+ *
+ * Failure: waiting for an exchange is bounded.  The clock starts when every
+ * local device has reached the all-gather (only the peers can hold it up) and
+ * RCCL's asynchronous error is polled meanwhile; on expiry or error the
+ * group's communicators are aborted (ncclCommAbort), the call returns
+ * IRIS_E_HIP, and every later call on the group or its databases fails the
+ * same way (the destroys excepted).  A rank whose own enqueue fails aborts too,
+ * so its peers see an error rather than a hang.  Bound: IRIS_GROUP_TIMEOUT_MS,
+ * iris_group_set_timeout, else max(30 s, 10 x the call's local work). */
 #define IRIS_GROUP_ID_BYTES 128
 typedef struct iris_group iris_group_t;
 typedef struct iris_group_db iris_group_db_t;
@@ -362,6 +381,8 @@ int iris_group_unique_id(uint8_t id[IRIS_GROUP_ID_BYTES]);
 int iris_group_create_rank(int ordinal, uint32_t nranks, uint32_t rank, const uint8_t id[IRIS_GROUP_ID_BYTES],
                            iris_group_t **out);
 int iris_group_destroy(iris_group_t *group);
+/* ms > 0: the exchange wait bound of this group's later calls; 0: automatic. */
+int iris_group_set_timeout(iris_group_t *group, uint32_t ms);
 /* local_devices: devices this process drives; ranks: RCCL ranks in the group
  * (all processes); first_rank: the rank of local device 0. */
 int iris_group_info(const iris_group_t *group, uint32_t *local_devices, uint32_t *ranks, uint32_t *first_rank);

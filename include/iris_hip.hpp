@@ -364,6 +364,8 @@ public:
     Group(const Group &) = delete;
     Group &operator=(const Group &) = delete;
     iris_group_t *handle() const { return h_; }
+    // bound of the exchange waits of later calls (0: automatic); see include/iris_hip.h
+    void set_timeout(uint32_t ms) { check(iris_group_set_timeout(h_, ms)); }
 
 private:
     iris_group_t *h_ = nullptr;

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <math.h>
+#include <stdio.h>
 #include <string.h>
 
 #include <algorithm>
@@ -84,10 +85,10 @@ int enqueue_u16_engine(iris_engine *e, const iris_db *db, uint64_t first, uint64
     const bool tiles = db->k.layout == IRIS_LAYOUT_TILES;
     if (e->kind == IRIS_KIND_MASKS)
         return timed(d, "masks", n, [&] {
-            return tiles ? launch_masks_mfma(stream, db->data, e->qfrag, r, o) : launch_masks(stream, db->data, e->qtab, r, o);
+            return tiles ? launch_masks_mfma(d->hooks, stream, db->data, e->qfrag, r, o) : launch_masks(stream, db->data, e->qtab, r, o);
         }, stream);
     return timed(d, "shares", n, [&] {
-        return tiles ? launch_shares_mfma(stream, db->data, e->qfrag, r, o) : launch_shares(stream, db->data, e->qtab, r, o);
+        return tiles ? launch_shares_mfma(d->hooks, stream, db->data, e->qfrag, r, o) : launch_shares(stream, db->data, e->qtab, r, o);
     }, stream);
 }
 
@@ -111,11 +112,9 @@ constexpr uint64_t kReadaheadMax = 1ull << 20;
 
 // TILES databases only: their kernels store the rows as 16-B runs (store_tile_rows), which the
 // host link takes well; the LANES kernels' 2-byte stores would each be a host-link write.
-// IRIS_READAHEAD=0 turns it off (tests run both forms).
+// IRIS_READAHEAD=0 turns it off (Hooks::readahead; tests run both forms).
 bool readahead_ok(const iris_db *db, uint64_t n) {
-    if (n > kReadaheadMax || db->k.layout != IRIS_LAYOUT_TILES) return false;
-    const char *f = getenv("IRIS_READAHEAD");
-    return !(f && f[0] == '0');
+    return db->dev->hooks.readahead && n <= kReadaheadMax && db->k.layout == IRIS_LAYOUT_TILES;
 }
 
 // Drops the engine's read-ahead: its kernels (side stream) have finished when this returns, so
@@ -220,11 +219,16 @@ int readahead_u16_call(iris_engine *e, const iris_db *a, uint64_t first, uint64_
     Readahead &ra = e->ra;
     iris_device *d = e->dev;
     const bool hit = ra.pending && ra.db == a && ra.version == a->version && ra.first == first && ra.n == n;
+    // speculate only inside a walk: this call read ahead for, or continuing where the last call ended
+    const bool walk = hit || (ra.last_db == a && ra.last_version == a->version && ra.last_end == first);
     if (!hit) CHK(ra_launch(e, a, first, n, ra.pending ? ra.cur ^ 1 : 0));
     const int b = ra.cur;
     ra.pending = false;
+    ra.last_db = a;
+    ra.last_version = a->version;
+    ra.last_end = first + n;
     const uint64_t next = first + n;
-    if (next < end) CHK(ra_launch(e, a, next, std::min<uint64_t>(n, end - next), b ^ 1));
+    if (walk && next < end) CHK(ra_launch(e, a, next, std::min<uint64_t>(n, end - next), b ^ 1));
     HIPCHK(hipEventSynchronize(ra.computed[b]));
     parallel_copy(out, ra.rows[b], (size_t)n * kRot * 2);
     if (d->profiling) fold_done(d);
@@ -412,6 +416,15 @@ const char *iris_version(void) {
     return v.c_str();
 }
 
+int iris_config(const iris_device_t *d, char *buf, size_t len, size_t *needed) {
+    ARG(buf || len == 0, "NULL buffer");
+    Hooks now;
+    if (!d) read_hooks(&now);
+    const size_t n = format_hooks(d ? d->hooks : now, buf, len);
+    if (needed) *needed = n;
+    return 0;
+}
+
 int iris_device_count(int *count) {
     ARG(count, "count is NULL");
     int n = 0;
@@ -434,13 +447,22 @@ int iris_device_open(int ordinal, iris_device_t **out) {
     iris_device *d = new (std::nothrow) iris_device();
     if (!d) return fail(IRIS_E_NOMEM, "out of host memory");
     d->ordinal = ordinal;
+    read_hooks(&d->hooks);  // the environment's knobs, once (iris_config reports them)
+    if (d->hooks.ignored) {  // said once per process: a test hook in a production environment does nothing
+        static std::once_flag warned;
+        std::call_once(warned, [&] {
+            char buf[512];
+            format_hooks(d->hooks, buf, sizeof(buf));
+            fprintf(stderr, "iris-hip: test-only hooks ignored (IRIS_TEST_HOOKS is not 1): %s\n", strstr(buf, "ignored="));
+        });
+    }
     hipError_t e = hipSetDevice(ordinal);
-    // IRIS_SCHEDULE = spin | yield | blocking: how host waits on this device behave (diagnostic;
-    // takes effect only before the process's first context on the device)
-    if (const char *sch = getenv("IRIS_SCHEDULE")) {
-        const unsigned f = !strcmp(sch, "spin") ? hipDeviceScheduleSpin
-                           : !strcmp(sch, "yield") ? hipDeviceScheduleYield
-                           : !strcmp(sch, "blocking") ? hipDeviceScheduleBlockingSync : hipDeviceScheduleAuto;
+    // test hook IRIS_SCHEDULE = spin | yield | blocking: how host waits on this device behave
+    // (takes effect only before the process's first context on the device)
+    if (d->hooks.schedule) {
+        const unsigned f = d->hooks.schedule == 1   ? hipDeviceScheduleSpin
+                           : d->hooks.schedule == 2 ? hipDeviceScheduleYield
+                                                    : hipDeviceScheduleBlockingSync;
         (void)hipSetDeviceFlags(f);
         (void)hipGetLastError();
     }
@@ -902,7 +924,7 @@ int iris_template_counts(iris_engine_t *e, const iris_db_t *db, uint64_t first, 
         uint16_t *da = den_out ? (uint16_t *)d->out_b.p : nullptr;
         CHK(timed(d, "template_counts", m, [&] {
             return db->k.layout == IRIS_LAYOUT_TILES
-                       ? launch_template_mfma_counts(d->stream, db->data, e->qfrag, r, na, da)
+                       ? launch_template_mfma_counts(d->hooks, d->stream, db->data, e->qfrag, r, na, da)
                        : launch_template_counts(d->stream, db->data, e->qtab, r, na, da);
         }));
         if (num_out)
@@ -928,14 +950,14 @@ int iris_api::search_enqueue(iris_engine_t *e, const iris_db_t *db, uint64_t fir
     if (n == 0) return 0;
     LaunchRange r{first, n};
     const int layout = db->k.layout;
-    if (layout == IRIS_LAYOUT_TILES && fused_search_ok(r)) {
+    if (layout == IRIS_LAYOUT_TILES && fused_search_ok(d->hooks, r)) {
         // small range: the kernel's last workgroup reduces and writes dst itself (no reduce launch)
         CHK(ensure_ticket(d));
-        CHK(ensure(d->partials, (size_t)mfma_search_partials(r) * sizeof(Partial)));
+        CHK(ensure(d->partials, (size_t)mfma_search_partials(d->hooks, r) * sizeof(Partial)));
         const FusedFinish fin{(uint32_t *)d->ticket.p, dst, idx_base, host_done, seq};
         uint32_t written = 0;
         CHK(timed(d, "template_search", n, [&] {
-            return launch_template_mfma_search(d->stream, db->data, e->qfrag, r, dist_dev, (Partial *)d->partials.p,
+            return launch_template_mfma_search(d->hooks, d->stream, db->data, e->qfrag, r, dist_dev, (Partial *)d->partials.p,
                                                &written, &fin);
         }));
         if (flagged) *flagged = host_done != nullptr;
@@ -950,7 +972,7 @@ int iris_api::search_enqueue(iris_engine_t *e, const iris_db_t *db, uint64_t fir
         if (done) HIPCHK(hipEventRecord(done, d->aux));
         return 0;
     }
-    const uint32_t np = layout == IRIS_LAYOUT_TILES ? mfma_search_partials(r) : search_partials(r);
+    const uint32_t np = layout == IRIS_LAYOUT_TILES ? mfma_search_partials(d->hooks, r) : search_partials(r);
     const size_t pbytes = (size_t)std::max<uint32_t>(np, 1) * sizeof(Partial);
     DevBuf *buf = &d->partials;
     int b = 0;
@@ -969,7 +991,7 @@ int iris_api::search_enqueue(iris_engine_t *e, const iris_db_t *db, uint64_t fir
     uint32_t written = 0;
     CHK(timed(d, "template_search", n, [&] {
         if (layout == IRIS_LAYOUT_TILES)
-            return launch_template_mfma_search(d->stream, db->data, e->qfrag, r, dist_dev, part, &written);
+            return launch_template_mfma_search(d->hooks, d->stream, db->data, e->qfrag, r, dist_dev, part, &written);
         return launch_template_search(d->stream, db->data, e->qtab, r, dist_dev, part, &written);
     }));
     if (!side)  // the reduce writes the winner straight into pinned host memory: no copy before the wait
@@ -1248,14 +1270,14 @@ int iris_template_batch_search(iris_engine_t *e, const iris_db_t *db, uint64_t f
         return 0;
     }
     LaunchRange r{first, n};
-    const BatchGeometry geo = batch_geometry(r, e->nq);
+    const BatchGeometry geo = batch_geometry(d->hooks, r, e->nq);
     const uint32_t nqp = geo.nqg * geo.qper;
     std::vector<Partial> res(nqp);
     if (n > 0) {
         CHK(ensure(d->partials, (size_t)nqp * geo.G * sizeof(Partial)));
         CHK(ensure_host_result(d, (size_t)nqp * sizeof(Partial)));
         CHK(timed(d, "template_batch", n * e->nq, [&] {
-            return launch_batch(d->stream, db->data, e->qfrag, r, geo, (Partial *)d->partials.p,
+            return launch_batch(d->hooks, d->stream, db->data, e->qfrag, r, geo, (Partial *)d->partials.p,
                                 (Partial *)d->host_result);
         }));
     }
@@ -1338,10 +1360,10 @@ int iris_resolver_search_masks(iris_engine_t *e, const iris_db_t *db, uint64_t f
     LaunchRange r{first, n};
     Partial res{};
     if (db->k.layout == IRIS_LAYOUT_TILES) {
-        const uint32_t np = n ? masks_resolve_partials(r) : 0;
+        const uint32_t np = n ? masks_resolve_partials(d->hooks, r) : 0;
         CHK(ensure(d->partials, (size_t)std::max<uint32_t>(np, 1) * sizeof(Partial)));
         CHK(timed(d, "masks_resolve", n, [&] {
-            return launch_masks_resolve(d->stream, db->data, e->qfrag, r, shares_device, parts, dist_out_device,
+            return launch_masks_resolve(d->hooks, d->stream, db->data, e->qfrag, r, shares_device, parts, dist_out_device,
                                         (Partial *)d->partials.p);
         }));
         CHK(resolver_finish(d, np, &res));

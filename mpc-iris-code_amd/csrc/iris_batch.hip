@@ -679,40 +679,36 @@ __global__ void __launch_bounds__(64 * NW, 1)
     }
 }
 
-// IRIS_BATCH_KERNEL (read per launch, so tests run every form): 4 = batch_lds_kernel with
+// IRIS_BATCH_KERNEL (a test hook, Hooks::batch_kernel, so tests run every form): 4 = batch_lds_kernel with
 // 2-query groups x 16-tile N-groups, 2 x 2 per wave (default: half the LDS fragment reads and
 // half the query-tile bytes per template of 2; 3.5 % faster, profiles/r03_batch_variants.txt);
 // 2 = batch_lds_kernel 4-query groups x 8 tiles, 4 x 1 per wave (round 2); 3 = 4-query groups,
 // 2 x 2 per wave; 1 = batch_kernel (LDS-DMA staged, round 1)
-static int batch_kernel_choice() {
-    const char *e = getenv("IRIS_BATCH_KERNEL");
-    const int k = e ? atoi(e) : 4;
-    return k >= 1 && k <= 4 ? k : 4;
-}
+static int batch_kernel_choice(const Hooks &h) { return h.batch_kernel >= 1 && h.batch_kernel <= 4 ? h.batch_kernel : 4; }
 
 uint32_t batch_query_group() { return BQ; }
 
-BatchGeometry batch_geometry(LaunchRange r, uint32_t nq) {
+BatchGeometry batch_geometry(const Hooks &h, LaunchRange r, uint32_t nq) {
     BatchGeometry g;
     g.tile0 = r.first / 32;
     const uint64_t tile1 = (r.first + r.n + 31) / 32;
     g.ntiles = tile1 - g.tile0;
-    const int kc = batch_kernel_choice();
+    const int kc = batch_kernel_choice(h);
     g.qper = kc == 4 ? 2 : BQ;  // queries per query group
     g.nqg = (nq + g.qper - 1) / g.qper;
     const uint32_t tiles_per_group = kc == 1 ? BT : kc == 4 ? 16 : 8;
     const uint64_t ngroups = (g.ntiles + tiles_per_group - 1) / tiles_per_group;
     // batch_kernel: ~2 workgroups per CU in total; batch_lds_kernel (one 128-KB-LDS workgroup
     // per CU): one round of workgroups
-    const uint64_t want = batch_kernel_choice() >= 2 ? resident_blocks(1) : 512;
+    const uint64_t want = kc >= 2 ? resident_blocks(1) : 512;
     uint64_t G = (want + g.nqg - 1) / g.nqg;
     if (G > ngroups) G = ngroups ? ngroups : 1;
     g.G = (uint32_t)G;
     g.xqg = 0;
     // XCD-aware grid (IRIS_BATCH_XQG = query groups per XCD per round): the 32 CUs of an XCD
     // run xqg query groups x 32/xqg N-slices, so their query tiles stay in that XCD's L2
-    if (const char *e = batch_kernel_choice() >= 2 ? nullptr : getenv("IRIS_BATCH_XQG")) {
-        const uint32_t x = (uint32_t)atoi(e);
+    if (kc == 1 && h.batch_xqg) {
+        const uint32_t x = h.batch_xqg;
         if (x && 32 % x == 0 && g.nqg % (8 * x) == 0 && ngroups >= 32 / x) {
             g.xqg = x;
             g.G = 32 / x;
@@ -721,10 +717,10 @@ BatchGeometry batch_geometry(LaunchRange r, uint32_t nq) {
     return g;
 }
 
-int launch_batch(void *stream, const void *db, const void *qtiles, LaunchRange r, const BatchGeometry &g,
+int launch_batch(const Hooks &h, void *stream, const void *db, const void *qtiles, LaunchRange r, const BatchGeometry &g,
                  Partial *partials, Partial *out, uint64_t idx_base) {
     if (r.n == 0) return 0;
-    const int kc = batch_kernel_choice();
+    const int kc = batch_kernel_choice(h);
     if (kc == 2)
         hipLaunchKernelGGL((batch_lds_kernel<8, 1>), dim3(g.nqg * g.G), dim3(64 * 8), 0, (hipStream_t)stream,
                            (const uint4 *)db, (const uint4 *)qtiles, g.tile0, g.ntiles, r.first, r.first + r.n, g.nqg,

@@ -315,22 +315,22 @@ __global__ void __launch_bounds__(64 * KS)
 // than the chip holds at two workgroups per CU — then one, for 8x / 4x / 2x the waves
 // (a participant-sized chunk of 20k records is only 625 tiles).  IRIS_TILES_PER_WAVE=1|4
 // pins the small or the big variant (tests run both).
-static int tiles_per_wave(uint64_t ntiles, int big) {
-    if (const char *f = getenv("IRIS_TILES_PER_WAVE")) return atoi(f) == 1 ? 1 : big;
+static int tiles_per_wave(const Hooks &h, uint64_t ntiles, int big) {
+    if (h.tiles_per_wave) return h.tiles_per_wave == 1 ? 1 : big;
     return ntiles / big < (uint64_t)resident_blocks(2) * kWaveSlots ? 1 : big;
 }
 
-int launch_masks_mfma(void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *out) {
+int launch_masks_mfma(const Hooks &h, void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *out) {
     if (r.n == 0) return 0;
     const uint64_t ntiles = tiles_of(r, 1).ntiles;
     // the K-split form for small ranges (IRIS_TILES_PER_WAVE pins the persistent kernel for tests)
-    if (ntiles <= kMasksSplitTiles && !getenv("IRIS_TILES_PER_WAVE")) {
+    if (ntiles <= kMasksSplitTiles && !h.tiles_per_wave) {
         hipLaunchKernelGGL(masks_split_kernel<kMasksSplitKS>, dim3((uint32_t)ntiles), dim3(64 * kMasksSplitKS), 0,
                            (hipStream_t)stream, (const uint4 *)db, (const uint4 *)qfrag, tiles_of(r, 1).tile0,
                            r.first, r.first + r.n, out);
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
-    const int tpw = tiles_per_wave(ntiles, kMasksTiles);
+    const int tpw = tiles_per_wave(h, ntiles, kMasksTiles);
     const Tiles t = tiles_of(r, tpw);
     const uint64_t grid = std::min<uint64_t>(t.grid, resident_blocks(kMasksBlocksPerCu));
     auto kern = tpw == 1 ? masks_mfma_kernel<MASKS_OUT, 1> : masks_mfma_kernel<MASKS_OUT>;
@@ -340,18 +340,18 @@ int launch_masks_mfma(void *stream, const void *db, const void *qfrag, LaunchRan
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-uint32_t masks_resolve_partials(LaunchRange r) {
-    const Tiles t = tiles_of(r, tiles_per_wave(tiles_of(r, 1).ntiles, kResolveTiles));
+uint32_t masks_resolve_partials(const Hooks &h, LaunchRange r) {
+    const Tiles t = tiles_of(r, tiles_per_wave(h, tiles_of(r, 1).ntiles, kResolveTiles));
     return (uint32_t)std::min<uint64_t>(t.grid, resident_blocks(kMasksBlocksPerCu));
 }
 
-int launch_masks_resolve(void *stream, const void *db, const void *qfrag, LaunchRange r,
+int launch_masks_resolve(const Hooks &h, void *stream, const void *db, const void *qfrag, LaunchRange r,
                          const uint16_t *const *shares, uint32_t parts, double *dist_out, Partial *partials) {
     if (r.n == 0) return 0;
     if (parts == 0 || parts > 8) return -1;
-    const int tpw = tiles_per_wave(tiles_of(r, 1).ntiles, kResolveTiles);
+    const int tpw = tiles_per_wave(h, tiles_of(r, 1).ntiles, kResolveTiles);
     const Tiles t = tiles_of(r, tpw);
-    const uint64_t grid = masks_resolve_partials(r);
+    const uint64_t grid = masks_resolve_partials(h, r);
     MaskResolve rs{};
     rs.aligned = true;
     for (uint32_t p = 0; p < parts; ++p) {
@@ -592,14 +592,14 @@ __global__ void __launch_bounds__(64 * KS, 2)
 
 // K-slices for a range (1 = no split): enough one-tile waves to fill the chip, a
 // divisor of the 200 steps, at most 10.
-static bool shares_lds_split(uint64_t ntiles) {
-    return ntiles <= kSharesSplitTiles && !getenv("IRIS_TILES_PER_WAVE");
+static bool shares_lds_split(const Hooks &h, uint64_t ntiles) {
+    return ntiles <= kSharesSplitTiles && !h.tiles_per_wave;
 }
 
-int launch_shares_mfma(void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *out) {
+int launch_shares_mfma(const Hooks &h, void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *out) {
     if (r.n == 0) return 0;
     const int2 *qsum = (const int2 *)((const uint4 *)qfrag + kShareFragUint4);
-    if (shares_lds_split(tiles_of(r, 1).ntiles)) {
+    if (shares_lds_split(h, tiles_of(r, 1).ntiles)) {
         const Tiles t = tiles_of(r, 1);
         hipLaunchKernelGGL((shares_split_kernel<kSharesSplitT, kSharesSplitKS>),
                            dim3((uint32_t)((t.ntiles + kSharesSplitT - 1) / kSharesSplitT)), dim3(64 * kSharesSplitKS), 0,
@@ -607,7 +607,7 @@ int launch_shares_mfma(void *stream, const void *db, const void *qfrag, LaunchRa
                            r.first + r.n, out);
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
-    const int tpw = tiles_per_wave(tiles_of(r, 1).ntiles, kSharesTiles);
+    const int tpw = tiles_per_wave(h, tiles_of(r, 1).ntiles, kSharesTiles);
     const Tiles t = tiles_of(r, tpw);
     auto kern = tpw == 1 ? shares_mfma_kernel<1> : shares_mfma_kernel<>;
     hipLaunchKernelGGL(kern, dim3((uint32_t)t.grid), dim3(256), 0, (hipStream_t)stream, (const uint4 *)db,

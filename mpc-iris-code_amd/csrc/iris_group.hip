@@ -13,13 +13,27 @@
 //
 // Exchange record: one Partial (24 B: num, den, rotation, global index) per
 // shard and query.  Pipelined searches run the partials reduce, the all-gather
-// and the merge on each device's side stream, in order, so one send / recv
-// buffer per device serves every search in flight while the next search's
-// kernel already runs on the main stream.
+// and the merge on each device's side stream, in order, while the next search's
+// kernel already runs on the main stream.  The shard winners are written into a
+// ring of kSendRing send slots per device: a small (fused) shard search writes
+// its winner from the kernel itself, on the MAIN stream, so search k's kernels
+// wait for the all-gather that last read their slot (search k - kSendRing) --
+// without that order a search's kernel could overwrite the winners an earlier
+// search's all-gather, delayed by a slow peer, has not sent yet.  The recv buffer
+// is written and read on the side stream only, in order.
+//
+// Failure: the wait for a search (or batch) is bounded.  Its clock starts when
+// every local device has reached the exchange, i.e. when only the all-gather
+// (which waits for the peers) and the merge are left; RCCL's asynchronous error
+// is polled meanwhile.  On expiry or error the group's communicators are
+// aborted (ncclCommAbort) and the call returns IRIS_E_HIP; the group then
+// refuses every further call except the destroys.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <string.h>
 
+#include <array>
+#include <chrono>
 #include <new>
 #include <thread>
 
@@ -34,12 +48,20 @@ using namespace iris_api;
         if (r_ != ncclSuccess) return fail(IRIS_E_HIP, std::string(#x) + ": " + ncclGetErrorString(r_)); \
     } while (0)
 
+constexpr uint32_t kSendRing = 4;  // send slots per device (pipelined searches in flight per slot reuse)
+
 struct iris_group {
     std::vector<iris_device *> devs;  // local devices (owned)
     std::vector<ncclComm_t> comms;    // comms[i]: local device i, RCCL rank rank0 + i
     uint32_t ranks = 0, rank0 = 0;
     std::mutex mu;                    // serialises group calls
     std::atomic<int> refs{1};         // the group handle + each database and pending search
+    uint32_t timeout_ms = 0;          // exchange wait bound (0: auto, group_timeout)
+    // set when the communicators were aborted: every later call fails with broken_msg
+    std::atomic<bool> broken{false};
+    std::string broken_msg;
+    // test hook IRIS_GROUP_STALL: coherent host word the stalled all-gathers wait on
+    uint32_t *release = nullptr;
 };
 
 struct iris_group_db {
@@ -49,26 +71,50 @@ struct iris_group_db {
     uint32_t spd = 1, S = 0, first_shard = 0;
     std::vector<iris_db *> shards;          // local shard i lives on local device i / spd
     std::vector<uint64_t> first, count;     // global index of record 0, records
-    std::vector<DevBuf> send, recv;         // per local device: [spd] / [S] Partials (single query)
+    std::vector<DevBuf> send, recv;         // per local device: [kSendRing][spd] / [S] Partials (single query)
+    // per local device and send slot: recorded on the side stream after the all-gather that read it
+    std::vector<std::array<hipEvent_t, kSendRing>> sent;
+    uint64_t searches = 0;                  // ring cursor: search k uses send slot k % kSendRing
+    uint64_t max_count = 0;                 // largest local shard (the wait bound's estimate)
 };
 
 struct iris_group_pending {
     iris_group *g = nullptr;
     std::vector<Partial *> slots;  // pinned merge result of each local device
     std::vector<hipEvent_t> evs;   // recorded after each device's merge
+    std::vector<hipEvent_t> reached;  // recorded on each side stream just before the exchange
+    uint32_t timeout_ms = 0;
 };
 
 namespace {
 
 void group_teardown(iris_group *g) {
+    bool live = false;
     for (size_t i = 0; i < g->comms.size(); ++i) {
         if (!g->comms[i]) continue;
+        live = true;
         (void)hipSetDevice(g->devs[i]->ordinal);
         (void)hipStreamSynchronize(g->devs[i]->stream);
         if (g->devs[i]->aux) (void)hipStreamSynchronize(g->devs[i]->aux);
-        (void)ncclCommDestroy(g->comms[i]);
+    }
+    // One thread owns all local communicators: finalize them inside one RCCL group (each flushes
+    // its outstanding work without waiting for the others), then destroy them.  Aborted
+    // communicators (a broken group) are already gone.
+    if (live) {
+        ncclResult_t r = ncclGroupStart();
+        for (size_t i = 0; r == ncclSuccess && i < g->comms.size(); ++i)
+            if (g->comms[i]) r = ncclCommFinalize(g->comms[i]);
+        const ncclResult_t r2 = ncclGroupEnd();
+        for (size_t i = 0; i < g->comms.size(); ++i) {
+            if (!g->comms[i]) continue;
+            if (r == ncclSuccess && r2 == ncclSuccess)
+                (void)ncclCommDestroy(g->comms[i]);
+            else
+                (void)ncclCommAbort(g->comms[i]);  // finalize failed: release without flushing
+        }
     }
     for (iris_device *d : g->devs) iris_device_close(d);
+    if (g->release) (void)hipHostFree(g->release);
     delete g;
 }
 
@@ -123,10 +169,168 @@ inline uint64_t shard_first(uint64_t total, uint32_t S, uint32_t s) {
     return (uint64_t)((unsigned __int128)total * s / S);
 }
 
+int usable(const iris_group *g) {
+    if (g->broken.load(std::memory_order_acquire))
+        return fail(IRIS_E_HIP, "the device group was aborted (" + g->broken_msg + "); destroy it and form a new one");
+    return 0;
+}
+
 int search_args(iris_group_db *gdb) {
     ARG(gdb, "NULL argument");
     ARG(gdb->kind == IRIS_KIND_TEMPLATES, "group search needs a template database");
+    return usable(gdb->g);
+}
+
+// ---- test hooks (IRIS_TEST_HOOKS=1, iris_internal.hpp Hooks): a one-thread kernel on the side stream
+// before the all-gather that spins on the wall clock for `ticks` (IRIS_GROUP_DELAY_US: a slow peer), or
+// until the host sets *release, at most `ticks` (IRIS_GROUP_STALL: a peer that never arrives; the
+// grid always drains within the cap)
+
+constexpr uint64_t kStallCapUs = 60ull * 1000 * 1000;
+
+__global__ void hook_spin_kernel(uint64_t ticks, const uint32_t *release) {
+    const uint64_t t0 = wall_clock64();
+    while (wall_clock64() - t0 < ticks) {
+        if (release && __hip_atomic_load(release, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) return;
+        __builtin_amdgcn_s_sleep(8);
+    }
+}
+
+int enqueue_hooks(iris_group *g, iris_device *d, hipStream_t stream) {
+    const Hooks &h = d->hooks;
+    if (!h.group_delay_us && !h.group_stall) return 0;
+    int khz = 0;
+    HIPCHK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, d->ordinal));
+    if (h.group_delay_us)
+        hipLaunchKernelGGL(hook_spin_kernel, dim3(1), dim3(1), 0, stream, (uint64_t)h.group_delay_us * khz / 1000,
+                           (const uint32_t *)nullptr);
+    if (h.group_stall) {
+        if (!g->release) {
+            void *p = nullptr;
+            HIPCHK(hipHostMalloc(&p, 64, hipHostMallocCoherent | hipHostMallocMapped));
+            g->release = (uint32_t *)p;
+            __atomic_store_n(g->release, 0u, __ATOMIC_RELEASE);
+        }
+        hipLaunchKernelGGL(hook_spin_kernel, dim3(1), dim3(1), 0, stream, kStallCapUs * khz / 1000,
+                           (const uint32_t *)g->release);
+    }
+    HIPCHK(hipGetLastError());
     return 0;
+}
+
+bool stall_hooked(const iris_group *g) {
+    for (const iris_device *d : g->devs)
+        if (d->hooks.group_stall) return true;
+    return false;
+}
+
+// ---- bounded waits and abort
+
+// The exchange wait bound: IRIS_GROUP_TIMEOUT_MS / iris_group_set_timeout, else 10 x the local
+// work the call enqueued (at 5e10 comparisons/s, a fifth of one GPU's single-query rate), at least
+// 30 s -- generous: it only has to turn a lost peer from a hang into an error.
+uint32_t group_timeout(const iris_group *g, uint64_t records, uint32_t nq) {
+    if (g->timeout_ms) return g->timeout_ms;
+    if (g->devs[0]->hooks.group_timeout_ms) return g->devs[0]->hooks.group_timeout_ms;
+    const double est_ms = (double)records * nq * kRot / 5e10 * 1e3;
+    return (uint32_t)std::min(24.0 * 3600 * 1000, std::max(30000.0, 10 * est_ms));
+}
+
+// True when every device stream and side stream of the group has drained within `ms`.
+bool drain(iris_group *g, uint32_t ms) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        bool idle = true;
+        for (iris_device *d : g->devs) {
+            (void)hipSetDevice(d->ordinal);
+            if (hipStreamQuery(d->stream) == hipErrorNotReady) idle = false;
+            if (d->aux && hipStreamQuery(d->aux) == hipErrorNotReady) idle = false;
+        }
+        if (idle) return true;
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(ms)) return false;
+        std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
+}
+
+// Aborts the group's communicators (an all-gather stuck on a lost peer polls RCCL's abort flag and
+// ends) and marks the group broken.  Returns whether the streams drained (only then may the
+// caller recycle what the aborted work wrote into).  Caller holds g->mu.
+bool group_abort(iris_group *g, const std::string &why) {
+    if (!g->broken.load(std::memory_order_acquire)) {
+        g->broken_msg = why;
+        g->broken.store(true, std::memory_order_release);
+    }
+    const bool stalled = stall_hooked(g);
+    if (g->release) __atomic_store_n(g->release, 1u, __ATOMIC_RELEASE);
+    // The stall hook stands in for a lost peer but holds its (1-rank) all-gather back rather than
+    // inside RCCL: let it run out first, so no RCCL work is still queued when the communicator goes.
+    bool drained = stalled ? drain(g, 10000) : true;
+    for (size_t i = 0; i < g->comms.size(); ++i) {
+        if (!g->comms[i]) continue;
+        (void)hipSetDevice(g->devs[i]->ordinal);
+        (void)ncclCommAbort(g->comms[i]);
+        g->comms[i] = nullptr;
+    }
+    if (!stalled) drained = drain(g, 10000);
+    return drained;
+}
+
+// Waits for every done[i] (one per local device), bounded as described at the top of the file.
+// Returns 0, or fails after aborting the group; *drained tells whether the devices are idle.
+// locked: the caller holds g->mu (else the abort takes it).
+int group_wait(iris_group *g, const std::vector<hipEvent_t> &reached, const std::vector<hipEvent_t> &done,
+               uint32_t timeout_ms, bool locked, bool *drained) {
+    *drained = true;
+    using clk = std::chrono::steady_clock;
+    const auto t_start = clk::now();
+    bool at_exchange = false;
+    clk::time_point t_reached;
+    std::string why;
+    for (uint64_t it = 0;; ++it) {
+        bool all = true;
+        for (size_t i = 0; i < done.size() && why.empty(); ++i) {
+            (void)hipSetDevice(g->devs[i]->ordinal);
+            const hipError_t q = hipEventQuery(done[i]);
+            if (q == hipErrorNotReady)
+                all = false;
+            else if (q != hipSuccess)
+                why = std::string("hipEventQuery: ") + hipGetErrorString(q);
+        }
+        if (all && why.empty()) return 0;
+        if (why.empty() && !at_exchange) {
+            bool r = true;
+            for (size_t i = 0; i < reached.size() && r; ++i) {
+                (void)hipSetDevice(g->devs[i]->ordinal);
+                r = hipEventQuery(reached[i]) == hipSuccess;
+            }
+            if (r) {
+                at_exchange = true;
+                t_reached = clk::now();
+            }
+        }
+        if (why.empty() && (it & 255) == 255) {
+            for (size_t i = 0; i < g->comms.size() && why.empty(); ++i) {
+                ncclResult_t ae = ncclSuccess;
+                if (g->comms[i] && ncclCommGetAsyncError(g->comms[i], &ae) == ncclSuccess && ae != ncclSuccess &&
+                    ae != ncclInProgress)
+                    why = std::string("RCCL asynchronous error: ") + ncclGetErrorString(ae);
+            }
+            if (why.empty() && at_exchange && clk::now() - t_reached > std::chrono::milliseconds(timeout_ms))
+                why = "the exchange did not complete within " + std::to_string(timeout_ms) +
+                      " ms (a peer rank failed or is unreachable)";
+        }
+        if (!why.empty()) {
+            std::unique_lock<std::mutex> gl(g->mu, std::defer_lock);
+            if (!locked) gl.lock();
+            *drained = group_abort(g, why);
+            return fail(IRIS_E_HIP, "device group aborted: " + why +
+                                        (*drained ? std::string() : std::string(" (device work still outstanding)")));
+        }
+        if (clk::now() - t_start < std::chrono::milliseconds(2))
+            __builtin_ia32_pause();
+        else
+            std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
 }
 
 bool same_partial(const Partial &a, const Partial &b) {
@@ -157,6 +361,9 @@ void gdb_free_locked(iris_group_db *gdb) {
         if (d->aux) (void)hipStreamSynchronize(d->aux);
         if (gdb->send[i].p) (void)hipFree(gdb->send[i].p);
         if (gdb->recv[i].p) (void)hipFree(gdb->recv[i].p);
+        if (i < gdb->sent.size())
+            for (hipEvent_t &e : gdb->sent[i])
+                if (e) (void)hipEventDestroy(e);
     }
     delete gdb;
 }
@@ -262,11 +469,19 @@ int iris_group_db_destroy(iris_group_db_t *gdb) {
     return 0;
 }
 
+int iris_group_set_timeout(iris_group_t *g, uint32_t ms) {
+    ARG(g, "NULL argument");
+    std::lock_guard<std::mutex> gl(g->mu);
+    g->timeout_ms = ms;
+    return 0;
+}
+
 int iris_group_db_create(iris_group_t *g, int kind, uint64_t total, int layout, uint32_t spd, iris_group_db_t **out) {
     IRIS_KEEP_DEVICE();
     ARG(g && out, "NULL argument");
     ARG(spd >= 1, "shards_per_device must be at least 1");
     CHK(check_kind(kind));
+    CHK(usable(g));
     std::lock_guard<std::mutex> gl(g->mu);
     iris_group_db *gdb = new (std::nothrow) iris_group_db();
     if (!gdb) return fail(IRIS_E_NOMEM, "out of host memory");
@@ -290,15 +505,23 @@ int iris_group_db_create(iris_group_t *g, int kind, uint64_t total, int layout, 
         gdb->shards.push_back(db);
         gdb->first.push_back(f);
         gdb->count.push_back(c);
+        gdb->max_count = std::max(gdb->max_count, c);
     }
     gdb->send.resize(L);
     gdb->recv.resize(L);
+    gdb->sent.resize(L);
+    for (auto &ev : gdb->sent) ev.fill(nullptr);
     for (uint32_t i = 0; i < L && rc == 0; ++i) {
         iris_device *d = g->devs[i];
         std::lock_guard<std::recursive_mutex> l(d->mu);
         rc = set_device(d);
-        if (rc == 0) rc = ensure(gdb->send[i], (size_t)spd * sizeof(Partial));
+        if (rc == 0) rc = ensure(gdb->send[i], (size_t)kSendRing * spd * sizeof(Partial));
         if (rc == 0) rc = ensure(gdb->recv[i], (size_t)gdb->S * sizeof(Partial));
+        for (uint32_t b = 0; rc == 0 && b < kSendRing; ++b)
+            if (hipEventCreateWithFlags(&gdb->sent[i][b], hipEventDisableTiming) != hipSuccess) {
+                gdb->sent[i][b] = nullptr;
+                rc = fail(IRIS_E_HIP, "hipEventCreate failed");
+            }
     }
     if (rc != 0) {
         const std::string m = g_err;
@@ -332,6 +555,7 @@ int iris_group_db_shard(const iris_group_db_t *gdb, uint32_t i, iris_db_t **db, 
 int iris_group_db_generate(iris_group_db_t *gdb, uint64_t seed) {
     IRIS_KEEP_DEVICE();
     ARG(gdb, "NULL argument");
+    CHK(usable(gdb->g));
     iris_group *g = gdb->g;
     std::lock_guard<std::mutex> gl(g->mu);
     return per_device(g, [&](size_t i) {
@@ -350,6 +574,7 @@ int iris_group_db_generate(iris_group_db_t *gdb, uint64_t seed) {
 int iris_group_db_write(iris_group_db_t *gdb, uint64_t index, const void *records, uint64_t n) {
     IRIS_KEEP_DEVICE();
     ARG(gdb, "NULL argument");
+    CHK(usable(gdb->g));
     if (index > gdb->total || n > gdb->total - index) return fail(IRIS_E_RANGE, "record range outside the group database");
     if (n == 0) return 0;
     ARG(records, "records is NULL");
@@ -366,6 +591,7 @@ int iris_group_db_write(iris_group_db_t *gdb, uint64_t index, const void *record
 int iris_group_db_read(const iris_group_db_t *gdb, uint64_t index, uint64_t n, void *records) {
     IRIS_KEEP_DEVICE();
     ARG(gdb, "NULL argument");
+    CHK(usable(gdb->g));
     if (index > gdb->total || n > gdb->total - index) return fail(IRIS_E_RANGE, "record range outside the group database");
     if (n == 0) return 0;
     ARG(records, "records is NULL");
@@ -386,6 +612,7 @@ int iris_group_db_read(const iris_group_db_t *gdb, uint64_t index, uint64_t n, v
 int iris_group_db_load_file(iris_group_db_t *gdb, const char *path, uint64_t first) {
     IRIS_KEEP_DEVICE();
     ARG(gdb && path, "NULL argument");
+    CHK(usable(gdb->g));
     iris_group *g = gdb->g;
     std::lock_guard<std::mutex> gl(g->mu);
     return per_device(g, [&](size_t i) {
@@ -412,14 +639,18 @@ int iris_group_template_search_async(iris_group_db_t *gdb, const iris_template_t
     ARG(query && out, "NULL argument");
     iris_group *g = gdb->g;
     std::lock_guard<std::mutex> gl(g->mu);
+    CHK(usable(g));
     DeviceLocks locks(g);
     const size_t L = g->devs.size();
+    const bool remote = g->ranks > L;  // peers in other processes take part in the exchange
     iris_group_pending *p = new (std::nothrow) iris_group_pending();
     if (!p) return fail(IRIS_E_NOMEM, "out of host memory");
     p->g = g;
     p->slots.assign(L, nullptr);
     p->evs.assign(L, nullptr);
-    auto abandon = [&](int rc) {
+    p->reached.assign(L, nullptr);
+    p->timeout_ms = group_timeout(g, gdb->max_count, 1);
+    auto abandon = [&](int rc, bool gather_started) {
         const std::string m = g_err;
         for (size_t i = 0; i < L; ++i) {
             iris_device *d = g->devs[i];
@@ -428,19 +659,29 @@ int iris_group_template_search_async(iris_group_db_t *gdb, const iris_template_t
             if (d->aux) (void)hipStreamSynchronize(d->aux);
             if (p->slots[i]) d->free_slots.push_back(p->slots[i]);
             if (p->evs[i]) d->event_pool.push_back(p->evs[i]);
+            if (p->reached[i]) d->event_pool.push_back(p->reached[i]);
         }
         delete p;
+        // The peers are (or will be) inside this search's all-gather, and this process's
+        // communicators are out of step with theirs: abort rather than let every rank hang.
+        if (remote || gather_started) (void)group_abort(g, "a rank failed to enqueue its search: " + m);
         return fail(rc, m);
     };
-    // per device: the query's engine, then every local shard's search + reduce (side stream)
+    const uint32_t b = (uint32_t)(gdb->searches++ % kSendRing);
+    // per device: the query's engine, then every local shard's search + reduce into send slot b
     for (size_t i = 0; i < L; ++i) {
         iris_device *d = g->devs[i];
         int rc = set_device(d);
         iris_engine *e = nullptr;
         if (rc == 0) rc = take_result_slot(d, &p->slots[i]);
         if (rc == 0 && !(p->evs[i] = take_event(d))) rc = fail(IRIS_E_HIP, "hipEventCreate failed");
+        if (rc == 0 && !(p->reached[i] = take_event(d))) rc = fail(IRIS_E_HIP, "hipEventCreate failed");
         if (rc == 0) rc = template_engine_locked(d, query, &e);
-        Partial *send = (Partial *)gdb->send[i].p;
+        Partial *send = (Partial *)gdb->send[i].p + (size_t)b * gdb->spd;
+        // a fused shard search writes its winner from the kernel, on the device stream: the
+        // all-gather that last read slot b (search k - kSendRing, side stream) precedes it
+        if (rc == 0 && !d->hooks.group_unordered && hipStreamWaitEvent(d->stream, gdb->sent[i][b], 0) != hipSuccess)
+            rc = fail(IRIS_E_HIP, "hipStreamWaitEvent");
         for (uint32_t j = 0; rc == 0 && j < gdb->spd; ++j) {
             const size_t s = i * gdb->spd + j;
             if (gdb->count[s] == 0) {  // an empty shard sends "no candidate"
@@ -451,27 +692,30 @@ int iris_group_template_search_async(iris_group_db_t *gdb, const iris_template_t
             }
         }
         if (e) engine_free(e);
-        if (rc != 0) return abandon(rc);
+        if (rc == 0 && hipEventRecord(p->reached[i], d->aux) != hipSuccess) rc = fail(IRIS_E_HIP, "hipEventRecord");
+        if (rc == 0) rc = enqueue_hooks(g, d, d->aux);
+        if (rc != 0) return abandon(rc, false);
     }
     // the exchange: every device's shard winners to every device (side streams, in order after the reduces)
     {
         ncclResult_t r = ncclGroupStart();
         for (size_t i = 0; r == ncclSuccess && i < L; ++i)
-            r = ncclAllGather(gdb->send[i].p, gdb->recv[i].p, (size_t)gdb->spd * sizeof(Partial), ncclUint8, g->comms[i],
-                              g->devs[i]->aux);
+            r = ncclAllGather((Partial *)gdb->send[i].p + (size_t)b * gdb->spd, gdb->recv[i].p,
+                              (size_t)gdb->spd * sizeof(Partial), ncclUint8, g->comms[i], g->devs[i]->aux);
         const ncclResult_t r2 = ncclGroupEnd();
         if (r == ncclSuccess) r = r2;
-        if (r != ncclSuccess) return abandon(fail(IRIS_E_HIP, std::string("ncclAllGather: ") + ncclGetErrorString(r)));
+        if (r != ncclSuccess) return abandon(fail(IRIS_E_HIP, std::string("ncclAllGather: ") + ncclGetErrorString(r)), true);
     }
     for (size_t i = 0; i < L; ++i) {
         iris_device *d = g->devs[i];
         int rc = set_device(d);
+        if (rc == 0 && hipEventRecord(gdb->sent[i][b], d->aux) != hipSuccess) rc = fail(IRIS_E_HIP, "hipEventRecord");
         if (rc == 0)
             rc = timed(d, "group_merge", gdb->S, [&] {
                 return launch_group_merge(d->aux, (const Partial *)gdb->recv[i].p, gdb->S, 1, 1, p->slots[i]);
             }, d->aux);
         if (rc == 0 && hipEventRecord(p->evs[i], d->aux) != hipSuccess) rc = fail(IRIS_E_HIP, "hipEventRecord");
-        if (rc != 0) return abandon(rc);
+        if (rc != 0) return abandon(rc, true);
     }
     group_retain(g);
     *out = p;
@@ -484,22 +728,23 @@ int iris_group_pending_wait(iris_group_pending_t *p, iris_match_t *out) {
     iris_group *g = p->g;
     const size_t L = g->devs.size();
     std::vector<Partial> res(L);
-    hipError_t err = hipSuccess;
-    for (size_t i = 0; i < L; ++i) {
-        const hipError_t e = hipEventSynchronize(p->evs[i]);
-        if (e != hipSuccess && err == hipSuccess) err = e;
-        if (e == hipSuccess) memcpy(&res[i], p->slots[i], sizeof(Partial));
-    }
-    for (size_t i = 0; i < L; ++i) {
-        iris_device *d = g->devs[i];
-        std::lock_guard<std::recursive_mutex> l(d->mu);
-        d->free_slots.push_back(p->slots[i]);
-        d->event_pool.push_back(p->evs[i]);
-        fold_done(d);
-    }
+    bool drained = true;
+    const int rc = group_wait(g, p->reached, p->evs, p->timeout_ms, false, &drained);
+    const std::string m = rc ? g_err : std::string();
+    if (rc == 0)
+        for (size_t i = 0; i < L; ++i) memcpy(&res[i], p->slots[i], sizeof(Partial));
+    if (drained)  // otherwise aborted work may still write them: leaked rather than reused
+        for (size_t i = 0; i < L; ++i) {
+            iris_device *d = g->devs[i];
+            std::lock_guard<std::recursive_mutex> l(d->mu);
+            d->free_slots.push_back(p->slots[i]);
+            d->event_pool.push_back(p->evs[i]);
+            d->event_pool.push_back(p->reached[i]);
+            fold_done(d);
+        }
     delete p;
     group_release(g);
-    if (err != hipSuccess) return fail(IRIS_E_HIP, std::string("hipEventSynchronize: ") + hipGetErrorString(err));
+    if (rc != 0) return fail(rc, m);
     Partial best;
     CHK(agree(res, 1, 1, &best));
     if (out) fill_match(best, out);
@@ -524,13 +769,19 @@ int iris_group_template_batch_search(iris_group_db_t *gdb, const iris_template_t
         "batched search of more than 3 queries needs a template database in the TILES layout");
     iris_group *g = gdb->g;
     std::lock_guard<std::mutex> gl(g->mu);
+    CHK(usable(g));
     DeviceLocks locks(g);
     const size_t L = g->devs.size();
+    const bool remote = g->ranks > L;
+    std::vector<hipEvent_t> reached(L, nullptr), done(L, nullptr);
+    bool gather_started = false;
     const uint32_t spd = gdb->spd, S = gdb->S;
     const uint32_t stride = nq <= kBatchStreamMax ? nq : (nq + batch_query_group() - 1) / batch_query_group() * batch_query_group();
     std::vector<DevBuf> send(L), recv(L);
     std::vector<iris_engine *> eng(L, nullptr);
+    bool drained = true;
     auto cleanup = [&] {
+        if (!drained) return;  // aborted work may still use them: leaked rather than freed
         for (size_t i = 0; i < L; ++i) {
             iris_device *d = g->devs[i];
             (void)hipSetDevice(d->ordinal);
@@ -538,6 +789,8 @@ int iris_group_template_batch_search(iris_group_db_t *gdb, const iris_template_t
             if (eng[i]) iris_engine_destroy(eng[i]);
             if (send[i].p) (void)hipFree(send[i].p);
             if (recv[i].p) (void)hipFree(recv[i].p);
+            if (reached[i]) d->event_pool.push_back(reached[i]);
+            if (done[i]) d->event_pool.push_back(done[i]);
         }
     };
     int rc = 0;
@@ -547,6 +800,8 @@ int iris_group_template_batch_search(iris_group_db_t *gdb, const iris_template_t
         if (rc == 0) rc = ensure(send[i], (size_t)spd * stride * sizeof(Partial));
         if (rc == 0) rc = ensure(recv[i], (size_t)S * stride * sizeof(Partial));
         if (rc == 0) rc = ensure_host_result(d, (size_t)stride * sizeof(Partial));
+        if (rc == 0 && !(reached[i] = take_event(d))) rc = fail(IRIS_E_HIP, "hipEventCreate failed");
+        if (rc == 0 && !(done[i] = take_event(d))) rc = fail(IRIS_E_HIP, "hipEventCreate failed");
         if (rc == 0) rc = iris_template_batch_engine_new(d, queries, nq, &eng[i]);
         if (rc != 0) break;
         iris_engine *e = eng[i];
@@ -566,7 +821,7 @@ int iris_group_template_batch_search(iris_group_db_t *gdb, const iris_template_t
             size_t pmax = 0;
             for (uint32_t j = 0; j < spd; ++j) {
                 const size_t s = i * spd + j;
-                const BatchGeometry geo = batch_geometry(LaunchRange{0, gdb->count[s]}, nq);
+                const BatchGeometry geo = batch_geometry(d->hooks, LaunchRange{0, gdb->count[s]}, nq);
                 pmax = std::max(pmax, (size_t)geo.nqg * geo.qper * geo.G * sizeof(Partial));
             }
             rc = ensure(d->partials, pmax);
@@ -574,15 +829,18 @@ int iris_group_template_batch_search(iris_group_db_t *gdb, const iris_template_t
                 const size_t s = i * spd + j;
                 if (gdb->count[s] == 0) continue;
                 const LaunchRange r{0, gdb->count[s]};
-                const BatchGeometry geo = batch_geometry(r, nq);
+                const BatchGeometry geo = batch_geometry(d->hooks, r, nq);
                 rc = timed(d, "template_batch", r.n * nq, [&] {
-                    return launch_batch(d->stream, gdb->shards[s]->data, e->qfrag, r, geo, (Partial *)d->partials.p,
+                    return launch_batch(d->hooks, d->stream, gdb->shards[s]->data, e->qfrag, r, geo, (Partial *)d->partials.p,
                                         sbuf + (size_t)j * stride, gdb->first[s]);
                 });
             }
         }
+        if (rc == 0 && hipEventRecord(reached[i], d->stream) != hipSuccess) rc = fail(IRIS_E_HIP, "hipEventRecord");
+        if (rc == 0) rc = enqueue_hooks(g, d, d->stream);
     }
     if (rc == 0) {
+        gather_started = true;
         ncclResult_t r = ncclGroupStart();
         for (size_t i = 0; r == ncclSuccess && i < L; ++i)
             r = ncclAllGather(send[i].p, recv[i].p, (size_t)spd * stride * sizeof(Partial), ncclUint8, g->comms[i],
@@ -598,12 +856,19 @@ int iris_group_template_batch_search(iris_group_db_t *gdb, const iris_template_t
             rc = timed(d, "group_merge", (uint64_t)S * nq, [&] {
                 return launch_group_merge(d->stream, (const Partial *)recv[i].p, S, nq, stride, (Partial *)d->host_result);
             });
+        if (rc == 0 && hipEventRecord(done[i], d->stream) != hipSuccess) rc = fail(IRIS_E_HIP, "hipEventRecord");
     }
+    if (rc != 0 && (remote || gather_started)) {  // the peers are inside (or headed for) this exchange
+        const std::string m = g_err;
+        drained = group_abort(g, "a rank failed to enqueue its batch search: " + m);
+        rc = fail(rc, m);
+    }
+    if (rc == 0) rc = group_wait(g, reached, done, group_timeout(g, gdb->max_count, nq), true, &drained);
     std::vector<Partial> res((size_t)L * stride);
     for (size_t i = 0; i < L && rc == 0; ++i) {
         iris_device *d = g->devs[i];
         rc = set_device(d);
-        if (rc == 0) rc = sync(d);
+        if (rc == 0) fold_done(d);
         if (rc == 0) memcpy(&res[i * stride], d->host_result, (size_t)nq * sizeof(Partial));
     }
     const std::string m = rc != 0 ? g_err : std::string();

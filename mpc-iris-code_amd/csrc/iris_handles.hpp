@@ -60,6 +60,7 @@ struct DevBuf {
 
 struct iris_device {
     int ordinal = 0;
+    iris::Hooks hooks;  // environment knobs, read once when the device opened
     hipStream_t stream = nullptr;
     std::recursive_mutex mu;
     bool profiling = false;
@@ -130,7 +131,7 @@ inline uint64_t next_db_version() {
 // [first, first + n) are copied to the caller, the engine already computes [first + n, first + 2n)
 // on the device's side stream, its kernel storing the rows straight into the other of two pinned
 // host buffers; the next call, if it asks for exactly that range of the same version of the same
-// database, only copies those rows out.
+// database, only copies those rows out.  Speculation starts with the second consecutive call.
 struct Readahead {
     const struct iris_db *db = nullptr;
     uint64_t version = 0, first = 0, n = 0;  // the range in flight into rows[cur]
@@ -139,6 +140,11 @@ struct Readahead {
     hipEvent_t computed[2] = {nullptr, nullptr};  // side stream, after the kernel into rows[b]
     int cur = 0;
     bool pending = false;
+    // the previous call's range end: a call that starts there (or was read ahead) is part of a
+    // walk, and only then is the next range computed speculatively (a random-access caller
+    // never pays for rows it does not ask for)
+    const struct iris_db *last_db = nullptr;
+    uint64_t last_version = 0, last_end = 0;
 };
 
 struct iris_engine {

@@ -6,6 +6,7 @@
 // (the reference reaches the same permutation with whole-byte rotates plus a
 // carry chain, src/bits.rs:178-205; tests pin the two against each other).
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "iris_internal.hpp"
@@ -211,9 +212,11 @@ void build_query_tile(const iris_template_t *q, uint32_t *tile) {
 
 // ------------------------------------------------------------------ parallel host copies
 
+#include <algorithm>
 #include <atomic>
 #include <condition_variable>
 #include <mutex>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -297,6 +300,78 @@ int copy_helpers() {  // IRIS_COPY_HELPERS (0..15) overrides, read when the pool
 }
 
 }  // namespace
+
+// ---------------------------------------------------------------- runtime configuration
+
+namespace {
+
+// Test-only hooks in the order of Hooks::ignored's bits.
+constexpr const char *kHookNames[] = {"IRIS_TILES_PER_WAVE", "IRIS_FUSED_REDUCE", "IRIS_BATCH_KERNEL",
+                                      "IRIS_BATCH_XQG",      "IRIS_SCHEDULE",     "IRIS_LOAD_PREAD",
+                                      "IRIS_GROUP_DELAY_US", "IRIS_GROUP_STALL",  "IRIS_GROUP_UNORDERED"};
+constexpr int kNumHooks = (int)(sizeof(kHookNames) / sizeof(kHookNames[0]));
+
+const char *env(const char *name) {
+    const char *v = getenv(name);
+    return v && *v ? v : nullptr;
+}
+
+uint32_t env_u32(const char *v, uint32_t max) {
+    const long long x = atoll(v);
+    return x < 0 ? 0u : x > (long long)max ? max : (uint32_t)x;
+}
+
+}  // namespace
+
+void read_hooks(Hooks *h) {
+    *h = Hooks{};
+    if (const char *v = env("IRIS_READAHEAD")) h->readahead = v[0] != '0';
+    if (const char *v = env("IRIS_GROUP_TIMEOUT_MS")) h->group_timeout_ms = env_u32(v, 24u * 3600 * 1000);
+    const char *t = env("IRIS_TEST_HOOKS");
+    h->test = t && t[0] == '1';
+    for (int i = 0; i < kNumHooks; ++i) {
+        const char *v = env(kHookNames[i]);
+        if (!v) continue;
+        if (!h->test) {
+            h->ignored |= 1u << i;
+            continue;
+        }
+        switch (i) {
+        case 0: h->tiles_per_wave = atoi(v) == 1 ? 1 : 4; break;
+        case 1: h->fused_reduce = v[0] != '0'; break;
+        case 2: h->batch_kernel = atoi(v) >= 1 && atoi(v) <= 4 ? atoi(v) : 4; break;
+        case 3: h->batch_xqg = env_u32(v, 32); break;
+        case 4: h->schedule = !strcmp(v, "spin") ? 1 : !strcmp(v, "yield") ? 2 : !strcmp(v, "blocking") ? 3 : 0; break;
+        case 5: h->load_pread = v[0] != '0'; break;
+        case 6: h->group_delay_us = env_u32(v, 1000000); break;
+        case 7: h->group_stall = v[0] != '0'; break;
+        case 8: h->group_unordered = v[0] != '0'; break;
+        }
+    }
+}
+
+size_t format_hooks(const Hooks &h, char *buf, size_t len) {
+    static const char *sched[] = {"auto", "spin", "yield", "blocking"};
+    std::string s = "readahead=" + std::to_string(h.readahead) + " group_timeout_ms=" +
+                    (h.group_timeout_ms ? std::to_string(h.group_timeout_ms) : std::string("auto")) +
+                    " copy_helpers=" + std::to_string(copy_helpers()) + " test_hooks=" + std::to_string(h.test);
+    if (h.test)
+        s += " tiles_per_wave=" + (h.tiles_per_wave ? std::to_string(h.tiles_per_wave) : std::string("auto")) +
+             " fused_reduce=" + std::to_string(h.fused_reduce) + " batch_kernel=" + std::to_string(h.batch_kernel) +
+             " batch_xqg=" + std::to_string(h.batch_xqg) + " schedule=" + sched[h.schedule & 3] +
+             " load_pread=" + std::to_string(h.load_pread) + " group_delay_us=" + std::to_string(h.group_delay_us) +
+             " group_stall=" + std::to_string(h.group_stall) + " group_unordered=" + std::to_string(h.group_unordered);
+    std::string ign;
+    for (int i = 0; i < kNumHooks; ++i)
+        if (h.ignored >> i & 1u) ign += (ign.empty() ? "" : ",") + std::string(kHookNames[i]);
+    if (!ign.empty()) s += " ignored=" + ign;
+    if (buf && len) {
+        const size_t n = std::min(len - 1, s.size());
+        memcpy(buf, s.data(), n);
+        buf[n] = 0;
+    }
+    return s.size();
+}
 
 void parallel_copy(void *dst, const void *src, size_t bytes) {
     static std::mutex create_mu;

@@ -174,6 +174,33 @@ IRIS_HD inline uint64_t gen_limb(uint64_t key, uint64_t ctr) {
     return mix64(key + (ctr + 1) * 0x9E3779B97F4A7C15ULL);
 }
 
+// ---------------------------------------------------------------- runtime configuration
+// Environment knobs are read once, when a device opens (read_hooks, iris_host.cpp), into that
+// device's Hooks; launchers take them from there, never from the environment.  The test-only
+// hooks pin kernel variants or inject delays and faults: they are honoured only when
+// IRIS_TEST_HOOKS=1 is also set, and otherwise ignored (iris_config reports both).
+struct Hooks {
+    // production knobs
+    bool readahead = true;           // IRIS_READAHEAD=0: no read-ahead of host-output engine calls
+    uint32_t group_timeout_ms = 0;   // IRIS_GROUP_TIMEOUT_MS: bound of a group exchange wait (0: auto)
+    // test-only hooks (IRIS_TEST_HOOKS=1)
+    bool test = false;
+    int tiles_per_wave = 0;          // IRIS_TILES_PER_WAVE=1|4: pins the TILES kernels' variant (0: by range)
+    bool fused_reduce = true;        // IRIS_FUSED_REDUCE=0: small searches launch the separate reduce
+    int batch_kernel = 4;            // IRIS_BATCH_KERNEL=1..4: batched-query kernel form (iris_batch.hip)
+    uint32_t batch_xqg = 0;          // IRIS_BATCH_XQG: XCD-aware grid of batch kernel 1
+    int schedule = 0;                // IRIS_SCHEDULE=spin|yield|blocking (1|2|3): host wait mode
+    bool load_pread = false;         // IRIS_LOAD_PREAD=1: file loads through the pinned-buffer path
+    uint32_t group_delay_us = 0;     // IRIS_GROUP_DELAY_US: side-stream spin before each group all-gather
+    bool group_stall = false;        // IRIS_GROUP_STALL=1: a group all-gather waits on a peer that never comes
+    bool group_unordered = false;    // IRIS_GROUP_UNORDERED=1: drop the exchange-buffer ordering (shows the race)
+    uint32_t ignored = 0;            // bit i: test hook kHookNames[i] was set without IRIS_TEST_HOOKS=1
+};
+// Reads the environment (the Hooks a device opened now gets).
+void read_hooks(Hooks *h);
+// "key=value ..." of h plus the process-wide knobs (IRIS_COPY_HELPERS); returns the length.
+size_t format_hooks(const Hooks &h, char *buf, size_t len);
+
 // ---------------------------------------------------------------- launchers
 // (defined in iris_kernels.hip; all asynchronous on `stream`)
 struct LaunchRange {
@@ -203,7 +230,7 @@ int launch_generate(void *stream, const KindInfo &k, void *db, uint64_t t_first,
                     uint64_t global_index0);
 int launch_template_counts(void *stream, const void *db, const void *qtab, LaunchRange r, uint16_t *num_out,
                            uint16_t *den_out);
-int launch_template_mfma_counts(void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *num_out,
+int launch_template_mfma_counts(const Hooks &h, void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *num_out,
                                 uint16_t *den_out);
 // Fused finish of a small search (grids of at most kFusedReduceMax workgroups): the last
 // workgroup to finish reduces the partials and writes the winner (idx + idx_base) to dst;
@@ -219,10 +246,10 @@ struct FusedFinish {
     uint32_t seq;
 };
 constexpr uint32_t kFusedReduceMax = 4096;
-bool fused_search_ok(LaunchRange r);
-int launch_template_mfma_search(void *stream, const void *db, const void *qfrag, LaunchRange r, double *dist_out,
+bool fused_search_ok(const Hooks &h, LaunchRange r);
+int launch_template_mfma_search(const Hooks &h, void *stream, const void *db, const void *qfrag, LaunchRange r, double *dist_out,
                                 Partial *partials, uint32_t *n_partials, const FusedFinish *fin = nullptr);
-uint32_t mfma_search_partials(LaunchRange r);
+uint32_t mfma_search_partials(const Hooks &h, LaunchRange r);
 // nq = 2 queries per streamed pass; partials [nq][*n_partials]
 uint32_t multi_search_partials(LaunchRange r, int nq);
 int launch_template_multi_search(void *stream, const void *db, const void *const *qfrags, int nq, LaunchRange r,
@@ -234,9 +261,9 @@ int launch_pack_tiles_kind(void *stream, int kind, const void *staging, void *db
 int launch_unpack_tiles_kind(void *stream, int kind, const void *db, void *staging, uint64_t t_first, uint64_t n);
 int launch_generate_tiles_kind(void *stream, int kind, void *db, uint64_t t_first, uint64_t n, uint64_t seed,
                                uint64_t global_index0);
-int launch_masks_mfma(void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *out);
-uint32_t masks_resolve_partials(LaunchRange r);
-int launch_masks_resolve(void *stream, const void *db, const void *qfrag, LaunchRange r,
+int launch_masks_mfma(const Hooks &h, void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *out);
+uint32_t masks_resolve_partials(const Hooks &h, LaunchRange r);
+int launch_masks_resolve(const Hooks &h, void *stream, const void *db, const void *qfrag, LaunchRange r,
                          const uint16_t *const *shares, uint32_t parts, double *dist_out, Partial *partials);
 uint32_t resolver_partials(uint64_t n);
 struct BatchGeometry {
@@ -245,13 +272,13 @@ struct BatchGeometry {
     uint32_t qper;    // queries per query group (nqg * qper results; at most the engine's padding)
     uint32_t xqg;     // > 0: XCD-aware grid, xqg query groups per XCD at a time (iris_batch.hip)
 };
-BatchGeometry batch_geometry(LaunchRange r, uint32_t nq);
+BatchGeometry batch_geometry(const Hooks &h, LaunchRange r, uint32_t nq);
 uint32_t batch_query_group();  // queries per batch_kernel query group (padding unit)
-int launch_batch(void *stream, const void *db, const void *qtiles, LaunchRange r, const BatchGeometry &g,
+int launch_batch(const Hooks &h, void *stream, const void *db, const void *qtiles, LaunchRange r, const BatchGeometry &g,
                  Partial *partials, Partial *out, uint64_t idx_base = 0);
 int launch_resolver(void *stream, const uint16_t *const *shares, uint32_t parts, const uint16_t *denoms, uint64_t n,
                     double *dist_out, Partial *partials);
-int launch_shares_mfma(void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *out);
+int launch_shares_mfma(const Hooks &h, void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *out);
 int launch_template_search(void *stream, const void *db, const void *qtab, LaunchRange r, double *dist_out,
                            Partial *partials, uint32_t *n_partials);
 // consumes partials; the winner's idx (range-relative) is offset by idx_base

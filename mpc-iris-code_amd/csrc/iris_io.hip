@@ -148,7 +148,7 @@ int iris_db_load_file(iris_db_t *db, const char *path, uint64_t first, uint64_t 
         const uint64_t unit = page / gcd;
         const uint64_t pch = std::max<uint64_t>(unit, ch / unit * unit);
         const uint64_t lead = (first + unit - 1) / unit * unit - first;  // records before an aligned boundary
-        const bool force_pread = getenv("IRIS_LOAD_PREAD") != nullptr;  // test hook: the fallback path
+        const bool force_pread = db->dev->hooks.load_pread;  // test hook: the fallback path
         void *map = pch <= ch && !force_pread ? ::mmap(nullptr, (size_t)size, PROT_READ, MAP_SHARED, f.fd, 0)
                                               : MAP_FAILED;
         if (map != MAP_FAILED) {

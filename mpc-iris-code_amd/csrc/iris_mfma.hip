@@ -520,7 +520,7 @@ constexpr uint64_t kSmallTiles = 4 * kWaveSlots * 256 * 2;
 // one tile's K instead.
 constexpr uint64_t kSplitTiles = 1024;
 
-static TileRange tile_range(LaunchRange r) {
+static TileRange tile_range(const Hooks &h, LaunchRange r) {
     TileRange t;
     t.tile0 = r.first / kTileRecs;
     const uint64_t tile1 = (r.first + r.n + kTileRecs - 1) / kTileRecs;
@@ -529,8 +529,8 @@ static TileRange tile_range(LaunchRange r) {
     t.ksplit = t.ntiles <= kSplitTiles ? 4 : 1;
     // test hook: IRIS_TILES_PER_WAVE=1|4 pins the variant (tests run all three on small ranges:
     // unset = the K-split form there)
-    if (const char *f = getenv("IRIS_TILES_PER_WAVE")) {
-        t.tiles_per_wave = atoi(f) == 1 ? 1 : kMfmaTiles;
+    if (h.tiles_per_wave) {
+        t.tiles_per_wave = h.tiles_per_wave == 1 ? 1 : kMfmaTiles;
         t.ksplit = 1;
     }
     if (t.ksplit > 1) {
@@ -543,7 +543,7 @@ static TileRange tile_range(LaunchRange r) {
     return t;
 }
 
-uint32_t mfma_search_partials(LaunchRange r) { return (uint32_t)tile_range(r).grid; }
+uint32_t mfma_search_partials(const Hooks &h, LaunchRange r) { return (uint32_t)tile_range(h, r).grid; }
 
 uint32_t multi_search_partials(LaunchRange r, int nq) {
     const uint64_t tile0 = r.first / kTileRecs, tile1 = (r.first + r.n + kTileRecs - 1) / kTileRecs;
@@ -564,10 +564,10 @@ int launch_template_multi_search(void *stream, const void *db, const void *const
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_template_mfma_counts(void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *num_out,
+int launch_template_mfma_counts(const Hooks &h, void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *num_out,
                                 uint16_t *den_out) {
     if (r.n == 0) return 0;
-    const TileRange t = tile_range(r);
+    const TileRange t = tile_range(h, r);
     auto kern = t.ksplit > 1 ? template_mfma_kernel<MF_COUNTS, kSplitT, 4>
                 : t.tiles_per_wave == 1 ? template_mfma_kernel<MF_COUNTS, 1> : template_mfma_kernel<MF_COUNTS>;
     hipLaunchKernelGGL(kern, dim3((uint32_t)t.grid), dim3(256), 0, (hipStream_t)stream,
@@ -576,9 +576,9 @@ int launch_template_mfma_counts(void *stream, const void *db, const void *qfrag,
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_template_mfma_search(void *stream, const void *db, const void *qfrag, LaunchRange r, double *dist_out,
+int launch_template_mfma_search(const Hooks &h, void *stream, const void *db, const void *qfrag, LaunchRange r, double *dist_out,
                                 Partial *partials, uint32_t *n_partials, const FusedFinish *fin) {
-    const TileRange t = tile_range(r);
+    const TileRange t = tile_range(h, r);
     *n_partials = (uint32_t)t.grid;
     if (r.n == 0) return 0;
     const bool fused = fin && t.grid <= kFusedReduceMax;
@@ -595,10 +595,9 @@ int launch_template_mfma_search(void *stream, const void *db, const void *qfrag,
 }
 
 // test hook: IRIS_FUSED_REDUCE=0 runs small searches with the separate reduce kernel
-bool fused_search_ok(LaunchRange r) {
-    const char *f = getenv("IRIS_FUSED_REDUCE");
-    if (f && f[0] == '0') return false;
-    return r.n > 0 && tile_range(r).grid <= kFusedReduceMax;
+bool fused_search_ok(const Hooks &h, LaunchRange r) {
+    if (!h.fused_reduce) return false;
+    return r.n > 0 && tile_range(h, r).grid <= kFusedReduceMax;
 }
 
 }  // namespace iris

@@ -72,6 +72,7 @@ def load_library(path=None):
         sig = {
             "iris_last_error": ([], ctypes.c_char_p),
             "iris_version": ([], ctypes.c_char_p),
+            "iris_config": ([P, ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)], ctypes.c_int),
             "iris_device_count": ([ctypes.POINTER(ctypes.c_int)], ctypes.c_int),
             "iris_device_open": ([ctypes.c_int, PP], ctypes.c_int),
             "iris_device_close": ([P], ctypes.c_int),
@@ -143,6 +144,7 @@ def load_library(path=None):
             "iris_group_unique_id": ([P], ctypes.c_int),
             "iris_group_create_rank": ([ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, P, PP], ctypes.c_int),
             "iris_group_destroy": ([P], ctypes.c_int),
+            "iris_group_set_timeout": ([P, ctypes.c_uint32], ctypes.c_int),
             "iris_group_info": ([P, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32),
                                  ctypes.POINTER(ctypes.c_uint32)], ctypes.c_int),
             "iris_group_device": ([P, ctypes.c_uint32, PP], ctypes.c_int),
@@ -171,7 +173,7 @@ def load_library(path=None):
 
 def exported_symbols():
     return [
-        "iris_last_error", "iris_version", "iris_device_count", "iris_device_open", "iris_device_close",
+        "iris_last_error", "iris_version", "iris_config", "iris_device_count", "iris_device_open", "iris_device_close",
         "iris_device_synchronize", "iris_device_stream", "iris_device_set_profiling", "iris_device_kernel_stats",
         "iris_device_reset_stats", "iris_device_alloc", "iris_device_free", "iris_memcpy_d2h", "iris_db_create",
         "iris_db_create_ex", "iris_db_layout",
@@ -187,7 +189,7 @@ def exported_symbols():
         "iris_query_table_sizes", "iris_engine_query_tables", "iris_host_query_tables", "iris_device_memory",
         "iris_template_search_async", "iris_pending_wait",
         "iris_db_attach_host", "iris_db_detach_host",
-        "iris_group_create", "iris_group_unique_id", "iris_group_create_rank", "iris_group_destroy", "iris_group_info",
+        "iris_group_create", "iris_group_unique_id", "iris_group_create_rank", "iris_group_destroy", "iris_group_set_timeout", "iris_group_info",
         "iris_group_device", "iris_group_db_create", "iris_group_db_destroy", "iris_group_db_info",
         "iris_group_db_shard", "iris_group_db_generate", "iris_group_db_write", "iris_group_db_read",
         "iris_group_db_load_file", "iris_group_template_search", "iris_group_template_search_async",
@@ -471,6 +473,10 @@ class Device:
     def synchronize(self):
         _check(load_library().iris_device_synchronize(self.handle))
 
+    def config(self):
+        """The environment knobs this device read when it opened (iris_config), as a dict."""
+        return config(self)
+
     def memory(self):
         """(free, total) device memory in bytes."""
         f, t = ctypes.c_size_t(), ctypes.c_size_t()
@@ -510,6 +516,22 @@ class Device:
     def h2d(self, device_ptr, host_array):
         a = np.ascontiguousarray(host_array)
         _check(load_library().iris_memcpy_h2d(self.handle, ctypes.c_void_p(device_ptr), _ptr(a), a.nbytes))
+
+
+def config(device=None):
+    """iris_config as a dict: the knobs of `device`, or (None) those a device opened now would get.
+    Test-only hooks set without IRIS_TEST_HOOKS=1 appear under "ignored" (a list)."""
+    lib = load_library()
+    h = device.handle if device is not None else None
+    need = ctypes.c_size_t()
+    _check(lib.iris_config(h, None, 0, ctypes.byref(need)))
+    buf = ctypes.create_string_buffer(need.value + 1)
+    _check(lib.iris_config(h, buf, len(buf), None))
+    out = {}
+    for kv in buf.value.decode().split():
+        k, v = kv.split("=", 1)
+        out[k] = v.split(",") if k == "ignored" else v
+    return out
 
 
 _default = None
@@ -565,6 +587,7 @@ class Database:
 
     def close(self):
         if self.handle:
+            self._release_attached()
             load_library().iris_db_destroy(self.handle)
             self.handle = None
 
@@ -580,6 +603,14 @@ class Database:
         except Exception:
             pass
 
+    def _release_attached(self):
+        # every change of the records ends the attachment in the library: the host array is
+        # writable again (if it was before attach_host)
+        a = getattr(self, "_attached", None)
+        if a is not None and getattr(self, "_attached_writable", False):
+            a.setflags(write=True)
+        self._attached = None
+
     def __len__(self):
         n = ctypes.c_uint64()
         _check(load_library().iris_db_len(self.handle, ctypes.byref(n)))
@@ -593,10 +624,12 @@ class Database:
 
     def append(self, records):
         a = _records(self.kind, records)
+        self._release_attached()
         _check(load_library().iris_db_append(self.handle, _ptr(a), a.shape[0]))
 
     def write(self, index, records):
         a = _records(self.kind, records)
+        self._release_attached()
         _check(load_library().iris_db_write(self.handle, int(index), _ptr(a), a.shape[0]))
 
     def read(self, first, n):
@@ -608,21 +641,24 @@ class Database:
     def generate(self, n, seed, global_index0=None):
         """Append n synthetic records; generator index defaults to the DB position."""
         g0 = len(self) if global_index0 is None else global_index0
+        self._release_attached()
         _check(load_library().iris_db_generate(self.handle, int(n), int(seed), int(g0)))
 
     def clear(self):
+        self._release_attached()
         _check(load_library().iris_db_clear(self.handle))
-        self._attached = None
 
     def truncate(self, n):
+        if int(n) != len(self):
+            self._release_attached()
         _check(load_library().iris_db_truncate(self.handle, int(n)))
-        self._attached = None
 
     def load_file(self, path, first=0, count=None):
         """Appends records [first, first+count) of a raw record file (.masks / .share-i /
         raw templates; src/main.rs:386-400,455-469).  Returns the number appended."""
         got = ctypes.c_uint64(0)
         cnt = (1 << 64) - 1 if count is None else int(count)
+        self._release_attached()
         _check(load_library().iris_db_load_file(self.handle, os.fsencode(path), int(first), cnt,
                                                 ctypes.byref(got)))
         return got.value
@@ -638,17 +674,24 @@ class Database:
         memory-mapped record file, src/main.rs:389-391,458-460): upload=True fills the (empty)
         database from it; upload=False checks it already holds them.  Engine batch_process
         calls on slices (numpy views) of `host` then run on the device copy without an
-        upload.  Keeps a reference to `host` while attached."""
+        upload.  Keeps a reference to `host` while attached and makes that array read-only
+        until the attachment ends (detach_host, or any write to the database): the device copy
+        would not see a change (other views of the same memory are not locked -- the rows must
+        stay unchanged while attached, as include/iris_hip.h says)."""
         a = host if isinstance(host, np.ndarray) else np.asarray(host)
         dt, width = _REC_DTYPE[self.kind]
         if a.dtype != dt or a.ndim != 2 or a.shape[1] != width or not a.flags["C_CONTIGUOUS"]:
             raise IrisError(-1, f"host must be a C-contiguous [n, {width}] {np.dtype(dt).name} array")
+        self._release_attached()
         _check(load_library().iris_db_attach_host(self.handle, _ptr(a), a.shape[0], 1 if upload else 0))
         self._attached = a
+        self._attached_writable = bool(a.flags.writeable)
+        if self._attached_writable:
+            a.setflags(write=False)
 
     def detach_host(self):
         _check(load_library().iris_db_detach_host(self.handle))
-        self._attached = None
+        self._release_attached()
 
 
 # ====================================================================== engines
@@ -906,6 +949,10 @@ class Group:
         _check(load_library().iris_group_create_rank(int(ordinal), int(nranks), int(rank), buf, ctypes.byref(h)))
         return cls(_handle=h)
 
+    def set_timeout(self, ms):
+        """Bound (ms) of the exchange waits of later calls; 0 = automatic (iris_group_set_timeout)."""
+        _check(load_library().iris_group_set_timeout(self.handle, int(ms)))
+
     def close(self):
         if getattr(self, "handle", None):
             load_library().iris_group_destroy(self.handle)
@@ -1144,6 +1191,6 @@ __all__ = [
     "DistanceEngine", "TemplateEngine", "TemplateBatchEngine", "Device", "Database", "Match", "merge_matches", "dot_bool", "dot_u16",
     "Group", "GroupDatabase", "GroupPendingSearch",
     "dot_bool_batch", "dot_u16_batch", "IrisError", "load_library", "KIND_MASKS", "KIND_SHARES", "KIND_TEMPLATES",
-    "LAYOUT_DEFAULT", "LAYOUT_LANES", "LAYOUT_TILES",
+    "LAYOUT_DEFAULT", "LAYOUT_LANES", "LAYOUT_TILES", "config",
     "ROTATIONS", "BITS", "LIMBS", "COLS", "ROWS",
 ]

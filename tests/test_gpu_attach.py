@@ -112,11 +112,13 @@ def launches(dev, name):
 
 @pytest.mark.parametrize("kind", [ih.KIND_MASKS, ih.KIND_SHARES])
 @pytest.mark.parametrize("readahead", ["1", "0"])
-def test_attached_chunk_walk_readahead(device, monkeypatch, kind, readahead):
+def test_attached_chunk_walk_readahead(device, hooked_device, kind, readahead):
     """The reference's loop (src/main.rs:427-431, 511-516): consecutive equal chunks of the
     attached file, the last one short.  With readahead every chunk after the first comes from
     the engine's read-ahead rows, computed once: one engine launch per chunk."""
-    monkeypatch.setenv("IRIS_READAHEAD", readahead)
+    if readahead == "0":  # a production knob, read when the device opens
+        device = hooked_device(IRIS_READAHEAD="0")
+        assert device.config()["readahead"] == "0"
     n, chunk = (5003, 1000) if kind == ih.KIND_MASKS else (1301, 300)
     host = oc.gen_masks(SEED + 5, 0, n) if kind == ih.KIND_MASKS else oc.gen_shares(SEED + 5, 0, n)
     qt = oc.gen_templates(SEED + 6, 0, 1)[0]
@@ -160,8 +162,11 @@ def test_readahead_dropped_when_attachment_changes(device):
         out = np.empty((chunk, 31), np.uint16)
         eng.batch_process(out, host[:chunk])  # chunk 1 is now read ahead from the old contents
         assert (out == oc.masks_batch(q, host[:chunk])).all()
+        with pytest.raises(ValueError):  # read-only while attached (the device copy would not see it)
+            host[0, 0] = 1
+        db.detach_host()
         host[:] = new
-        db.write(0, host)  # detaches
+        db.write(0, host)
         db.attach_host(host, upload=False)  # same address, new attachment
         eng.batch_process(out, host[chunk:2 * chunk])
         assert (out == oc.masks_batch(q, new[chunk:2 * chunk])).all()

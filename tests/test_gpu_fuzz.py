@@ -28,10 +28,10 @@ def bits_eq(a, b):
 
 
 @pytest.mark.parametrize("tiles_per_wave", ["auto", "1", "4"])
-def test_fuzz_templates(device, monkeypatch, tiles_per_wave):
+def test_fuzz_templates(device, hooked_device, tiles_per_wave):
     # small ranges run one tile per wave by default; "4" pins the large-range variant
     if tiles_per_wave != "auto":
-        monkeypatch.setenv("IRIS_TILES_PER_WAVE", tiles_per_wave)
+        device = hooked_device(IRIS_TILES_PER_WAVE=tiles_per_wave)
     recs = oc.gen_templates(101, 0, 700)
     for i, (total, first, n, layout) in enumerate(_draws(1, 700)):
         q = recs[(i * 37) % total].copy()
@@ -51,11 +51,11 @@ def test_fuzz_templates(device, monkeypatch, tiles_per_wave):
 
 
 @pytest.mark.parametrize("tiles_per_wave", ["auto", "1", "4"])
-def test_fuzz_masks_and_shares(device, monkeypatch, tiles_per_wave):
+def test_fuzz_masks_and_shares(device, hooked_device, tiles_per_wave):
     # small ranges run one tile per wave (shares: split over K-slices) by default; "1" pins
     # one tile per wave without the K-split, "4" the large-range variants
     if tiles_per_wave != "auto":
-        monkeypatch.setenv("IRIS_TILES_PER_WAVE", tiles_per_wave)
+        device = hooked_device(IRIS_TILES_PER_WAVE=tiles_per_wave)
     masks = oc.gen_templates(102, 0, 600)[:, 200:].copy()
     shares = np.random.default_rng(103).integers(0, 2**16, (300, 12800), dtype=np.uint16)
     for i, (total, first, n, layout) in enumerate(_draws(2, 300)):
@@ -80,18 +80,21 @@ def test_fuzz_masks_and_shares(device, monkeypatch, tiles_per_wave):
                 assert m.index == 2**64 - 1
 
 
-def test_fused_reduce_equals_reduce_kernel(device, monkeypatch):
+def test_fused_reduce_equals_reduce_kernel(device, hooked_device):
     """Small searches finish in the kernel (its last workgroup folds the partials, published
     with system-scope atomics across the XCDs): 300 random queries over ranges up to the
-    fused limit (4096 workgroups) must equal the separate reduce kernel and the oracle."""
+    fused limit (4096 workgroups) must equal the separate reduce kernel (a device opened with
+    IRIS_FUSED_REDUCE=0, holding the same records) and the oracle."""
     import iris_hip as ih
     from oracle import oracle_c as oc
 
     n = 140_000
     rng = np.random.default_rng(12)
     ref = oc.gen_templates(5, 0, n)
-    with ih.Database(device, ih.KIND_TEMPLATES, n) as db:
+    unfused = hooked_device(IRIS_FUSED_REDUCE="0")
+    with ih.Database(device, ih.KIND_TEMPLATES, n) as db, ih.Database(unfused, ih.KIND_TEMPLATES, n) as udb:
         db.generate(n, 5)
+        udb.generate(n, 5)
         for it in range(300):
             q = oc.gen_templates(1000 + it, 0, 1)[0]
             first = int(rng.integers(0, n - 1))
@@ -101,12 +104,11 @@ def test_fused_reduce_equals_reduce_kernel(device, monkeypatch):
                 p = ih.Bits(q[:200]).rotated(int(rng.integers(-15, 16))).limbs
                 m = ih.Bits(q[200:]).rotated(0).limbs
                 db.write(site, np.concatenate([p, m])[None, :])
+                udb.write(site, np.concatenate([p, m])[None, :])
                 ref[site] = np.concatenate([p, m])
-            with ih.TemplateEngine(device, q) as eng:
-                monkeypatch.setenv("IRIS_FUSED_REDUCE", "1")
+            with ih.TemplateEngine(device, q) as eng, ih.TemplateEngine(unfused, q) as ueng:
                 a = eng.search(db, first, cnt, index_base=7)
-                monkeypatch.setenv("IRIS_FUSED_REDUCE", "0")
-                b = eng.search(db, first, cnt, index_base=7)
+                b = ueng.search(udb, first, cnt, index_base=7)
             assert (a.index, a.num, a.den, a.rotation) == (b.index, b.num, b.den, b.rotation), (it, a, b)
             if it % 25 == 0:
                 best, idx = oc.argmin(oc.template_distances(q, ref[first:first + cnt]))

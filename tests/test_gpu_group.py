@@ -39,6 +39,32 @@ def group():
         yield g
 
 
+@pytest.fixture
+def hooked_group(monkeypatch):
+    """hooked_group(IRIS_X="v", ...): a one-device group whose device read the test hooks
+    when it opened (IRIS_TEST_HOOKS=1 just for the open, like conftest.hooked_device)."""
+    groups = []
+
+    def open_(**env):
+        with monkeypatch.context() as m:
+            m.setenv("IRIS_TEST_HOOKS", "1")
+            for k, v in env.items():
+                m.setenv(k, str(v))
+            g = ih.Group([0])
+        groups.append(g)
+        assert g.devices[0].config()["test_hooks"] == "1"
+        return g
+
+    yield open_
+    for g in groups:
+        g.close()
+
+
+# IRIS_GROUP_DELAY_US: the side stream spins this long before every all-gather (a slow peer), so a
+# later search's kernels run while an earlier search's winners still wait to be sent
+DELAY_US = 3000
+
+
 @pytest.mark.parametrize("spd", [1, 3, 8])
 def test_group_search_equals_single_device_and_oracle(group, device, spd):
     n = 5003
@@ -103,22 +129,43 @@ def test_group_empty_shards_and_tiny_db(group):
         assert gdb.search(query).index == 2**64 - 1
 
 
-def test_group_async_out_of_order(group):
-    n, spd = 20000, 2
-    ref = oc.gen_templates(SEED, 0, n)
-    qs = oc.gen_templates(SEED + 10, 0, 5)
-    with ih.GroupDatabase(group, ih.KIND_TEMPLATES, n, shards_per_device=spd) as gdb:
+def async_out_of_order(g, nq=9):
+    """nq pipelined searches over 2 small shards (the fused kernel writes each shard's winner
+    into the exchange buffer itself), waited out of order: -> (got, want index)."""
+    n, spd = 40000, 2
+    qs = oc.gen_templates(SEED + 10, 0, nq)
+    with ih.GroupDatabase(g, ih.KIND_TEMPLATES, n, shards_per_device=spd) as gdb:
         gdb.generate(SEED)
         for k, q in enumerate(qs):
-            gdb.write(1000 + 3700 * k, planted(q, k - 2, 0x3)[None, :])
+            gdb.write(1000 + 4100 * k, planted(q, (k % 5) - 2, 0x3)[None, :])
         ref = gdb.read(0, n)
         pend = [gdb.search_async(q) for q in qs]
-        got = [None] * len(qs)
-        for k in (3, 0, 4, 1, 2):
+        got = [None] * nq
+        for k in list(range(3, nq)) + [0, 2, 1]:
             got[k] = pend[k].wait()
-        for k, q in enumerate(qs):
-            best, idx = oracle_best(q, ref)
-            assert same(got[k], best, idx) and idx == 1000 + 3700 * k
+    want = [oracle_best(q, ref) for q in qs]
+    return got, want
+
+
+@pytest.mark.parametrize("side", ["plain", "delayed"])
+def test_group_async_out_of_order(group, hooked_group, side):
+    """Pipelined searches, waited out of order; "delayed": every all-gather is held back by the
+    IRIS_GROUP_DELAY_US hook, so searches k + 4, k + 8 (the send-slot ring) run their kernels
+    before search k's winners are sent -- each must still get its own answer."""
+    g = group if side == "plain" else hooked_group(IRIS_GROUP_DELAY_US=DELAY_US)
+    got, want = async_out_of_order(g)
+    for k, (best, idx) in enumerate(want):
+        assert same(got[k], best, idx) and idx == 1000 + 4100 * k, (k, got[k], idx)
+
+
+def test_group_delay_hook_reaches_the_race_window(hooked_group):
+    """The same run with the exchange-buffer ordering dropped (IRIS_GROUP_UNORDERED, test-only):
+    later searches overwrite the winners of earlier ones before they are sent, so some answers
+    are wrong -- the delayed test above exercises the write-after-read hazard it guards."""
+    g = hooked_group(IRIS_GROUP_DELAY_US=DELAY_US, IRIS_GROUP_UNORDERED=1)
+    got, want = async_out_of_order(g)
+    wrong = [k for k, (best, idx) in enumerate(want) if not same(got[k], best, idx)]
+    assert wrong, "the delayed all-gathers never met a reused send slot"
 
 
 @pytest.mark.parametrize("layout", [ih.LAYOUT_LANES])
@@ -202,7 +249,8 @@ def test_group_single_rank_communicator():
             assert same(gdb.search(query), best, idx) and idx == 1234
 
 
-def test_group_configs4_shape_on_one_gpu(group, device):
+@pytest.mark.parametrize("side", ["plain", "delayed"])
+def test_group_configs4_shape_on_one_gpu(group, hooked_group, device, side):
     """configs[4]'s shape rehearsed on the one GPU: 8 logical shards as 8 GPUs would hold them
     (10M templates, so that the single-device copy for the comparison fits beside it), an exact
     tie between the last record of shard 0 and a record of the last shard (the lower global
@@ -210,6 +258,8 @@ def test_group_configs4_shape_on_one_gpu(group, device):
     boundary, searched pipelined through the group and compared with the single-device search
     of the same records."""
     n, spd = 10_000_000, 8
+    if side == "delayed":  # every all-gather held back: the next searches' kernels run before it
+        group = hooked_group(IRIS_GROUP_DELAY_US=DELAY_US)
     query = oc.gen_templates(SEED + 40, 0, 1)[0]
     with ih.GroupDatabase(group, ih.KIND_TEMPLATES, n, shards_per_device=spd) as gdb, \
             ih.Database(device, ih.KIND_TEMPLATES, n) as db:
@@ -235,3 +285,46 @@ def test_group_configs4_shape_on_one_gpu(group, device):
                 s1 = eng.search(db)
             assert (g.index, g.num, g.den, g.rotation) == (s1.index, s1.num, s1.den, s1.rotation), (k, g, s1)
             assert g.index == sites[k]
+
+
+@pytest.mark.parametrize("form", ["search", "async", "batch"])
+def test_group_lost_peer_is_an_error_not_a_hang(hooked_group, form):
+    """IRIS_GROUP_STALL holds every all-gather back as a peer that never arrives would: the
+    wait must give up after the group's bound, abort the communicator and fail; the group
+    then refuses further calls, and destroying the database and the group returns."""
+    import time
+
+    g = hooked_group(IRIS_GROUP_STALL=1)
+    g.set_timeout(700)
+    n = 5000
+    query = oc.gen_templates(SEED + 60, 0, 1)[0]
+    gdb = ih.GroupDatabase(g, ih.KIND_TEMPLATES, n, shards_per_device=2)
+    gdb.generate(SEED)
+    t0 = time.monotonic()
+    with pytest.raises(ih.IrisError) as ei:
+        if form == "search":
+            gdb.search(query)
+        elif form == "async":
+            gdb.search_async(query).wait()
+        else:
+            gdb.batch_search(oc.gen_templates(SEED + 61, 0, 9))
+    assert time.monotonic() - t0 < 20, "the bound did not end the wait"
+    assert "aborted" in str(ei.value) and "700 ms" in str(ei.value)
+    with pytest.raises(ih.IrisError) as ei2:  # the group is broken from now on
+        gdb.search(query)
+    assert "aborted" in str(ei2.value)
+    with pytest.raises(ih.IrisError):
+        ih.GroupDatabase(g, ih.KIND_TEMPLATES, 10)
+    gdb.close()
+    g.close()
+
+
+def test_group_finalizes_and_reforms(group):
+    """A healthy group tears down through ncclCommFinalize + ncclCommDestroy; a new group on
+    the same device then works (the communicator was released)."""
+    query = oc.gen_templates(SEED + 70, 0, 1)[0]
+    for _ in range(3):
+        with ih.Group([0]) as g, ih.GroupDatabase(g, ih.KIND_TEMPLATES, 3000, shards_per_device=2) as gdb:
+            gdb.generate(SEED)
+            best, idx = oracle_best(query, gdb.read(0, 3000))
+            assert same(gdb.search(query), best, idx)

@@ -65,17 +65,17 @@ def test_capacity_checked(device, tmp_path):
 
 
 @pytest.fixture(params=["mmap", "pread"])
-def load_path(request, monkeypatch):
+def load_device(request, device, hooked_device):
     """The loader's two paths: DMA from the registered page-cache mapping (default)
-    and pread into pinned buffers (the fallback, pinned by IRIS_LOAD_PREAD)."""
-    if request.param == "pread":
-        monkeypatch.setenv("IRIS_LOAD_PREAD", "1")
-    return request.param
+    and pread into pinned buffers (the fallback: a device opened with the IRIS_LOAD_PREAD
+    test hook)."""
+    return hooked_device(IRIS_LOAD_PREAD="1") if request.param == "pread" else device
 
 
-def test_multi_chunk_unaligned_templates(device, tmp_path, load_path):
+def test_multi_chunk_unaligned_templates(load_device, tmp_path):
     """A 96-MB template file loaded from an unaligned first record: a short leading chunk up
     to a page-aligned record boundary, then full chunks, then a ragged last one."""
+    device = load_device
     n, first = 30_000, 13
     recs = oc.gen_templates(91, 0, n)
     path = tmp_path / "t.bin"
@@ -85,9 +85,10 @@ def test_multi_chunk_unaligned_templates(device, tmp_path, load_path):
         assert (db.read(0, n - first) == recs[first:]).all()
 
 
-def test_multi_chunk_masks_file(device, tmp_path, load_path):
+def test_multi_chunk_masks_file(load_device, tmp_path):
     """50 000 masks = 80 MB: more than one 64 MB pinned buffer, so the double
     buffering and chunk offsets are exercised; then the engine runs on it."""
+    device = load_device
     n = 50_000
     recs = oc.gen_templates(77, 0, n)[:, 200:].copy()
     path = tmp_path / "big.masks"

@@ -602,11 +602,11 @@ def test_batch_search_matches_single(device, nq):
 
 @pytest.mark.parametrize("tiles_per_wave", ["auto", "4"])
 @pytest.mark.parametrize("first,n", [(0, 3000), (37, 1000), (64, 64), (5, 1)])
-def test_resolver_masks_fused(device, layout, first, n, monkeypatch, tiles_per_wave):
-    if tiles_per_wave != "auto":  # pin the large-range variant on these small ranges
-        monkeypatch.setenv("IRIS_TILES_PER_WAVE", tiles_per_wave)
+def test_resolver_masks_fused(device, hooked_device, layout, first, n, tiles_per_wave):
     """MasksEngine.resolve == MasksEngine.batch_process + resolver_search == oracle, on
     random participant outputs (ties, den = 0 rows) and a planted near-copy."""
+    if tiles_per_wave != "auto":  # pin the large-range variant on these small ranges
+        device = hooked_device(IRIS_TILES_PER_WAVE=tiles_per_wave)
     total = 3100
     masks = oc.gen_templates(61, 0, total)[:, 200:].copy()
     q = masks[first + n // 2].copy()

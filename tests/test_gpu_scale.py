@@ -60,11 +60,12 @@ def check_all(got, queries, recs, base=0):
 
 
 @pytest.mark.parametrize("kernel", ["2", "3", "4", "1"], ids=["batch_lds_kernel", "batch_lds_2x2", "batch_lds_q2", "batch_kernel"])
-def test_batch_1024_queries_vs_oracle(device, kernel, monkeypatch):
+def test_batch_1024_queries_vs_oracle(device, hooked_device, kernel):
     """Q = 1024 (256 query groups) over 4099 templates and a ragged sub-range: every query's
-    distance bits, index, winning fraction and rotation equal the oracle's (both batched
-    kernels: IRIS_BATCH_KERNEL)."""
-    monkeypatch.setenv("IRIS_BATCH_KERNEL", kernel)
+    distance bits, index, winning fraction and rotation equal the oracle's (every batched
+    kernel: the IRIS_BATCH_KERNEL test hook; 4 is the default)."""
+    if kernel != "4":
+        device = hooked_device(IRIS_BATCH_KERNEL=kernel)
     n, nq = 4099, 1024
     recs = oc.gen_templates(811, 0, n)
     queries = oc.gen_templates(812, 0, nq)
@@ -89,11 +90,12 @@ def test_batch_1024_queries_vs_oracle(device, kernel, monkeypatch):
 
 @pytest.mark.parametrize("kernel", ["2", "3", "4", "1"], ids=["batch_lds_kernel", "batch_lds_2x2", "batch_lds_q2", "batch_kernel"])
 @pytest.mark.parametrize("nq", [64, 1024])
-def test_batch_many_groups_200k(device, nq, kernel, monkeypatch):
+def test_batch_many_groups_200k(device, hooked_device, nq, kernel):
     """Q = 64 and 1024 over 200 003 templates (6252 tiles: many N-groups per workgroup and a
     ragged last tile): every query against the oracle (Q = 64) or, for Q = 1024, every query
     against the single-query search and 48 of them against the oracle."""
-    monkeypatch.setenv("IRIS_BATCH_KERNEL", kernel)
+    if kernel != "4":
+        device = hooked_device(IRIS_BATCH_KERNEL=kernel)
     n = 200_003
     recs = oc.gen_templates(913, 0, n)
     queries = oc.gen_templates(914, 0, nq)
