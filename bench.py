@@ -474,6 +474,14 @@ class Ranks:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
 
+    def gather_lists(self, xs):
+        """Every rank's list of floats, concatenated in rank order (the same on every rank)."""
+        if self.dist is None:
+            return list(xs)
+        out = [None] * self.dist.get_world_size()
+        self.dist.all_gather_object(out, [float(x) for x in xs])
+        return [x for part in out for x in part]
+
     def close(self):
         if self.group is not None:
             self.group.close()
@@ -497,7 +505,9 @@ def dry_run(args, ranks):
     local = ih.Match(0.25, ranks.rank * n + 7, 10, 40, -3, 0)
     merged = iris_dist.allgather_merge(local) if ranks.dist is not None else local
     elapsed = ranks.max_over_ranks(time.perf_counter() - t0)
-    ok = merged.index == 7 and merged.distance == 0.25
+    # the per-rank gather the real line uses for every GPU's kernel time (kernel.per_rank_kernel_ms)
+    gathered = [int(x) for x in ranks.gather_lists([ranks.rank])]
+    ok = merged.index == 7 and merged.distance == 0.25 and gathered == list(range(ranks.world))
     if ranks.rank == 0:
         print(json.dumps({"metric": METRIC, "value": None, "unit": "template comparisons/s", "n_gpus": ranks.world,
                           "ranks_seen": ranks.world, "backend": ranks.backend, "launcher": launcher_name(),
@@ -505,7 +515,8 @@ def dry_run(args, ranks):
                           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": None,
                           "data": "none (dry run)",
                           "config": {"workload": "launcher rehearsal", "templates_per_gpu": n},
-                          "check": {"merged_index": int(merged.index), "ok": bool(ok)}}))
+                          "check": {"merged_index": int(merged.index), "gathered_ranks": gathered,
+                                    "ok": bool(ok)}}))
     ranks.close()
     if not ok:
         sys.exit(3)
@@ -1022,11 +1033,15 @@ def main():
     launches = sum(s[0] for s in stats)
     kms = sum(s[1] for s in stats)
     rms = sum(d.kernel_stats("reduce")[1] for d in devs)
-    avg_ms = kms / max(1, launches)
     per_dev_ms = [s[1] / max(1, s[0]) for s in stats]
+    # every GPU's average kernel time, in rank order (torchrun ranks gather theirs; a single
+    # process holds all of its devices'): the roofline is the SLOWEST GPU's, which sets the step
+    per_gpu_ms = ranks.gather_lists(per_dev_ms)
+    per_gpu_step_ms = ranks.gather_lists([s[1] / max(1, args.steps) for s in stats])
+    avg_ms = max(per_gpu_ms) if per_gpu_ms else kms / max(1, launches)
     n_launch = total // world_gpus  # records per launch (one shard per device)
-    # kernel time of one step on one device (a batch of 1-3 queries streams: several launches per step)
-    step_kernel_ms = kms / max(1, len(devs)) / max(1, args.steps)
+    # kernel time of one step on the slowest device (a batch of 1-3 queries streams: several launches per step)
+    step_kernel_ms = max(per_gpu_step_ms) if per_gpu_step_ms else kms / max(1, len(devs)) / max(1, args.steps)
     achieved = rec_bytes * n_launch / (avg_ms * 1e-3) / 1e9
     # batch: HBM bytes of the 1024-query launch (the DB once per XCD-shared pass + query tiles)
     traffic, traffic_src = (load_traffic(args.workload, n_launch, args.layout)
@@ -1098,7 +1113,11 @@ def main():
                          ("shares", "tiles"): "shares_mfma_kernel (i8 MFMA)",
                          ("shares", "lanes"): "shares_kernel (VALU v_pk_mad_u16)",
                          ("batch", "tiles"): "batch_lds_kernel<8,2,2,2> (fp4 MFMA GEMM: 2-query groups x 16-tile N-groups, 2 x 2 per wave, LDS query-fragment ring)"}[(args.workload, args.layout)],
-                "avg_ms": avg_ms, "launches": launches, "per_device_avg_ms": per_dev_ms,
+                "avg_ms": avg_ms, "avg_ms_is": "the slowest GPU's average (it sets the step)",
+                "launches": launches, "per_device_avg_ms": per_dev_ms,
+                "per_rank_kernel_ms": per_gpu_ms,
+                "kernel_ms_min": min(per_gpu_ms) if per_gpu_ms else None,
+                "kernel_ms_max": max(per_gpu_ms) if per_gpu_ms else None,
                 "reduce_avg_ms": rms / max(1, launches),
                 "frac_of_guide_copy_bw": achieved / HBM_GUIDE_COPY_GBS,
                 "frac_of_read_ceiling": achieved / HBM_READ_CEILING_GBS,

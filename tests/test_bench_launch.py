@@ -40,6 +40,7 @@ def test_self_launch_dry_run(n):
     assert d["n_gpus"] == n and d["ranks_seen"] == n and d["backend"] == "gloo"
     assert d["launcher"].startswith("bench.py") and d["dry_run"] and d["check"]["ok"]
     assert d["check"]["merged_index"] == 7  # equal distances: the lowest global index (rank 0) wins
+    assert d["check"]["gathered_ranks"] == list(range(n))  # every rank's entry, in rank order
 
 
 def test_too_many_rccl_ranks_fail_loudly():

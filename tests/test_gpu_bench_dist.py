@@ -60,6 +60,9 @@ def test_bench_eight_ranks_one_gpu():
     assert d["n_gpus"] == 8 and d["ranks_seen"] == 8 and d["backend"] == "gloo" and d["check"]["ok"]
     assert d["config"]["total_templates"] == 1_600_000
     assert d["check"]["planted_index"] >= 200000
+    k = d["kernel"]  # every rank's kernel time; the roofline is the slowest one's
+    assert len(k["per_rank_kernel_ms"]) == 8 and k["kernel_ms_max"] == max(k["per_rank_kernel_ms"])
+    assert k["avg_ms"] == k["kernel_ms_max"] and k["kernel_ms_min"] <= k["kernel_ms_max"]
 
 
 def test_bench_self_launch_two_ranks():
