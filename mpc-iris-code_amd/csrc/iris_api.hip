@@ -76,19 +76,23 @@ int range_ok(const iris_db *db, uint64_t first, uint64_t n) {
 constexpr uint64_t kU16Chunk = 4ull << 20;  // records per engine launch of the host-output forms
 
 // Enqueues the engine kernel over [first, first+n) of db, [n][31] u16 rows to the device buffer
-// o, on `stream` (default: the device stream); nothing waits.
+// o, on `stream` (default: the device stream); nothing waits.  sig (TILES only): the kernel's
+// completion word, if the kernel chosen signals one (sig->armed).
 int enqueue_u16_engine(iris_engine *e, const iris_db *db, uint64_t first, uint64_t n, uint16_t *o,
-                       hipStream_t stream = nullptr) {
+                       hipStream_t stream = nullptr, DoneSignal *sig = nullptr) {
     iris_device *d = e->dev;
     if (!stream) stream = d->stream;
     LaunchRange r{first, n};
     const bool tiles = db->k.layout == IRIS_LAYOUT_TILES;
+    if (sig) sig->armed = false;
     if (e->kind == IRIS_KIND_MASKS)
         return timed(d, "masks", n, [&] {
-            return tiles ? launch_masks_mfma(d->hooks, stream, db->data, e->qfrag, r, o) : launch_masks(stream, db->data, e->qtab, r, o);
+            return tiles ? launch_masks_mfma(d->hooks, stream, db->data, e->qfrag, r, o, sig)
+                         : launch_masks(stream, db->data, e->qtab, r, o);
         }, stream);
     return timed(d, "shares", n, [&] {
-        return tiles ? launch_shares_mfma(d->hooks, stream, db->data, e->qfrag, r, o) : launch_shares(stream, db->data, e->qtab, r, o);
+        return tiles ? launch_shares_mfma(d->hooks, stream, db->data, e->qfrag, r, o, sig)
+                     : launch_shares(stream, db->data, e->qtab, r, o);
     }, stream);
 }
 
@@ -860,8 +864,26 @@ int iris_engine_batch_process_device(iris_engine_t *e, const iris_db_t *db, uint
     CHK(range_ok(db, first, n));
     if (n == 0) return 0;
     ARG(out_device, "out is NULL");
-    CHK(enqueue_u16_engine(e, db, first, n, out_device));
-    return sync(d);
+    // a participant-sized range: the kernel's last workgroup publishes a sequence word in coherent
+    // host memory once every row is stored, and the call returns when it lands (as the small
+    // search does) -- later work on the device stream, the rows' consumers, follows the kernel
+    DoneSignal sig{};
+#ifndef IRIS_DEVICE_OUT_DONE  // 0: wait for the stream instead (A/B builds)
+#define IRIS_DEVICE_OUT_DONE 1
+#endif
+    if (IRIS_DEVICE_OUT_DONE && db->k.layout == IRIS_LAYOUT_TILES) {
+        CHK(ensure_ticket(d));
+        CHK(ensure_host_done(d));
+        sig.ticket = (uint32_t *)d->ticket.p;
+        sig.done = d->host_done;
+        sig.seq = ++d->done_seq;
+        if (sig.seq == 0) sig.seq = ++d->done_seq;  // 0 is the word's initial value
+    }
+    CHK(enqueue_u16_engine(e, db, first, n, out_device, nullptr, sig.done ? &sig : nullptr));
+    if (!sig.armed) return sync(d);
+    CHK(wait_done(d, sig.seq));
+    if (d->profiling) fold_done(d);
+    return 0;
 }
 
 int iris_engine_batch_process_host(iris_engine_t *e, const void *records, uint64_t n, uint16_t *out) {

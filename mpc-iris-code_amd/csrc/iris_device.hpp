@@ -254,4 +254,19 @@ __device__ __forceinline__ void fold_partials_last(Partial *partials, const Part
     }
 }
 
+// Completion word of a blocking device-output call (DoneSignal): called by ONE thread of each
+// workgroup once that workgroup's stores have completed (its waves waited for vmcnt(0)); the
+// last workgroup to arrive (the two-level ticket of fold_partials_last) resets the ticket and
+// stores the sequence number into the coherent host word the caller spins on.
+__device__ __forceinline__ void signal_done_last(const DoneSignal &s) {
+    const uint32_t c = blockIdx.x % kTicketGroups, groups = gridDim.x < kTicketGroups ? gridDim.x : kTicketGroups;
+    const uint32_t members = (gridDim.x - c + kTicketGroups - 1) / kTicketGroups;
+    uint32_t *sub = s.ticket + kTicketStride * (1 + c);
+    if (__hip_atomic_fetch_add(sub, 1u, __ATOMIC_RELAXED, IRIS_FUSED_SCOPE) != members - 1) return;
+    __hip_atomic_store(sub, 0u, __ATOMIC_RELAXED, IRIS_FUSED_SCOPE);  // for the next launch
+    if (__hip_atomic_fetch_add(s.ticket, 1u, __ATOMIC_RELAXED, IRIS_FUSED_SCOPE) != groups - 1) return;
+    __hip_atomic_store(s.ticket, 0u, __ATOMIC_RELAXED, IRIS_FUSED_SCOPE);
+    __hip_atomic_store(s.done, s.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 }  // namespace iris

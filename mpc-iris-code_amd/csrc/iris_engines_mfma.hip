@@ -28,20 +28,39 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kTile = 32;
 #ifndef IRIS_MASKS_T
-#define IRIS_MASKS_T 8
+#define IRIS_MASKS_T 7
 #endif
 #ifndef IRIS_MASKS_BPC
 #define IRIS_MASKS_BPC 2
 #endif
-// tiles per wave: 8 for the [u16;31] output (longer groups, fewer store bursts:
-// 2.88-2.98 vs 2.98-3.03 ms per 10M in interleaved runs on two boxes, ~2 %; the first
-// run after a pause is ~7 % faster for either, the GPU is still cool); the fused resolver
-// keeps 4 (its epilogue state at 8 tiles costs registers: 5.1 vs 2.7 ms)
+// tiles per wave: 7 for the [u16;31] output (longer groups, fewer store bursts than 4:
+// round 2 measured 8 at 2.88-2.98 vs 2.98-3.03 ms per 10M for 4; but 8 tiles need 29 VGPRs
+// of scratch spills at two waves per SIMD, and 7 -- 252 VGPRs, none spilled -- runs 2.894-2.896
+// vs 2.916-2.919 ms for 8, 2.894-2.900 for 6, 2.910-2.912 for 5, interleaved on one box,
+// profiles/r04d_masks_tiles.txt); the fused resolver keeps 4 (its epilogue state at 8 tiles
+// costs registers: 5.1 vs 2.7 ms)
 constexpr int kMasksTiles = IRIS_MASKS_T;
 constexpr int kResolveTiles = 4;
 template <int MODE>
 constexpr int masks_tiles() { return MODE == 0 ? kMasksTiles : kResolveTiles; }
 constexpr int kMasksBlocksPerCu = IRIS_MASKS_BPC;  // persistent grid: workgroups per CU
+// 1: the compact query (51 KB) is staged in LDS per workgroup; 0: read from L2 by every wave
+// (no LDS for it, so three workgroups fit a CU)
+#ifndef IRIS_MASKS_QLDS
+#define IRIS_MASKS_QLDS 1
+#endif
+// The fused resolver (4 tiles per wave, 168 VGPRs) runs three workgroups per CU with the query
+// read from L2: 2.78 vs 2.87 ms per 10M masks + 3 x 10M share rows, interleaved on one box
+// (profiles/r04c_masks_ab.txt); for the [u16;31] output the same shape measured even (2.90-3.01
+// vs 2.93-3.00 ms), so MasksEngine keeps 8 tiles per wave at two workgroups per CU.
+#ifndef IRIS_RESOLVE_BPC
+#define IRIS_RESOLVE_BPC 3
+#endif
+#ifndef IRIS_RESOLVE_QLDS
+#define IRIS_RESOLVE_QLDS 0
+#endif
+template <int MODE>
+constexpr int masks_blocks_per_cu() { return MODE == 0 ? kMasksBlocksPerCu : IRIS_RESOLVE_BPC; }
 constexpr int kSharesTiles = 2;
 
 __device__ __forceinline__ uint4 nt_load(const uint4 *p) {
@@ -112,14 +131,18 @@ enum { MASKS_OUT = 0, MASKS_RESOLVE = 1 };
 // and a running (fraction, lowest index) best per lane becomes one partial per
 // workgroup — the denominators never reach memory.
 template <int MODE, int T = masks_tiles<MODE>()>
-__global__ void __launch_bounds__(256, kMasksBlocksPerCu)
+__global__ void __launch_bounds__(256, masks_blocks_per_cu<MODE>())
     masks_mfma_kernel(const uint4 *__restrict__ db, const uint4 *__restrict__ qfrag, uint64_t tile0, uint64_t ntiles,
                       uint64_t first, uint64_t end, uint16_t *__restrict__ out, MaskResolve rs) {
     constexpr uint32_t kSteps = kMaskChunks / 4;  // 50 steps of 4 chunks
-    __shared__ uint4 sq[kMaskFragUint4];
+    const uint4 *sq = qfrag;  // the query's compact fragments: in LDS, or read from L2
+    if constexpr ((MODE == MASKS_OUT && IRIS_MASKS_QLDS) || (MODE != MASKS_OUT && IRIS_RESOLVE_QLDS)) {
+        __shared__ uint4 sq_lds[kMaskFragUint4];
+        for (int i = threadIdx.x; i < (int)kMaskFragUint4; i += blockDim.x) sq_lds[i] = qfrag[i];
+        __syncthreads();
+        sq = sq_lds;
+    }
     __shared__ __attribute__((aligned(16))) uint16_t sh_out[kWaveSlots][1024];
-    for (int i = threadIdx.x; i < (int)kMaskFragUint4; i += blockDim.x) sq[i] = qfrag[i];
-    __syncthreads();
 
     const int lane = threadIdx.x & 63;
     const uint64_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaveSlots + (threadIdx.x >> 6));
@@ -271,7 +294,7 @@ constexpr uint64_t kMasksSplitTiles = 1024;
 template <int KS>
 __global__ void __launch_bounds__(64 * KS)
     masks_split_kernel(const uint4 *__restrict__ db, const uint4 *__restrict__ qfrag, uint64_t tile0,
-                       uint64_t first, uint64_t end, uint16_t *__restrict__ out) {
+                       uint64_t first, uint64_t end, uint16_t *__restrict__ out, DoneSignal sig) {
     constexpr int kSteps = kMaskChunks / 4;  // 50
     static_assert(kSteps % KS == 0, "K-split geometry");
     constexpr int kG = kSteps / KS;
@@ -309,6 +332,10 @@ __global__ void __launch_bounds__(64 * KS)
         for (int i = 0; i < 16; ++i) acc[i] += red[k][i][lane];
     store_tile_rows(out, sh_out, tile * kTile, first, end, true, lane,
                     [&](int r) { return (uint16_t)(uint32_t)acc[r]; });
+    if (sig.done) {  // wave 0 stored the workgroup's rows: once they are performed, take the ticket
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) signal_done_last(sig);
+    }
 }
 
 // Tiles per wave for a range of `ntiles` tiles: `big`, unless that leaves fewer waves
@@ -320,14 +347,21 @@ static int tiles_per_wave(const Hooks &h, uint64_t ntiles, int big) {
     return ntiles / big < (uint64_t)resident_blocks(2) * kWaveSlots ? 1 : big;
 }
 
-int launch_masks_mfma(const Hooks &h, void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *out) {
+int launch_masks_mfma(const Hooks &h, void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *out,
+                      DoneSignal *sig) {
+    if (sig) sig->armed = false;
     if (r.n == 0) return 0;
     const uint64_t ntiles = tiles_of(r, 1).ntiles;
     // the K-split form for small ranges (IRIS_TILES_PER_WAVE pins the persistent kernel for tests)
     if (ntiles <= kMasksSplitTiles && !h.tiles_per_wave) {
+        DoneSignal s{};
+        if (sig) {
+            s = *sig;
+            sig->armed = true;
+        }
         hipLaunchKernelGGL(masks_split_kernel<kMasksSplitKS>, dim3((uint32_t)ntiles), dim3(64 * kMasksSplitKS), 0,
                            (hipStream_t)stream, (const uint4 *)db, (const uint4 *)qfrag, tiles_of(r, 1).tile0,
-                           r.first, r.first + r.n, out);
+                           r.first, r.first + r.n, out, s);
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
     const int tpw = tiles_per_wave(h, ntiles, kMasksTiles);
@@ -342,7 +376,7 @@ int launch_masks_mfma(const Hooks &h, void *stream, const void *db, const void *
 
 uint32_t masks_resolve_partials(const Hooks &h, LaunchRange r) {
     const Tiles t = tiles_of(r, tiles_per_wave(h, tiles_of(r, 1).ntiles, kResolveTiles));
-    return (uint32_t)std::min<uint64_t>(t.grid, resident_blocks(kMasksBlocksPerCu));
+    return (uint32_t)std::min<uint64_t>(t.grid, resident_blocks(masks_blocks_per_cu<MASKS_RESOLVE>()));
 }
 
 int launch_masks_resolve(const Hooks &h, void *stream, const void *db, const void *qfrag, LaunchRange r,
@@ -483,7 +517,8 @@ constexpr uint64_t kSharesSplitTiles = 4096;
 template <int T, int KS>
 __global__ void __launch_bounds__(64 * KS, 2)
     shares_split_kernel(const uint4 *__restrict__ db, const uint4 *__restrict__ qfrag, const int2 *__restrict__ qsum,
-                        uint64_t tile0, uint64_t ntiles, uint64_t first, uint64_t end, uint16_t *__restrict__ out) {
+                        uint64_t tile0, uint64_t ntiles, uint64_t first, uint64_t end, uint16_t *__restrict__ out,
+                        DoneSignal sig) {
     constexpr int kSteps = kShareChunks / 2 / KS;
     static_assert(kShareChunks % (2 * KS) == 0, "K-split geometry");
     const int lane = threadIdx.x & 63;
@@ -588,6 +623,10 @@ __global__ void __launch_bounds__(64 * KS, 2)
             return (uint16_t)(lo + 256u * cross);
         });
     }
+    if (sig.done) {  // wave 0 stored the workgroup's rows: once they are performed, take the ticket
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) signal_done_last(sig);
+    }
 }
 
 // K-slices for a range (1 = no split): enough one-tile waves to fill the chip, a
@@ -596,15 +635,22 @@ static bool shares_lds_split(const Hooks &h, uint64_t ntiles) {
     return ntiles <= kSharesSplitTiles && !h.tiles_per_wave;
 }
 
-int launch_shares_mfma(const Hooks &h, void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *out) {
+int launch_shares_mfma(const Hooks &h, void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *out,
+                       DoneSignal *sig) {
+    if (sig) sig->armed = false;
     if (r.n == 0) return 0;
     const int2 *qsum = (const int2 *)((const uint4 *)qfrag + kShareFragUint4);
     if (shares_lds_split(h, tiles_of(r, 1).ntiles)) {
         const Tiles t = tiles_of(r, 1);
+        DoneSignal s{};
+        if (sig) {
+            s = *sig;
+            sig->armed = true;
+        }
         hipLaunchKernelGGL((shares_split_kernel<kSharesSplitT, kSharesSplitKS>),
                            dim3((uint32_t)((t.ntiles + kSharesSplitT - 1) / kSharesSplitT)), dim3(64 * kSharesSplitKS), 0,
                            (hipStream_t)stream, (const uint4 *)db, (const uint4 *)qfrag, qsum, t.tile0, t.ntiles, r.first,
-                           r.first + r.n, out);
+                           r.first + r.n, out, s);
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
     const int tpw = tiles_per_wave(h, tiles_of(r, 1).ntiles, kSharesTiles);

@@ -235,7 +235,7 @@ inline int wait_done(iris_device *d, uint32_t seq) {
             const hipError_t q = hipStreamQuery(d->stream);
             if (q == hipSuccess) {
                 if (__atomic_load_n(d->host_done, __ATOMIC_ACQUIRE) == seq) return 0;
-                return fail(IRIS_E_HIP, "search kernel completed without publishing its result");
+                return fail(IRIS_E_HIP, "kernel completed without publishing its completion word");
             }
             if (q != hipErrorNotReady) return fail(IRIS_E_HIP, std::string("hipStreamQuery: ") + hipGetErrorString(q));
         }

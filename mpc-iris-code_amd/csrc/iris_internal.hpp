@@ -261,7 +261,18 @@ int launch_pack_tiles_kind(void *stream, int kind, const void *staging, void *db
 int launch_unpack_tiles_kind(void *stream, int kind, const void *db, void *staging, uint64_t t_first, uint64_t n);
 int launch_generate_tiles_kind(void *stream, int kind, void *db, uint64_t t_first, uint64_t n, uint64_t seed,
                                uint64_t global_index0);
-int launch_masks_mfma(const Hooks &h, void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *out);
+// Completion word of a blocking device-output engine call: the kernel's last workgroup, once
+// every workgroup's rows are stored, stores seq into the coherent host word done (ticket: the
+// device's zeroed 4-KB ticket block, left zeroed).  The launcher sets armed when the kernel it
+// chose signals (the small-range K-split kernels); otherwise the caller waits for the stream.
+struct DoneSignal {
+    uint32_t *ticket;
+    uint32_t *done;
+    uint32_t seq;
+    bool armed;
+};
+int launch_masks_mfma(const Hooks &h, void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *out,
+                      DoneSignal *sig = nullptr);
 uint32_t masks_resolve_partials(const Hooks &h, LaunchRange r);
 int launch_masks_resolve(const Hooks &h, void *stream, const void *db, const void *qfrag, LaunchRange r,
                          const uint16_t *const *shares, uint32_t parts, double *dist_out, Partial *partials);
@@ -278,7 +289,8 @@ int launch_batch(const Hooks &h, void *stream, const void *db, const void *qtile
                  Partial *partials, Partial *out, uint64_t idx_base = 0);
 int launch_resolver(void *stream, const uint16_t *const *shares, uint32_t parts, const uint16_t *denoms, uint64_t n,
                     double *dist_out, Partial *partials);
-int launch_shares_mfma(const Hooks &h, void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *out);
+int launch_shares_mfma(const Hooks &h, void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *out,
+                       DoneSignal *sig = nullptr);
 int launch_template_search(void *stream, const void *db, const void *qtab, LaunchRange r, double *dist_out,
                            Partial *partials, uint32_t *n_partials);
 // consumes partials; the winner's idx (range-relative) is offset by idx_base

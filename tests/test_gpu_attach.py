@@ -285,3 +285,51 @@ def test_fresh_engine_first_call(device, kind):
                 out2 = np.empty((10, 31), np.uint16)
                 eng.batch_process(out2, db, first=a, n=10)
                 assert (out2 == want[a:a + 10]).all(), it
+
+
+@pytest.mark.parametrize("kind", [ih.KIND_MASKS, ih.KIND_SHARES])
+def test_device_output_chunks_return_on_completion_word(device, kind):
+    """Participant-sized device-output calls (iris_engine_batch_process_device) return when the
+    kernel's last workgroup publishes the completion word, not at the stream's end: chunk after
+    chunk into the SAME device buffer (each call's rows overwrite the last one's), each read back
+    at once and compared with the oracle, with a ragged last chunk, a one-record call and the
+    other engine kind interleaved on the same device stream."""
+    if kind == ih.KIND_MASKS:
+        n, chunk = 45_001, 20_000
+        recs = oc.gen_masks(SEED + 20, 0, n)
+        q = oc.gen_masks(SEED + 21, 0, 1)[0]
+        eng, oracle = ih.MasksEngine(device, q), (lambda r: oc.masks_batch(q, r))
+        other_kind, other_recs = ih.KIND_SHARES, oc.gen_shares(SEED + 22, 0, 64)
+        other_q = oc.gen_shares(SEED + 23, 0, 1)[0]
+        other = ih.DistanceEngine(device, other_q)
+        other_want = oc.distance_batch(other_q, other_recs)
+    else:
+        n, chunk = 4_501, 2_000
+        recs = oc.gen_shares(SEED + 24, 0, n)
+        q = oc.gen_shares(SEED + 25, 0, 1)[0]
+        eng, oracle = ih.DistanceEngine(device, q), (lambda r: oc.distance_batch(q, r))
+        other_kind, other_recs = ih.KIND_MASKS, oc.gen_masks(SEED + 26, 0, 64)
+        other_q = oc.gen_masks(SEED + 27, 0, 1)[0]
+        other = ih.MasksEngine(device, other_q)
+        other_want = oc.masks_batch(other_q, other_recs)
+    want = oracle(recs)
+    with eng, other, ih.Database(device, kind, n) as db, ih.Database(device, other_kind, 64) as odb:
+        db.append(recs)
+        odb.append(other_recs)
+        out = device.alloc(chunk * 31 * 2)
+        oout = device.alloc(64 * 31 * 2)
+        try:
+            for walk in range(2):
+                for a in list(range(0, n, chunk)) + [n - 1]:
+                    m = min(chunk, n - a)
+                    eng.batch_process_device(db, out, first=a, n=m)
+                    other.batch_process_device(odb, oout)
+                    rows = np.empty((m, 31), np.uint16)
+                    device.d2h(rows, out)
+                    assert (rows == want[a:a + m]).all(), (walk, a)
+                    orows = np.empty((64, 31), np.uint16)
+                    device.d2h(orows, oout)
+                    assert (orows == other_want).all(), (walk, a)
+        finally:
+            device.free(out)
+            device.free(oout)

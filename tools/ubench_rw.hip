@@ -108,7 +108,7 @@ int main() {
     (void)hipMemset(dst, 0, wbytes);
     (void)hipDeviceSynchronize();
     for (int rep = 0; rep < 2; ++rep)
-        for (int bpc : {2}) {
+        for (int bpc : {2, 3}) {
             run<0>(src, groups, dst, out, bpc);
             run<1>(src, groups, dst, out, bpc);
             run<2>(src, groups, dst, out, bpc);
