@@ -37,7 +37,7 @@ constexpr int kTile = 32;
 // round 2 measured 8 at 2.88-2.98 vs 2.98-3.03 ms per 10M for 4; but 8 tiles need 29 VGPRs
 // of scratch spills at two waves per SIMD, and 7 -- 252 VGPRs, none spilled -- runs 2.894-2.896
 // vs 2.916-2.919 ms for 8, 2.894-2.900 for 6, 2.910-2.912 for 5, interleaved on one box,
-// profiles/r04d_masks_tiles.txt); the fused resolver keeps 4 (its epilogue state at 8 tiles
+// profiles/r04_masks_variants.txt); the fused resolver keeps 4 (its epilogue state at 8 tiles
 // costs registers: 5.1 vs 2.7 ms)
 constexpr int kMasksTiles = IRIS_MASKS_T;
 constexpr int kResolveTiles = 4;
@@ -51,7 +51,7 @@ constexpr int kMasksBlocksPerCu = IRIS_MASKS_BPC;  // persistent grid: workgroup
 #endif
 // The fused resolver (4 tiles per wave, 168 VGPRs) runs three workgroups per CU with the query
 // read from L2: 2.78 vs 2.87 ms per 10M masks + 3 x 10M share rows, interleaved on one box
-// (profiles/r04c_masks_ab.txt); for the [u16;31] output the same shape measured even (2.90-3.01
+// (profiles/r04_masks_variants.txt); for the [u16;31] output the same shape measured even (2.90-3.01
 // vs 2.93-3.00 ms), so MasksEngine keeps 8 tiles per wave at two workgroups per CU.
 #ifndef IRIS_RESOLVE_BPC
 #define IRIS_RESOLVE_BPC 3
