@@ -366,9 +366,14 @@ def batch_pmc():
         j = json.loads(p.read_text())
     except Exception:
         return None
-    return {"valu_per_mfma": j["valu_per_mfma_incl_mfma"], "valu_per_mfma_excl_mfma": j["valu_per_mfma_excl_mfma"],
-            "lds_insts_per_mfma": j["lds_insts_per_mfma"], "beyond_l2_bytes_per_launch": j["beyond_l2_bytes_per_launch"],
-            "source": "profiles/" + p.name + " (committed rocprofv3 --pmc run of this command)"}
+    out = {"valu_per_mfma": j["valu_per_mfma_incl_mfma"], "valu_per_mfma_excl_mfma": j["valu_per_mfma_excl_mfma"],
+           "lds_insts_per_mfma": j["lds_insts_per_mfma"], "beyond_l2_bytes_per_launch": j["beyond_l2_bytes_per_launch"],
+           "source": "profiles/" + p.name + " (committed rocprofv3 --pmc run of this command)"}
+    if "energy" in j:  # round 4 on: nJ per MFMA against the fp4 MFMA alone, same box
+        e = j["energy"]
+        out["energy"] = {k: e[k] for k in ("nj_per_mfma_batch", "nj_per_mfma_mfma_alone", "gap",
+                                           "batch_rate_vs_mfma_alone", "source")}
+    return out
 
 
 # ---------------------------------------------------------------------------- launching
@@ -1043,9 +1048,14 @@ def main():
     # kernel time of one step on the slowest device (a batch of 1-3 queries streams: several launches per step)
     step_kernel_ms = max(per_gpu_step_ms) if per_gpu_step_ms else kms / max(1, len(devs)) / max(1, args.steps)
     achieved = rec_bytes * n_launch / (avg_ms * 1e-3) / 1e9
-    # batch: HBM bytes of the 1024-query launch (the DB once per XCD-shared pass + query tiles)
-    traffic, traffic_src = (load_traffic(args.workload, n_launch, args.layout)
-                            if args.workload != "batch" or nq == 1024 else (None, None))
+    # batch: bytes fetched beyond L2 per 1024-query launch, from the SAME committed PMC run as
+    # kernel.pmc (the template DB about once per XCD + the query tiles re-streamed from the MALL)
+    bpmc = batch_pmc() if args.workload == "batch" and nq == 1024 else None
+    if args.workload != "batch":
+        traffic, traffic_src = load_traffic(args.workload, n_launch, args.layout)
+    else:
+        traffic, traffic_src = ((bpmc["beyond_l2_bytes_per_launch"], bpmc["source"].split(" ")[0][len("profiles/"):])
+                                if bpmc else (None, None))
     ms_per_step = elapsed / args.steps * 1e3
     value = ROT * total * nq / (elapsed / args.steps)
     mfma_frac = MFMA_MACS_PER_TEMPLATE * n_launch * nq / (step_kernel_ms * 1e-3) / FP4_DENSE_PEAK_MACS
@@ -1128,7 +1138,7 @@ def main():
                                  "are re-streamed from the 256-MB MALL for each N-group, "
                                  "the template DB comes from HBM about once per XCD" if args.workload == "batch"
                                  else None),
-                "pmc": batch_pmc() if args.workload == "batch" and nq == 1024 else None,
+                "pmc": bpmc,
             },
             "cpu_baseline": cpu,
             "check": check,

@@ -330,6 +330,13 @@ impl Group {
         check(unsafe { ffi::iris_group_info(self.raw, &mut l, &mut r, &mut f) })?;
         Ok((l, r, f))
     }
+
+    /// Bound of the exchange waits of later calls in milliseconds (0: automatic). A wait that
+    /// runs out aborts the group's communicators and returns `Err`; the group then refuses
+    /// further calls (include/iris_hip.h, "device groups").
+    pub fn set_timeout(&self, ms: u32) -> Result<()> {
+        check(unsafe { ffi::iris_group_set_timeout(self.raw, ms) })
+    }
 }
 
 impl Drop for Group {
