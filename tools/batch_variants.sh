@@ -7,7 +7,7 @@ Q=$1; shift
 O=gpurun_out/batch_variants; mkdir -p $O
 for spec in "$@"; do
     IFS=: read label lib k <<< "$spec"
-    export IRIS_HIP_LIB=$PWD/mpc-iris-code_amd/$lib IRIS_BATCH_KERNEL=$k
+    export IRIS_HIP_LIB=$PWD/mpc-iris-code_amd/$lib IRIS_BATCH_KERNEL=$k IRIS_TEST_HOOKS=1
     timeout -k 10 200 python bench.py --workload batch --queries $Q --steps 3 --warmup 1 --no-cpu-baseline --prewarm-s 0.5 > $O/$label.log 2>&1
     rc=$?
     if [ $rc -ne 0 ] && [ $rc -ne 3 ]; then echo "$label bench rc=$rc"; tail -3 $O/$label.log; exit 1; fi

@@ -32,6 +32,7 @@ run chunk20k_search_reuse 200 --n-per-gpu 20000 --steps 200 --warmup 10 --no-cpu
 run chunk20k_masks_reuse 200 --workload masks --n-per-gpu 20000 --steps 200 --warmup 10 --no-cpu-baseline --reuse-engine
 run chunk20k_shares_reuse 200 --workload shares --n-per-gpu 20000 --steps 200 --warmup 10 --no-cpu-baseline --reuse-engine
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_search -o run -- python3 bench.py --no-cpu-baseline --steps 20 --warmup 3 > $O/prof_search.log 2>&1 || { echo "prof rc=$?"; exit 1; }
+[ -n "$SKIP_PMC" ] && { echo "all ok (pmc skipped)"; exit 0; }
 # HBM traffic of every HBM-bound kernel on this tree (FETCH_SIZE / WRITE_SIZE in separate passes)
 WORKLOADS="search masks shares resolver resolve-masks" timeout -k 10 900 bash tools/pmc_traffic.sh > $O/pmc.log 2>&1 || { echo "pmc rc=$?"; tail -5 $O/pmc.log; exit 1; }
 echo all ok
