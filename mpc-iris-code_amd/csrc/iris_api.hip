@@ -1262,13 +1262,9 @@ int iris_template_batch_engine_new(iris_device_t *d, const iris_template_t *quer
     const uint32_t qgs = batch_query_group();
     const uint32_t nqp = (nq + qgs - 1) / qgs * qgs;  // padded to the kernel's query groups (zero tiles: no candidate)
     const size_t tile_bytes = (size_t)16 * kPlaneGroups * 64;
-    // row-packed kernel (IRIS_BATCH_KERNEL 5): ceil(31 nq / 32) tiles, padded to its 2-tile groups (<= nqp)
-    const bool packed = batch_packed(d->hooks);
-    const uint32_t nrt = (uint32_t)(((31ull * nq + 31) / 32 + 1) / 2 * 2);
     CHK(engine_from_query(d, IRIS_KIND_TEMPLATES, queries, (size_t)nq * sizeof(iris_template_t), 0,
                           (size_t)nqp * tile_bytes, out, [&](void *stream, const void *q, uint32_t *, uint32_t *frag) {
-                              return packed ? launch_query_rows(stream, q, nq, nrt, frag)
-                                            : launch_query_tiles(stream, q, nq, nqp, frag);
+                              return launch_query_tiles(stream, q, nq, nqp, frag);
                           }));
     (*out)->nq = nq;
     device_retain(d);
@@ -1297,10 +1293,10 @@ int iris_template_batch_search(iris_engine_t *e, const iris_db_t *db, uint64_t f
     }
     LaunchRange r{first, n};
     const BatchGeometry geo = batch_geometry(d->hooks, r, e->nq);
-    const uint32_t nqp = geo.nres;
+    const uint32_t nqp = geo.nqg * geo.qper;
     std::vector<Partial> res(nqp);
     if (n > 0) {
-        CHK(ensure(d->partials, (size_t)geo.nparts * geo.G * sizeof(Partial)));
+        CHK(ensure(d->partials, (size_t)nqp * geo.G * sizeof(Partial)));
         CHK(ensure_host_result(d, (size_t)nqp * sizeof(Partial)));
         CHK(timed(d, "template_batch", n * e->nq, [&] {
             return launch_batch(d->hooks, d->stream, db->data, e->qfrag, r, geo, (Partial *)d->partials.p,

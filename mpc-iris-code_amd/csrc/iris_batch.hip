@@ -301,35 +301,6 @@ __global__ void __launch_bounds__(64 * NW, NW <= 8 ? 8 / NW : 1)
     }
 }
 
-// row-packed batches: one workgroup per query, its G partials of part 0 and, when the query's rows
-// straddle two row-tile groups (rtg row tiles each), the G of part 1; ties keep the lower rotation
-__global__ void __launch_bounds__(256) batch_reduce_rows_kernel(const Partial *__restrict__ partials, uint32_t G,
-                                                                uint32_t rtg, Partial *__restrict__ out,
-                                                                uint64_t idx_base) {
-    const uint32_t q = blockIdx.x;
-    const uint32_t parts = (31u * q + 30u) / 32u / rtg != 31u * q / 32u / rtg ? 2u : 1u;
-    Partial c = partial_none();
-    for (uint32_t i = threadIdx.x; i < parts * G; i += blockDim.x) {
-        const Partial p = partials[(uint64_t)2 * q * G + i];
-        if (partial_better_rot(p, c)) c = p;
-    }
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        const Partial o = partial_shfl_xor(c, off);
-        if (partial_better_rot(o, c)) c = o;
-    }
-    __shared__ Partial sh[4];
-    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = c;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        Partial b = sh[0];
-        for (int i = 1; i < 4; ++i)
-            if (partial_better_rot(sh[i], b)) b = sh[i];
-        if (b.den != 0) b.idx += idx_base;
-        out[q] = b;
-    }
-}
-
 // one workgroup per query: reduce its G partials
 __global__ void __launch_bounds__(256) batch_reduce_kernel(const Partial *__restrict__ partials, uint32_t G,
                                                            Partial *__restrict__ out, uint64_t idx_base) {
@@ -418,15 +389,10 @@ constexpr int kGP = IRIS_BATCH2_GP;      // chunk pairs per K-step
 #ifndef IRIS_BATCH2_GP_Q2
 #define IRIS_BATCH2_GP_Q2 4  // chunk pairs per K-step of the 2-query-group shape (5: 197 VGPRs spilled)
 #endif
-// PACK (IRIS_BATCH_KERNEL 5): the A tiles are row-packed (launch_query_rows: row R = 31 q + k, 32 rows per
-// tile, no zero row), so a "query" of the kernel is a row tile spanning at most two queries; each lane
-// keeps a running best per (row tile, query slot), and the workgroup writes one partial per (query, part)
-// — part 1 when the query's first row lies in an earlier workgroup's row tiles — into partials[2 nq][G].
-template <int NW, int WT, int WQL = 4, int BQL = 4, int GPL = lds2::kGP, bool PACK = false>
+template <int NW, int WT, int WQL = 4, int BQL = 4, int GPL = lds2::kGP>
 __global__ void __launch_bounds__(64 * NW, 1)
     batch_lds_kernel(const uint4 *__restrict__ db, const uint4 *__restrict__ qtiles, uint64_t tile0, uint64_t ntiles,
-                     uint64_t first, uint64_t end, uint32_t nqg, uint32_t G, Partial *__restrict__ partials,
-                     uint32_t nq = 0) {
+                     uint64_t first, uint64_t end, uint32_t nqg, uint32_t G, Partial *__restrict__ partials) {
     constexpr int kGP = GPL;                        // chunk pairs per K-step
     constexpr int kSteps = kPlaneGroups / kGP;
     static_assert(kPlaneGroups % kGP == 0, "K-step must tile the 100 chunk pairs");
@@ -512,19 +478,11 @@ __global__ void __launch_bounds__(64 * NW, 1)
 
     // running best per lane and query across the walk: (num | den << 16, N-group x tile << 5 | rotation);
     // den 0 = none yet
-    constexpr int NS = PACK ? 2 : 1;  // query slots per row tile
-    uint32_t run_nd[WQL][1], run_jr[WQL][1];
+    uint32_t run_nd[WQL], run_jr[WQL];
 #pragma unroll
     for (int qi = 0; qi < WQL; ++qi) {
-        run_nd[qi][0] = 1;  // (num 1, den 0): none
-        run_jr[qi][0] = 0;
-    }
-    // PACK: the per-(row tile, slot) running bests live in LDS (lane-linear, read and written once per
-    // N-group): in registers they spill the main loop
-    __shared__ uint2 run_lds[PACK ? NW * WQL * 2 * 64 : 1];
-    if constexpr (PACK) {
-#pragma unroll
-        for (int i = 0; i < WQL * 2; ++i) run_lds[(w * WQL * 2 + i) * 64 + lane] = make_uint2(1u, 0u);
+        run_nd[qi] = 1;  // (num 1, den 0): none
+        run_jr[qi] = 0;
     }
     Partial wave_best;
     v16f den[WQL][WT], sacc[WQL][WT];
@@ -654,44 +612,6 @@ __global__ void __launch_bounds__(64 * NW, 1)
                 const bool valid = live && trel < ntiles && tg >= first && tg < end;
 #pragma unroll
                 for (int qi = 0; qi < WQL; ++qi) {
-                    if constexpr (PACK) {
-                        // row k of row tile mt is batch row 32 mt + k = query q0 + slot, rotation pos - 31 slot
-                        const uint32_t mt = qg * kBQ + qset * WQL + qi;
-                        uint32_t base = 32u * mt - 31u * (32u * mt / 31u);
-                        // opaque here: otherwise hipcc hoists the 32 loop-invariant row masks and rotations
-                        // out of the walk and spills the main loop
-                        asm volatile("; row base %0" : "+s"(base));
-                        uint32_t bn[2] = {1, 1}, bd[2] = {0, 0}, br[2] = {0, 0};
-#pragma unroll
-                        for (int r = 0; r < 16; ++r) {
-                            const int k = (r & 3) + 8 * (r >> 2) + 4 * h;  // ascending in r: ties keep the lower rotation
-                            const uint32_t pos = base + (uint32_t)k;
-                            const bool s1 = pos >= 31u;
-                            const uint32_t dd = (uint32_t)den[qi][t][r];
-                            const uint32_t nn = (uint32_t)(((int)dd - (int)sacc[qi][t][r]) >> 1);
-                            const bool b0 = !s1 && __umul24(nn, bd[0]) < __umul24(bn[0], dd);
-                            const bool b1 = s1 && __umul24(nn, bd[1]) < __umul24(bn[1], dd);
-                            if (b0) {
-                                bn[0] = nn;
-                                bd[0] = dd;
-                                br[0] = pos;
-                            }
-                            if (b1) {
-                                bn[1] = nn;
-                                bd[1] = dd;
-                                br[1] = pos - 31u;
-                            }
-                        }
-#pragma unroll
-                        for (int sl = 0; sl < 2; ++sl) {
-                            uint2 &run = run_lds[((w * WQL + qi) * 2 + sl) * 64 + lane];
-                            const uint2 cur = run;
-                            const uint32_t rn = cur.x & 0xFFFFu, rd = cur.x >> 16;
-                            if (valid && __umul24(bn[sl], rd) < __umul24(rn, bd[sl]))
-                                run = make_uint2(bn[sl] | (bd[sl] << 16), ((j * (uint32_t)WT + (uint32_t)t) << 5) | br[sl]);
-                        }
-                        continue;
-                    }
                     // (bn, bd) = (1, 0) is "none": a row with den 0 (no jointly valid bit; also the
                     // zero row k = 31) is (0, 0) and never wins, n * 0 < 1 * d holds for any real
                     // candidate, so the scan needs no validity tests
@@ -709,12 +629,12 @@ __global__ void __launch_bounds__(64 * NW, 1)
                             br = (uint32_t)k;
                         }
                     }
-                    const uint32_t rn = run_nd[qi][0] & 0xFFFFu, rd = run_nd[qi][0] >> 16;
+                    const uint32_t rn = run_nd[qi] & 0xFFFFu, rd = run_nd[qi] >> 16;
                     // strict <: an equal fraction keeps the earlier (lower-index) template; the
                     // running best starts as (1, 0) too
                     if (valid && __umul24(bn, rd) < __umul24(rn, bd)) {
-                        run_nd[qi][0] = bn | (bd << 16);
-                        run_jr[qi][0] = ((j * (uint32_t)WT + (uint32_t)t) << 5) | br;
+                        run_nd[qi] = bn | (bd << 16);
+                        run_jr[qi] = ((j * (uint32_t)WT + (uint32_t)t) << 5) | br;
                     }
                 }
             }
@@ -729,61 +649,30 @@ __global__ void __launch_bounds__(64 * NW, 1)
     {
         Partial best = partial_none();
 #pragma unroll
-        for (int qi = 0; qi < WQL; ++qi)
-#pragma unroll
-            for (int sl = 0; sl < NS; ++sl) {
-                Partial c = partial_none();
-                uint32_t rnd = run_nd[qi][0], rjr = run_jr[qi][0];
-                if constexpr (PACK) {
-                    const uint2 run = run_lds[((w * WQL + qi) * 2 + sl) * 64 + lane];
-                    rnd = run.x;
-                    rjr = run.y;
-                }
-                if (rnd >> 16) {
-                    const uint32_t jt = rjr >> 5, jj = jt / WT, t = jt - jj * WT;
-                    const uint64_t trel = (gi + (uint64_t)jj * G) * kTilesPerGroup + tset * WT + t;
-                    c.num = rnd & 0xFFFFu;
-                    c.den = rnd >> 16;
-                    c.rot = (int)(rjr & 31u);
-                    c.idx = (tile0 + trel) * 32 + (lane & 31) - first;
-                }
-#pragma unroll
-                for (int off = 32; off >= 1; off >>= 1) {
-                    const Partial o = partial_shfl_xor(c, off);
-                    if (partial_better_rot(o, c)) c = o;
-                }
-                if (lane == qi * NS + sl) best = c;
+        for (int qi = 0; qi < WQL; ++qi) {
+            Partial c = partial_none();
+            if (run_nd[qi] >> 16) {
+                const uint32_t jt = run_jr[qi] >> 5, jj = jt / WT, t = jt - jj * WT;
+                const uint64_t trel = (gi + (uint64_t)jj * G) * kTilesPerGroup + tset * WT + t;
+                c.num = run_nd[qi] & 0xFFFFu;
+                c.den = run_nd[qi] >> 16;
+                c.rot = (int)(run_jr[qi] & 31u);
+                c.idx = (tile0 + trel) * 32 + (lane & 31) - first;
             }
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) {
+                const Partial o = partial_shfl_xor(c, off);
+                if (partial_better_rot(o, c)) c = o;
+            }
+            if (lane == qi) best = c;
+        }
         wave_best = best;
     }
 
     __syncthreads();
-    Partial *sP = (Partial *)&afrag[0][0][0][0][0];  // [wave][query (slot) of the wave]
-    if (lane < WQL * NS) sP[w * WQL * NS + lane] = wave_best;
+    Partial *sP = (Partial *)&afrag[0][0][0][0][0];  // [wave][query of the wave]
+    if (lane < WQL) sP[w * WQL + lane] = wave_best;
     __syncthreads();
-    if constexpr (PACK) {
-        // the workgroup's rows [32 mt0, 32 (mt0 + kBQ)) meet at most kQMeet queries qa, qa + 1, ...
-        constexpr int kQMeet = (kBQ * 32 + 30) / 31 + 1;
-        const uint32_t mt0 = qg * kBQ, qa = 32u * mt0 / 31u, qz = (32u * (mt0 + kBQ) - 1u) / 31u;
-        if (tid < kQMeet) {
-            const uint32_t q = qa + (uint32_t)tid;
-            if (q <= qz && q < nq) {
-                Partial b = partial_none();
-                for (int ww = 0; ww < NW; ++ww)
-#pragma unroll
-                    for (int qi = 0; qi < WQL; ++qi) {
-                        const uint32_t mt = mt0 + (uint32_t)((ww % QW) * WQL + qi), q0 = 32u * mt / 31u;
-#pragma unroll
-                        for (int sl = 0; sl < NS; ++sl)
-                            if (q0 + sl == q && partial_better_rot(sP[(ww * WQL + qi) * NS + sl], b))
-                                b = sP[(ww * WQL + qi) * NS + sl];
-                    }
-                const uint32_t part = 31u * q / 32u >= mt0 ? 0u : 1u;  // 1: q's first row is in an earlier group
-                partials[((uint64_t)2 * q + part) * G + gi] = b;
-            }
-        }
-        return;
-    }
     if (tid < kBQ) {  // query tid: the waves of its query set, one per tile set
         const int qs = tid / WQL, qi = tid % WQL;
         Partial b = sP[qs * WQL + qi];
@@ -797,11 +686,8 @@ __global__ void __launch_bounds__(64 * NW, 1)
 // 2-query groups x 16-tile N-groups, 2 x 2 per wave (default: half the LDS fragment reads and
 // half the query-tile bytes per template of 2; 3.5 % faster, profiles/r03_batch_variants.txt);
 // 2 = batch_lds_kernel 4-query groups x 8 tiles, 4 x 1 per wave (round 2); 3 = 4-query groups,
-// 2 x 2 per wave; 1 = batch_kernel (LDS-DMA staged, round 1); 5 = the shape of 4 on row-packed query
-// tiles (31 rows per query, no zero row: 31/32 of the MFMAs of 4)
-static int batch_kernel_choice(const Hooks &h) { return h.batch_kernel >= 1 && h.batch_kernel <= 5 ? h.batch_kernel : 4; }
-
-bool batch_packed(const Hooks &h) { return batch_kernel_choice(h) == 5; }
+// 2 x 2 per wave; 1 = batch_kernel (LDS-DMA staged, round 1)
+static int batch_kernel_choice(const Hooks &h) { return h.batch_kernel >= 1 && h.batch_kernel <= 4 ? h.batch_kernel : 4; }
 
 uint32_t batch_query_group() { return BQ; }
 
@@ -811,14 +697,9 @@ BatchGeometry batch_geometry(const Hooks &h, LaunchRange r, uint32_t nq) {
     const uint64_t tile1 = (r.first + r.n + 31) / 32;
     g.ntiles = tile1 - g.tile0;
     const int kc = batch_kernel_choice(h);
-    g.packed = kc == 5;
-    g.nq = nq;
-    g.qper = kc >= 4 ? 2 : BQ;  // queries (row tiles when packed) per query group
-    const uint64_t units = g.packed ? (31ull * nq + 31) / 32 : nq;
-    g.nqg = (uint32_t)((units + g.qper - 1) / g.qper);
-    g.nres = g.packed ? nq : g.nqg * g.qper;
-    g.nparts = g.packed ? 2 * nq : g.nqg * g.qper;
-    const uint32_t tiles_per_group = kc == 1 ? BT : kc >= 4 ? 16 : 8;
+    g.qper = kc == 4 ? 2 : BQ;  // queries per query group
+    g.nqg = (nq + g.qper - 1) / g.qper;
+    const uint32_t tiles_per_group = kc == 1 ? BT : kc == 4 ? 16 : 8;
     const uint64_t ngroups = (g.ntiles + tiles_per_group - 1) / tiles_per_group;
     // batch_kernel: ~2 workgroups per CU in total; batch_lds_kernel (one 128-KB-LDS workgroup
     // per CU): one round of workgroups
@@ -846,26 +727,16 @@ int launch_batch(const Hooks &h, void *stream, const void *db, const void *qtile
     if (kc == 2)
         hipLaunchKernelGGL((batch_lds_kernel<8, 1>), dim3(g.nqg * g.G), dim3(64 * 8), 0, (hipStream_t)stream,
                            (const uint4 *)db, (const uint4 *)qtiles, g.tile0, g.ntiles, r.first, r.first + r.n, g.nqg,
-                           g.G, partials, 0u);
+                           g.G, partials);
     else if (kc == 3)  // 2 queries x 2 tiles per wave: half the LDS fragment reads per MFMA
         hipLaunchKernelGGL((batch_lds_kernel<8, 2, 2>), dim3(g.nqg * g.G), dim3(64 * 8), 0, (hipStream_t)stream,
                            (const uint4 *)db, (const uint4 *)qtiles, g.tile0, g.ntiles, r.first, r.first + r.n, g.nqg,
-                           g.G, partials, 0u);
+                           g.G, partials);
     else if (kc == 4)  // 2-query groups x 16-tile N-groups: half the query-tile traffic beyond L2
         hipLaunchKernelGGL((batch_lds_kernel<8, 2, 2, 2, IRIS_BATCH2_GP_Q2>), dim3(g.nqg * g.G), dim3(64 * 8), 0,
                            (hipStream_t)stream,
                            (const uint4 *)db, (const uint4 *)qtiles, g.tile0, g.ntiles, r.first, r.first + r.n, g.nqg,
-                           g.G, partials, 0u);
-    else if (kc == 5) {  // the same on row-packed tiles: 2-row-tile groups
-        hipLaunchKernelGGL((batch_lds_kernel<8, 2, 2, 2, IRIS_BATCH2_GP_Q2, true>), dim3(g.nqg * g.G), dim3(64 * 8), 0,
-                           (hipStream_t)stream,
-                           (const uint4 *)db, (const uint4 *)qtiles, g.tile0, g.ntiles, r.first, r.first + r.n, g.nqg,
-                           g.G, partials, g.nq);
-        if (hipGetLastError() != hipSuccess) return -1;
-        hipLaunchKernelGGL(batch_reduce_rows_kernel, dim3(g.nq), dim3(256), 0, (hipStream_t)stream, partials, g.G,
-                           g.qper, out, idx_base);
-        return hipGetLastError() == hipSuccess ? 0 : -1;
-    }
+                           g.G, partials);
     else
         hipLaunchKernelGGL(batch_kernel, dim3(g.nqg * g.G), dim3(64 * NW), 0, (hipStream_t)stream, (const uint4 *)db,
                            (const uint4 *)qtiles, g.tile0, g.ntiles, r.first, r.first + r.n, g.nqg, g.G, g.xqg,

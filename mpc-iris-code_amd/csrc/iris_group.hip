@@ -822,7 +822,7 @@ int iris_group_template_batch_search(iris_group_db_t *gdb, const iris_template_t
             for (uint32_t j = 0; j < spd; ++j) {
                 const size_t s = i * spd + j;
                 const BatchGeometry geo = batch_geometry(d->hooks, LaunchRange{0, gdb->count[s]}, nq);
-                pmax = std::max(pmax, (size_t)geo.nparts * geo.G * sizeof(Partial));
+                pmax = std::max(pmax, (size_t)geo.nqg * geo.qper * geo.G * sizeof(Partial));
             }
             rc = ensure(d->partials, pmax);
             for (uint32_t j = 0; rc == 0 && j < spd; ++j) {

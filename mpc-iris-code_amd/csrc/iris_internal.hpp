@@ -215,8 +215,6 @@ int launch_query_template(void *stream, const void *q, uint32_t *tab, uint32_t *
 int launch_query_masks(void *stream, const void *qmask, uint32_t *tab, uint32_t *frag);
 int launch_query_shares(void *stream, const void *q, uint32_t *tab, uint32_t *frag);
 int launch_query_tiles(void *stream, const void *queries, uint32_t nq, uint32_t nqp, uint32_t *tiles);
-// row-packed batch tiles (31 rows per query, 32 per tile, no zero row): ntiles tiles
-int launch_query_rows(void *stream, const void *queries, uint32_t nq, uint32_t ntiles, uint32_t *tiles);
 // rounds: ChaCha8 / 12 / 20 (anything else: -1)
 int launch_prepare_shares(void *stream, const void *templates, uint64_t m, uint64_t g0, const uint8_t key[32],
                           uint64_t nonce, uint32_t rounds, uint32_t parties, void *shares);
@@ -284,13 +282,8 @@ struct BatchGeometry {
     uint32_t nqg, G;  // query groups, workgroups per query group
     uint32_t qper;    // queries per query group (nqg * qper results; at most the engine's padding)
     uint32_t xqg;     // > 0: XCD-aware grid, xqg query groups per XCD at a time (iris_batch.hip)
-    bool packed;      // row-packed A tiles (launch_query_rows): a "query group" is qper row tiles
-    uint32_t nq;      // queries of the batch
-    uint32_t nres;    // results the reduce writes (out[0 .. nres)): nqg * qper, or nq when packed
-    uint32_t nparts;  // partial rows per workgroup column (partials = nparts * G)
 };
 BatchGeometry batch_geometry(const Hooks &h, LaunchRange r, uint32_t nq);
-bool batch_packed(const Hooks &h);  // the device's batch kernel reads row-packed query tiles
 uint32_t batch_query_group();  // queries per batch_kernel query group (padding unit)
 int launch_batch(const Hooks &h, void *stream, const void *db, const void *qtiles, LaunchRange r, const BatchGeometry &g,
                  Partial *partials, Partial *out, uint64_t idx_base = 0);

@@ -192,48 +192,6 @@ __global__ void __launch_bounds__(256) query_tiles_kernel(const iris_template_t 
     }
 }
 
-// Row-packed batched-query tiles (IRIS_BATCH_KERNEL 5): the 31·nq rotation rows of the batch,
-// row R = 31 q + k (query q rotated by k − 15), packed 32 to a tile with no zero row: record j of
-// tile m is row 32 m + j (zero past the last row).  A tile spans at most two queries, whose planes
-// are staged in LDS.  One workgroup per tile; tiles past ceil(31 nq / 32) are zero tiles.
-__global__ void __launch_bounds__(256) query_rows_kernel(const iris_template_t *__restrict__ queries, uint32_t nq,
-                                                         uint4 *__restrict__ tiles) {
-    __shared__ uint32_t sp[2][kPlaneDwords], sm[2][kPlaneDwords];
-    const uint32_t m = blockIdx.x, rows = 31u * nq, qa = 32u * m / 31u;
-    uint4 *tile = tiles + (size_t)m * kPlaneGroups * 64;
-    if (32u * m >= rows) {
-        for (int i = threadIdx.x; i < kPlaneGroups * 64; i += blockDim.x) tile[i] = make_uint4(0, 0, 0, 0);
-        return;
-    }
-    for (int i = threadIdx.x; i < 2 * kPlaneDwords; i += blockDim.x) {
-        const uint32_t s = i / kPlaneDwords, d = i - s * kPlaneDwords, q = qa + s;
-        sp[s][d] = q < nq ? ((const uint32_t *)queries[q].pattern)[d] : 0u;
-        sm[s][d] = q < nq ? ((const uint32_t *)queries[q].mask)[d] : 0u;
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < kPlaneGroups * 64; i += blockDim.x) {
-        const int g = i >> 6, L = i & 63, j = L & 31, h = L >> 5;
-        const uint32_t R = 32u * m + (uint32_t)j;
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (R < rows) {
-            const uint32_t q = R / 31u, s = q - qa;
-            const int k = (int)(R - 31u * q);
-            const uint32_t em0 = rot_dword(sm[s], k - 15, 4 * g + h), ep0 = rot_dword(sp[s], k - 15, 4 * g + h);
-            const uint32_t em1 = rot_dword(sm[s], k - 15, 4 * g + 2 + h), ep1 = rot_dword(sp[s], k - 15, 4 * g + 2 + h);
-            v = make_uint4(xpack(em0 & 0xFFFFu, ep0 & 0xFFFFu), xpack(em0 >> 16, ep0 >> 16),
-                           xpack(em1 & 0xFFFFu, ep1 & 0xFFFFu), xpack(em1 >> 16, ep1 >> 16));
-        }
-        tile[i] = v;
-    }
-}
-
-int launch_query_rows(void *stream, const void *queries, uint32_t nq, uint32_t ntiles, uint32_t *tiles) {
-    if (ntiles == 0) return 0;
-    hipLaunchKernelGGL(query_rows_kernel, dim3(ntiles), dim3(256), 0, (hipStream_t)stream,
-                       (const iris_template_t *)queries, nq, (uint4 *)tiles);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
-}
-
 // q / qmask: HOST pointers (copied into the kernel arguments at launch)
 int launch_query_template(void *stream, const void *q, uint32_t *tab, uint32_t *frag) {
     TemplateArg a;
