@@ -927,9 +927,9 @@ def main():
                 ms = e.search(db, index_base=lo)
                 return iris_dist.allgather_merge_many(ms) if rehearsal and exchange else ms
             if args.workload != "search":
-                e.batch_process_device(db, out_dev)  # [n][31] u16 left in HBM
+                e.batch_process_device(db, out_dev, 0, n)  # [n][31] u16 left in HBM (n known, as out.len())
                 return None
-            m = e.search(db, index_base=lo)
+            m = e.search(db, 0, n, index_base=lo)
             return iris_dist.allgather_merge(m) if rehearsal and exchange else m
         finally:
             if eng is None:

@@ -60,6 +60,8 @@ _lock = threading.Lock()
 def load_library(path=None):
     """Load libiris_hip.so (fails loudly when it is absent)."""
     global _lib
+    if _lib is not None and path is None:  # per-call fast path: no lock once loaded
+        return _lib
     with _lock:
         if _lib is not None and path is None:
             return _lib
@@ -749,8 +751,9 @@ class _Engine:
 def _batch_process_device(self, db, out_device_ptr, first=0, n=None):
     """Results stay on the GPU: out_device_ptr is a device array of n*31 u16."""
     n = (len(db) - first) if n is None else n
-    _check(load_library().iris_engine_batch_process_device(self.handle, db.handle, int(first), int(n),
-                                                           ctypes.c_void_p(out_device_ptr)))
+    rc = load_library().iris_engine_batch_process_device(self.handle, db.handle, int(first), int(n), int(out_device_ptr))
+    if rc:
+        _check(rc)
 
 
 _Engine.batch_process_device = _batch_process_device
@@ -859,8 +862,10 @@ class TemplateEngine(_Engine):
         """Fused min/argmin (src/main.rs:581-621) -> Match."""
         n = (len(db) - first) if n is None else n
         m = Match()
-        _check(load_library().iris_template_search(self.handle, db.handle, int(first), int(n), int(index_base),
-                                                   ctypes.c_void_p(dist_out_device or 0), ctypes.byref(m)))
+        rc = load_library().iris_template_search(self.handle, db.handle, int(first), int(n), int(index_base),
+                                                 dist_out_device or None, ctypes.byref(m))
+        if rc:
+            _check(rc)
         return m
 
 
