@@ -443,9 +443,13 @@ class Ranks:
 
         if not args.dry_run:
             have = ih.Device.count()
-            if backend == "nccl" and self.local >= have:
+            # a launcher that gives each rank only its own GPU (a *_VISIBLE_DEVICES list per rank)
+            # leaves one device visible: that one is the rank's (RCCL refuses two ranks on one GPU)
+            own = have == 1 and any(os.environ.get(v) for v in
+                                    ("HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"))
+            if backend == "nccl" and self.local >= have and not own:
                 raise SystemExit(f"error: rank {self.rank} (local {self.local}) has no GPU of its own: {have} visible")
-            self.ordinal = self.local % max(1, have)
+            self.ordinal = 0 if own else self.local % max(1, have)
         dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
         if dist.get_world_size() != args.gpus:
             raise SystemExit(f"error: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
