@@ -22,7 +22,15 @@ static inline uint64_t resident_blocks(int per_cu) {
     return (uint64_t)n * per_cu;
 }
 
+
 typedef unsigned int u32x4_nt __attribute__((ext_vector_type(4)));
+
+// 16-B store written through the XCD's L2 (sc1: the line leaves L2 and is dropped there; the same
+// cost as a plain 16-B store, MI355X_MICROARCH.md "stores of each flavour").
+__device__ __forceinline__ void store16_wt(uint4 *dst, const uint4 &v) {
+    const u32x4_nt w = {v.x, v.y, v.z, v.w};
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(dst), "v"(w) : "memory");
+}
 
 // Writes one 32-record tile's [32][31] u16 output rows.  In the 32x32 MFMA C
 // layout lane l holds rows k = (r & 3) + 8 (r >> 2) + 4 (l >> 5), r = 0..15, of
@@ -30,9 +38,18 @@ typedef unsigned int u32x4_nt __attribute__((ext_vector_type(4)));
 // [first, end) whose output offset is 16-B aligned is staged through the
 // wave's 2 KB LDS buffer and written with 124 16-byte stores (1984 B); other
 // tiles fall back to per-element stores of their valid records.
+// wt (a kernel that signals completion before it ends, DoneSignal): every row byte is written
+// through L2 (sc1), so once the storing wave's vmcnt(0) wait returns the rows are in memory, where a
+// reader on any XCD -- a kernel on another stream, a copy engine -- finds them without this launch's
+// end-of-kernel write-back (nontemporal and plain stores stay dirty in the XCD's L2 until then).
+#ifndef IRIS_ROWS_WT
+#define IRIS_ROWS_WT 1  // 0: the signalling kernels store like the others (A/B builds of the visibility test)
+#endif
 template <class F>
 __device__ __forceinline__ void store_tile_rows(uint16_t *__restrict__ out, uint16_t *lds, uint64_t tile_t0,
-                                                uint64_t first, uint64_t end, bool tile_valid, int lane, F val) {
+                                                uint64_t first, uint64_t end, bool tile_valid, int lane, F val,
+                                                bool wt = false) {
+    wt = wt && IRIS_ROWS_WT;
     const int h = lane >> 5;
     const bool full = tile_valid && tile_t0 >= first && tile_t0 + 32 <= end && ((tile_t0 - first) & 7) == 0 &&
                       (((uintptr_t)out & 15) == 0);
@@ -53,6 +70,10 @@ __device__ __forceinline__ void store_tile_rows(uint16_t *__restrict__ out, uint
 #endif
         // diagnostic builds only (results wrong by design): 1 = half the row bytes, 2 = none
         constexpr int kStores = IRIS_STORE_DIAG == 0 ? 32 * kRot * 2 / 16 : IRIS_STORE_DIAG == 1 ? 32 * kRot / 16 : 0;
+        if (wt) {  // wave-uniform
+            for (int i = lane; i < kStores; i += 64) store16_wt(&dst[i], src[i]);
+            return;
+        }
         for (int i = lane; i < kStores; i += 64) {
             const uint4 v = src[i];
 #if IRIS_STORE_PLAIN
@@ -68,7 +89,11 @@ __device__ __forceinline__ void store_tile_rows(uint16_t *__restrict__ out, uint
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
             const int k = (r & 3) + 8 * (r >> 2) + 4 * h;
-            if (k < kRot) out[(tg - first) * kRot + k] = val(r);
+            if (k >= kRot) continue;
+            if (wt)  // agent-scope relaxed store: global_store_short ... sc1
+                __hip_atomic_store(&out[(tg - first) * kRot + k], val(r), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else
+                out[(tg - first) * kRot + k] = val(r);
         }
     }
 }

@@ -331,7 +331,7 @@ __global__ void __launch_bounds__(64 * KS)
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[i] += red[k][i][lane];
     store_tile_rows(out, sh_out, tile * kTile, first, end, true, lane,
-                    [&](int r) { return (uint16_t)(uint32_t)acc[r]; });
+                    [&](int r) { return (uint16_t)(uint32_t)acc[r]; }, sig.done != nullptr);
     if (sig.done) {  // wave 0 stored the workgroup's rows: once they are performed, take the ticket
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (lane == 0) signal_done_last(sig);
@@ -621,7 +621,7 @@ __global__ void __launch_bounds__(64 * KS, 2)
             const uint32_t cross = (uint32_t)s2[t][r] + 128u * (uint32_t)ehi + 128u * (uint32_t)qs.x +
                                    128u * (uint32_t)elo + 128u * (uint32_t)qs.y;
             return (uint16_t)(lo + 256u * cross);
-        });
+        }, sig.done != nullptr);
     }
     if (sig.done) {  // wave 0 stored the workgroup's rows: once they are performed, take the ticket
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

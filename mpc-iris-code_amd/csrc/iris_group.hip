@@ -652,19 +652,28 @@ int iris_group_template_search_async(iris_group_db_t *gdb, const iris_template_t
     p->timeout_ms = group_timeout(g, gdb->max_count, 1);
     auto abandon = [&](int rc, bool gather_started) {
         const std::string m = g_err;
-        for (size_t i = 0; i < L; ++i) {
-            iris_device *d = g->devs[i];
-            (void)hipSetDevice(d->ordinal);
-            (void)hipStreamSynchronize(d->stream);
-            if (d->aux) (void)hipStreamSynchronize(d->aux);
-            if (p->slots[i]) d->free_slots.push_back(p->slots[i]);
-            if (p->evs[i]) d->event_pool.push_back(p->evs[i]);
-            if (p->reached[i]) d->event_pool.push_back(p->reached[i]);
-        }
-        delete p;
         // The peers are (or will be) inside this search's all-gather, and this process's
-        // communicators are out of step with theirs: abort rather than let every rank hang.
-        if (remote || gather_started) (void)group_abort(g, "a rank failed to enqueue its search: " + m);
+        // communicators are out of step with theirs: abort rather than let every rank hang.  The
+        // abort comes first: an earlier search's all-gather still queued on a side stream may be
+        // waiting for a lost peer, and only the abort ends it (group_abort drains with a bound).
+        bool drained = true;
+        if (remote || gather_started) {
+            drained = group_abort(g, "a rank failed to enqueue its search: " + m);
+        } else {
+            for (iris_device *d : g->devs) {
+                (void)hipSetDevice(d->ordinal);
+                (void)hipStreamSynchronize(d->stream);
+                if (d->aux) (void)hipStreamSynchronize(d->aux);
+            }
+        }
+        if (drained)  // otherwise aborted work may still write them: leaked rather than reused
+            for (size_t i = 0; i < L; ++i) {
+                iris_device *d = g->devs[i];
+                if (p->slots[i]) d->free_slots.push_back(p->slots[i]);
+                if (p->evs[i]) d->event_pool.push_back(p->evs[i]);
+                if (p->reached[i]) d->event_pool.push_back(p->reached[i]);
+            }
+        delete p;
         return fail(rc, m);
     };
     const uint32_t b = (uint32_t)(gdb->searches++ % kSendRing);

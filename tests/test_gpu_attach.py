@@ -333,3 +333,42 @@ def test_device_output_chunks_return_on_completion_word(device, kind):
         finally:
             device.free(out)
             device.free(oout)
+
+
+@pytest.mark.parametrize("kind", [ih.KIND_MASKS, ih.KIND_SHARES])
+def test_device_output_rows_visible_to_unordered_reader(device, kind):
+    """A device-output call returns on the kernel's completion word, before the launch has ended
+    (and before its end-of-kernel cache write-back): the rows must already be in memory for a
+    reader that is not ordered after the library's stream -- here the runtime's own blocking
+    hipMemcpy on the null stream, issued the moment the call returns (the library's stream is
+    non-blocking, so nothing orders the two).  The signalling kernels write their rows through
+    the XCD's L2 for this (store_tile_rows, wt).  A build without the write-through
+    (-DIRIS_ROWS_WT=0) also passed on the box it ran on (gpurun_out r04l): the copy starts
+    microseconds after the launch's own end-of-kernel write-back, so this pins the contract
+    rather than catching the unfixed timing window."""
+    import ctypes
+
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    if kind == ih.KIND_MASKS:
+        n, chunk = 60_000, 20_000
+        recs = oc.gen_masks(SEED + 30, 0, n)
+        q = oc.gen_masks(SEED + 31, 0, 1)[0]
+        eng, want = ih.MasksEngine(device, q), oc.masks_batch(q, recs)
+    else:
+        n, chunk = 6_000, 2_000
+        recs = oc.gen_shares(SEED + 32, 0, n)
+        q = oc.gen_shares(SEED + 33, 0, 1)[0]
+        eng, want = ih.DistanceEngine(device, q), oc.distance_batch(q, recs)
+    with eng, ih.Database(device, kind, n) as db:
+        db.append(recs)
+        out = device.alloc(chunk * 31 * 2)
+        rows = np.empty((chunk, 31), np.uint16)
+        try:
+            for it in range(12):
+                a = (it % 3) * chunk  # each call overwrites the previous call's rows in the same buffer
+                eng.batch_process_device(db, out, first=a, n=chunk)
+                assert hip.hipMemcpy(rows.ctypes.data, out, rows.nbytes, 2) == 0  # hipMemcpyDeviceToHost
+                assert (rows == want[a:a + chunk]).all(), it
+        finally:
+            device.free(out)
