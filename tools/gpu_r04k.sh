@@ -10,6 +10,8 @@ tail -1 $O/smoke.log
 timeout -k 10 300 python bench.py > $O/default.log 2>&1 || { echo "default bench rc=$?"; tail -5 $O/default.log; exit 1; }
 grep '^{' $O/default.log > $O/default.jsonl
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_search -o run -- python3 bench.py --no-cpu-baseline --steps 20 --warmup 3 > $O/prof_search.log 2>&1 || { echo "prof rc=$?"; exit 1; }
+timeout -k 10 120 tools/call_overhead > $O/call_overhead.txt 2>&1 || { echo "call_overhead rc=$?"; exit 1; }
+cat $O/call_overhead.txt
 for w in search masks shares; do
   timeout -k 10 200 python bench.py --workload $w --n-per-gpu 20000 --steps 400 --warmup 20 --no-cpu-baseline --reuse-engine > $O/chunk20k_${w}_reuse.log 2>&1 || { echo "chunk $w rc=$?"; exit 1; }
   grep '^{' $O/chunk20k_${w}_reuse.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); k=d['kernel']['avg_ms']; print('chunk20k_$w', 'step_us', round(d['ms_per_step']*1e3,1), 'unprofiled_us', round(d['ms_per_step_unprofiled']*1e3,1), 'kernel_us', round(k*1e3,1), 'ratio', round(d['ms_per_step_unprofiled']/k,3), d['check']['ok'])"
