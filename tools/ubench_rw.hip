@@ -7,6 +7,9 @@
 //   2 burst, plain stores
 //   3 trickle: the previous group's words stored over the first 8 steps
 //   4 spread: ~10 words per step over the 50 steps of the next group
+//   5 slotted: the group's words held (as in 3) and stored only inside chip-wide write windows of
+//     the constant-rate clock (s_memrealtime, 100 MHz: W of every P ticks), so every wave's writes
+//     fall in the same short bursts; a wave still holding words when its next group ends stores them
 // All modes read the same bytes; modes 1-4 write the same bytes.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -18,7 +21,8 @@ constexpr int kT = 4, kSteps = 50, kWords = 496;  // 16-B output words per group
 
 template <int MODE>
 __global__ void __launch_bounds__(256, 2) rw_kernel(const uint4 *__restrict__ src, uint64_t groups,
-                                                     uint4 *__restrict__ dst, uint32_t *out) {
+                                                     uint4 *__restrict__ dst, uint32_t *out, uint32_t P = 0,
+                                                     uint32_t W = 0) {
     const int lane = threadIdx.x & 63;
     const uint64_t wave = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const uint64_t nwaves = (uint64_t)gridDim.x * 4;
@@ -27,7 +31,17 @@ __global__ void __launch_bounds__(256, 2) rw_kernel(const uint4 *__restrict__ sr
 #pragma unroll
     for (int i = 0; i < 8; ++i) pend[i] = u32x4{0, 0, 0, 0};
     uint64_t prev = ~0ull;
+    bool held = false;  // mode 5: words of group `prev` not stored yet
+    auto store_held = [&] {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int i = k * 64 + lane;
+            if (i < kWords) __builtin_nontemporal_store(pend[k], (u32x4 *)(dst + prev * kWords + i));
+        }
+        held = false;
+    };
     for (uint64_t g = wave; g < groups; g += nwaves) {
+        if (MODE == 5 && held) store_held();  // no window came during the whole group
         const uint4 *base = src + g * kT * 3200;  // 4 tiles of 3200 uint4 (51 200 B)
 #pragma unroll 2
         for (int s = 0; s < kSteps; ++s) {
@@ -42,6 +56,7 @@ __global__ void __launch_bounds__(256, 2) rw_kernel(const uint4 *__restrict__ sr
 #pragma unroll
                 for (int k = 0; k < 7; ++k) pend[k] = pend[k + 1];
             }
+            if (MODE == 5 && held && (uint32_t)(__builtin_amdgcn_s_memrealtime() % P) < W) store_held();
             if (MODE == 4 && prev != ~0ull && lane < 10) {
                 const int i = s * 10 + lane;
                 if (i < kWords) __builtin_nontemporal_store(u32x4{acc, 0, 0, 0}, (u32x4 *)(dst + prev * kWords + i));
@@ -56,9 +71,10 @@ __global__ void __launch_bounds__(256, 2) rw_kernel(const uint4 *__restrict__ sr
                     *(u32x4 *)(dst + g * kWords + i) = w;
             }
         }
-        if (MODE == 3) {
+        if (MODE == 3 || MODE == 5) {
 #pragma unroll
             for (int k = 0; k < 8; ++k) pend[k] = u32x4{acc, (uint32_t)k, 0, 0};
+            held = MODE == 5;
         }
         prev = g;
     }
@@ -69,29 +85,30 @@ __global__ void __launch_bounds__(256, 2) rw_kernel(const uint4 *__restrict__ sr
             if (i < kWords) __builtin_nontemporal_store(pend[k], (u32x4 *)(dst + prev * kWords + i));
         }
     }
+    if (MODE == 5 && held) store_held();
     if (MODE == 4 && prev != ~0ull && lane < 10)
         for (int i = lane; i < kWords; i += 10) dst[prev * kWords + i] = make_uint4(acc, 0, 0, 0);
     if (acc == 0x12345678u) out[0] = acc;
 }
 
 template <int MODE>
-void run(const uint4 *src, uint64_t groups, uint4 *dst, uint32_t *out, int bpc) {
+void run(const uint4 *src, uint64_t groups, uint4 *dst, uint32_t *out, int bpc, uint32_t P = 0, uint32_t W = 0) {
     const int grid = 256 * bpc;
     hipEvent_t e0, e1;
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
-    for (int i = 0; i < 2; ++i) hipLaunchKernelGGL((rw_kernel<MODE>), grid, 256, 0, 0, src, groups, dst, out);
+    for (int i = 0; i < 2; ++i) hipLaunchKernelGGL((rw_kernel<MODE>), grid, 256, 0, 0, src, groups, dst, out, P, W);
     const int reps = 20;
     (void)hipEventRecord(e0);
-    for (int i = 0; i < reps; ++i) hipLaunchKernelGGL((rw_kernel<MODE>), grid, 256, 0, 0, src, groups, dst, out);
+    for (int i = 0; i < reps; ++i) hipLaunchKernelGGL((rw_kernel<MODE>), grid, 256, 0, 0, src, groups, dst, out, P, W);
     (void)hipEventRecord(e1);
     (void)hipEventSynchronize(e1);
     float ms = 0;
     (void)hipEventElapsedTime(&ms, e0, e1);
     ms /= reps;
     const double rb = (double)groups * kT * 51200, wb = MODE ? (double)groups * kWords * 16 : 0;
-    printf("mode %d  blocks/CU %d  %7.3f ms  read %6.0f GB/s  read+write %6.0f GB/s\n", MODE, bpc, ms,
-           rb / (ms * 1e-3) / 1e9, (rb + wb) / (ms * 1e-3) / 1e9);
+    printf("mode %d  blocks/CU %d  P %4u W %3u  %7.3f ms  read %6.0f GB/s  read+write %6.0f GB/s\n", MODE, bpc, P, W,
+           ms, rb / (ms * 1e-3) / 1e9, (rb + wb) / (ms * 1e-3) / 1e9);
 }
 
 int main() {
@@ -108,12 +125,12 @@ int main() {
     (void)hipMemset(dst, 0, wbytes);
     (void)hipDeviceSynchronize();
     for (int rep = 0; rep < 2; ++rep)
-        for (int bpc : {2, 3}) {
+        for (int bpc : {2}) {
             run<0>(src, groups, dst, out, bpc);
             run<1>(src, groups, dst, out, bpc);
-            run<2>(src, groups, dst, out, bpc);
             run<3>(src, groups, dst, out, bpc);
-            run<4>(src, groups, dst, out, bpc);
+            for (uint32_t P : {500u, 1000u, 2000u, 4000u})
+                for (uint32_t W : {P / 20, P / 10, P / 5}) run<5>(src, groups, dst, out, bpc, P, W);
         }
     (void)hipFree(src);
     (void)hipFree(dst);
