@@ -236,7 +236,11 @@ int iris_engine_destroy(iris_engine_t *engine);
 int iris_engine_batch_process(iris_engine_t *engine, const iris_db_t *db, uint64_t first, uint64_t n,
                               uint16_t *out);
 /* As iris_engine_batch_process, with out_device a DEVICE array of n*31
- * uint16_t (for pipelines that keep the results on the GPU). */
+ * uint16_t (for pipelines that keep the results on the GPU).  Blocking: when
+ * it returns the rows are in device memory, visible to any reader (another
+ * stream, a copy engine, another process's mapping) -- a participant-sized
+ * range returns on a completion word its kernel writes after storing the rows
+ * through L2, before the launch itself has retired. */
 int iris_engine_batch_process_device(iris_engine_t *engine, const iris_db_t *db, uint64_t first, uint64_t n,
                                      uint16_t *out_device);
 /* Host-slice form with exactly the reference signature: `db` is a host array

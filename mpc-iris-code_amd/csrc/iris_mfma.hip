@@ -79,8 +79,10 @@ __device__ __forceinline__ void chunk_step(uint32_t x0, uint32_t x1, const QFrag
 #define IRIS_MFMA_DIAG 0
 #endif
     // diagnostic builds only (tools/, results wrong by design): 1 = no den MFMA, 2 = no
-    // MFMAs (operands kept live by an empty asm), 3 = no operand expansion (raw dwords)
-    if constexpr (IRIS_MFMA_DIAG == 0) {
+    // MFMAs (operands kept live by an empty asm), 3 = no operand expansion (raw dwords);
+    // 4 = the shipped arithmetic, but a search's dist_out receives each workgroup's timeline
+    // (start / end of the constant-rate clock, XCD id: 3 u64 per workgroup) instead of distances
+    if constexpr (IRIS_MFMA_DIAG == 0 || IRIS_MFMA_DIAG == 4) {
         den = mfma_fp4(q.am, bm, den);
         s = mfma_fp4(q.ae, be, s);
     } else if constexpr (IRIS_MFMA_DIAG == 1) {
@@ -116,6 +118,7 @@ __global__ void __launch_bounds__(256, kMfmaWgs)
                          uint16_t *__restrict__ den_out, double *__restrict__ dist_out,
                          Partial *__restrict__ partials, FusedFinish fin) {
     static_assert(KS == 1 || (kWaveSlots % KS == 0 && kPlaneGroups % KS == 0), "K-split geometry");
+    const uint64_t diag_t0 = IRIS_MFMA_DIAG == 4 ? __builtin_amdgcn_s_memrealtime() : 0;
     const int lane = threadIdx.x & 63;
     const int wslot = threadIdx.x >> 6;
     const int slice = wslot % KS;
@@ -252,7 +255,7 @@ __global__ void __launch_bounds__(256, kMfmaWgs)
                 dd = (uint32_t)den[t][r];
                 nn = (uint32_t)(((int)dd - (int)s[t][r]) >> 1);  // num = (den - S) / 2
             }, bn, bd, br);
-            if (valid && dist_out && h == 0) dist_out[o] = bd ? (double)bn / (double)bd : __builtin_inf();
+            if (IRIS_MFMA_DIAG != 4 && valid && dist_out && h == 0) dist_out[o] = bd ? (double)bn / (double)bd : __builtin_inf();
             Partial c;
             c.num = bn;
             c.den = valid ? bd : 0;
@@ -277,8 +280,168 @@ __global__ void __launch_bounds__(256, kMfmaWgs)
             for (int w = 1; w < kWaveSlots; ++w)
                 if (partial_better_dev(sh[w], b)) b = sh[w];
             if constexpr (!FUSED) partials[blockIdx.x] = b;
+            if (IRIS_MFMA_DIAG == 4 && dist_out) {
+                uint32_t xcc;
+                asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+                uint64_t *tl = (uint64_t *)dist_out + 3 * (uint64_t)blockIdx.x;
+                tl[0] = diag_t0;
+                tl[1] = __builtin_amdgcn_s_memrealtime();
+                tl[2] = xcc;
+            }
         }
         if constexpr (FUSED) fold_partials_last(partials, b, fin);
+    }
+}
+
+// ------------------------------------------------------------------ persistent search (large ranges)
+//
+// A grid that launches every workgroup the chip holds at once (kMfmaWgs per CU) and keeps it: each
+// wave takes its next unit of T tiles from a work counter (one agent-scope atomic add per unit, by
+// lane 0), fetched one unit AHEAD, so the 3-stage load pipeline streams on across the unit boundary
+// and the unit's epilogue overlaps the next unit's loads.  Why: with one short-lived workgroup per
+// 16 tiles (template_mfma_kernel), the per-workgroup timeline of a 10M search
+// (tools/search_timeline.py, -DIRIS_MFMA_DIAG=4) held only ~88 % of the 512 workgroup slots busy on
+// average -- workgroups are dealt to the XCDs in order, so a slot that frees on one XCD waits while
+// the next workgroup in line is bound for a full one -- and the XCDs finished 100-200 us apart.
+// Dynamic units fill every slot until the counter runs out, on every XCD alike.  Each wave folds its
+// units' winners into a running best (exact fraction, then lowest index: a total order, so the
+// order the units arrive in does not matter); one partial per workgroup.  *work must be 0 at launch
+// (the launcher clears it on the stream).
+#ifndef IRIS_SEARCH_DYN
+#define IRIS_SEARCH_DYN 1  // 0: large ranges launch template_mfma_kernel (one workgroup per 16 tiles)
+#endif
+template <int T = kMfmaTiles>
+__global__ void __launch_bounds__(256, kMfmaWgs)
+    template_search_dyn_kernel(const uint4 *__restrict__ db, const uint4 *__restrict__ qfrag, uint64_t tile0,
+                               uint64_t ntiles, uint64_t first, uint64_t end, double *__restrict__ dist_out,
+                               Partial *__restrict__ partials, uint32_t *__restrict__ work) {
+    constexpr int kG = kPlaneGroups;  // 100 steps of 2 chunks per unit
+    const int lane = threadIdx.x & 63;
+    const int wslot = threadIdx.x >> 6;
+    const uint32_t units = (uint32_t)((ntiles + T - 1) / T);
+#if IRIS_SEARCH_DYN == 2
+    auto fetch = [&]() -> uint32_t {
+        uint32_t u = 0;
+        if (lane == 0) u = __hip_atomic_fetch_add(work, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return __builtin_amdgcn_readfirstlane(u);
+    };
+#else  // static: wave w takes units w, w + nwaves, ... (no counter)
+    const uint32_t nwaves = gridDim.x * kWaveSlots;
+    uint32_t ticket = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaveSlots + wslot);
+    auto fetch = [&]() -> uint32_t {
+        const uint32_t u = ticket;
+        ticket += nwaves;
+        return u;
+    };
+#endif
+    uint32_t cur = fetch();
+    uint32_t nxt = cur < units ? fetch() : units;
+    Partial best = partial_none();
+    if (cur < units) {
+        v16f den[T], sm[T];
+        auto zero = [&] {
+#pragma unroll
+            for (int t = 0; t < T; ++t)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    den[t][i] = 0.f;
+                    sm[t][i] = 0.f;
+                }
+        };
+        zero();
+        const uint4 *qp = qfrag + lane;
+        struct Stage {
+            uint4 d[T];
+            uint4 q0, q1;
+        };
+        // step s of this wave's walk: unit ucur covers steps [s_unit, s_unit + kG); a load at most two
+        // steps ahead falls in ucur or in the prefetched unit nxt (past the last unit: ucur's last
+        // step again, never consumed)
+        uint32_t s_unit = 0;
+        auto load = [&](Stage &st, uint32_t step) {
+            uint32_t u = cur, g = step - s_unit;
+            if (g >= (uint32_t)kG) {
+                if (nxt < units) {
+                    u = nxt;
+                    g -= kG;
+                } else {
+                    g = kG - 1;
+                }
+            }
+#pragma unroll
+            for (int t = 0; t < T; ++t) {
+                const uint64_t rel = (uint64_t)u * T + t < ntiles ? (uint64_t)u * T + t : ntiles - 1;
+                st.d[t] = stream_load(db + (tile0 + rel) * (uint64_t)kTileUint4 + g * 64 + lane);
+            }
+            st.q0 = qp[(2 * g) * 64];
+            st.q1 = qp[(2 * g + 1) * 64];
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        // after the wave's last unit, cur >= units: the (at most two) steps still computed add into
+        // zeroed accumulators nobody reads
+        auto compute = [&](const Stage &st, uint32_t step) {
+            const QFrag f0 = qfrag_of(st.q0);
+#pragma unroll
+            for (int t = 0; t < T; ++t) chunk_step(st.d[t].x, st.d[t].y, f0, den[t], sm[t]);
+            const QFrag f1 = qfrag_of(st.q1);
+#pragma unroll
+            for (int t = 0; t < T; ++t) chunk_step(st.d[t].z, st.d[t].w, f1, den[t], sm[t]);
+            if (step - s_unit != (uint32_t)kG - 1) return;
+            // unit done: its tiles' winners into the running best, then the next unit
+            const int h = lane >> 5;
+#pragma unroll
+            for (int t = 0; t < T; ++t) {
+                const uint64_t tile = (uint64_t)cur * T + t;
+                const uint64_t tg = (tile0 + tile) * kTileRecs + (lane & 31);
+                const bool valid = tile < ntiles && tg >= first && tg < end;
+                uint32_t bn, bd;
+                int br;
+                best_rotation(lane, [&](int r, uint32_t &nn, uint32_t &dd) {
+                    dd = (uint32_t)den[t][r];
+                    nn = (uint32_t)(((int)dd - (int)sm[t][r]) >> 1);  // num = (den - S) / 2
+                }, bn, bd, br);
+                if (valid && dist_out && h == 0) dist_out[tg - first] = bd ? (double)bn / (double)bd : __builtin_inf();
+                Partial c;
+                c.num = bn;
+                c.den = valid ? bd : 0;
+                c.rot = br;
+                c.pad = 0;
+                c.idx = tg - first;
+                if (partial_better_dev(c, best)) best = c;
+            }
+            zero();
+            s_unit += kG;
+            cur = nxt;
+            if (cur < units) nxt = fetch();
+        };
+        Stage sa, sb, sc;
+        load(sa, 0);
+        load(sb, 1);
+#pragma unroll 1
+        for (uint32_t step = 0;; step += 3) {
+            load(sc, step + 2);
+            compute(sa, step);
+            load(sa, step + 3);
+            compute(sb, step + 1);
+            load(sb, step + 4);
+            compute(sc, step + 2);
+            if (cur >= units) break;  // set by compute at the wave's last unit end
+        }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const Partial o = partial_shfl_xor(best, off);
+        if (partial_better_dev(o, best)) best = o;
+    }
+    __shared__ Partial sh[kWaveSlots];
+    if (lane == 0) sh[wslot] = best;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        Partial b = sh[0];
+#pragma unroll
+        for (int w = 1; w < kWaveSlots; ++w)
+            if (partial_better_dev(sh[w], b)) b = sh[w];
+        partials[blockIdx.x] = b;
     }
 }
 
@@ -510,6 +673,7 @@ struct TileRange {
     uint64_t tile0, ntiles, grid;
     int tiles_per_wave;
     int ksplit;  // 4: a tile's 4 waves split K (ranges of at most kSplitTiles tiles)
+    bool dyn;    // persistent search grid (template_search_dyn_kernel): grid = resident workgroups
 };
 
 // Below this many tiles, 4 tiles per wave would leave CUs idle (fewer than 2
@@ -540,10 +704,25 @@ static TileRange tile_range(const Hooks &h, LaunchRange r) {
     }
     const uint64_t waves = (t.ntiles + t.tiles_per_wave - 1) / t.tiles_per_wave;
     t.grid = (waves + kWaveSlots - 1) / kWaveSlots;
+    t.dyn = false;
     return t;
 }
 
-uint32_t mfma_search_partials(const Hooks &h, LaunchRange r) { return (uint32_t)tile_range(h, r).grid; }
+// the search's form of tile_range: ranges of 4 tiles per wave that would take more workgroups than
+// the chip holds at once run the persistent kernel on exactly that many
+static TileRange search_range(const Hooks &h, LaunchRange r) {
+    TileRange t = tile_range(h, r);
+    t.dyn = IRIS_SEARCH_DYN && t.ksplit == 1 && t.tiles_per_wave == kMfmaTiles &&
+            t.grid > (uint64_t)resident_blocks(kMfmaWgs);
+    if (t.dyn) t.grid = resident_blocks(kMfmaWgs);
+    return t;
+}
+
+// partial records a search writes; the persistent form keeps its work counter one record further
+uint32_t mfma_search_partials(const Hooks &h, LaunchRange r) {
+    const TileRange t = search_range(h, r);
+    return (uint32_t)t.grid + (t.dyn ? 1u : 0u);
+}
 
 uint32_t multi_search_partials(LaunchRange r, int nq) {
     const uint64_t tile0 = r.first / kTileRecs, tile1 = (r.first + r.n + kTileRecs - 1) / kTileRecs;
@@ -578,11 +757,19 @@ int launch_template_mfma_counts(const Hooks &h, void *stream, const void *db, co
 
 int launch_template_mfma_search(const Hooks &h, void *stream, const void *db, const void *qfrag, LaunchRange r, double *dist_out,
                                 Partial *partials, uint32_t *n_partials, const FusedFinish *fin) {
-    const TileRange t = tile_range(h, r);
+    const TileRange t = search_range(h, r);
     *n_partials = (uint32_t)t.grid;
     if (r.n == 0) return 0;
-    const bool fused = fin && t.grid <= kFusedReduceMax;
+    const bool fused = fin && t.grid <= kFusedReduceMax && !t.dyn;
     if (fin && !fused) return -1;  // the caller asks fused_search_ok() first
+    if (t.dyn) {
+        uint32_t *work = (uint32_t *)(partials + t.grid);
+        if (hipMemsetAsync(work, 0, sizeof(uint32_t), (hipStream_t)stream) != hipSuccess) return -1;
+        hipLaunchKernelGGL(template_search_dyn_kernel<kMfmaTiles>, dim3((uint32_t)t.grid), dim3(256), 0,
+                           (hipStream_t)stream, (const uint4 *)db, (const uint4 *)qfrag, t.tile0, t.ntiles, r.first,
+                           r.first + r.n, dist_out, partials, work);
+        return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
     auto kern = fused ? (t.ksplit > 1 ? template_mfma_kernel<MF_SEARCH, kSplitT, 4, true>
                          : t.tiles_per_wave == 1 ? template_mfma_kernel<MF_SEARCH, 1, 1, true>
                                                  : template_mfma_kernel<MF_SEARCH, kMfmaTiles, 1, true>)
@@ -597,7 +784,9 @@ int launch_template_mfma_search(const Hooks &h, void *stream, const void *db, co
 // test hook: IRIS_FUSED_REDUCE=0 runs small searches with the separate reduce kernel
 bool fused_search_ok(const Hooks &h, LaunchRange r) {
     if (!h.fused_reduce) return false;
-    return r.n > 0 && tile_range(h, r).grid <= kFusedReduceMax;
+    if (r.n == 0) return false;
+    const TileRange t = search_range(h, r);
+    return !t.dyn && t.grid <= kFusedReduceMax;
 }
 
 }  // namespace iris

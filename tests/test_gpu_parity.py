@@ -743,3 +743,32 @@ def test_calls_keep_the_callers_current_device(device):
     th.start()
     th.join()
     assert not errors
+
+
+def test_persistent_search_ranges_vs_oracle(device):
+    """Ranges of more than 8192 tiles run the persistent search kernel (template_search_dyn_kernel:
+    one grid of resident workgroups, each wave walking 4-tile units until the range runs out).
+    Against the oracle on every template: the full database, a range ragged at both ends (neither
+    end on a tile), and a mid-database range whose unit count leaves the last round of waves
+    partly idle; distances bit for bit, and the winner with a planted tie far apart in the range
+    (equal fractions: the lower index must win, whichever wave holds which)."""
+    n = 300_007
+    seed = 20260417
+    recs = oc.gen_templates(seed, 0, n)
+    q = oc.gen_templates(seed + 1, 0, 1)[0]
+    near = oc.bits_rotated(q[:200], 7)
+    twin = np.concatenate([near ^ np.uint64(0x0101), oc.bits_rotated(q[200:], 7)])
+    for pos in (12_345, 287_001, 150_000):
+        recs[pos] = twin
+    with ih.Database(device, ih.KIND_TEMPLATES, n) as db:
+        db.append(recs)
+        want = oc.template_distances(q, recs)
+        with ih.TemplateEngine(device, q) as eng:
+            for first, m in ((0, n), (13, n - 13 - 5), (1_000, 270_001)):
+                d = eng.distances(db, first=first, n=m)
+                assert bits_eq(d, want[first:first + m]), (first, m)
+                got = eng.search(db, first=first, n=m, index_base=7)
+                best, idx = oc.argmin(want[first:first + m])
+                assert got.index == 7 + first + idx and bits_eq(got.distance, best), (first, m, got)
+            assert eng.search(db).index == 12_345
+            assert eng.search(db, first=13_000, n=n - 13_000).index == 150_000
