@@ -111,18 +111,20 @@ enum { MF_COUNTS = 0, MF_SEARCH = 1 };
 // a few hundred tiles still puts several waves on every SIMD.
 // FUSED (search, small grids): the last workgroup to finish folds every workgroup's
 // partial and writes the winner to fin.dst itself (iris_device.hpp, fold_partials_last).
-template <int MODE, int T = kMfmaTiles, int KS = 1, bool FUSED = false>
-__global__ void __launch_bounds__(256, kMfmaWgs)
+// W: waves per workgroup (IRIS_SEARCH_WG_WAVES = 8 for large searches: one 8-wave workgroup per CU,
+// all of whose waves start at the same K step and share the query fragments in L1)
+template <int MODE, int T = kMfmaTiles, int KS = 1, bool FUSED = false, int W = kWaveSlots>
+__global__ void __launch_bounds__(64 * W, kMfmaWgs * kWaveSlots / W)
     template_mfma_kernel(const uint4 *__restrict__ db, const uint4 *__restrict__ qfrag, uint64_t tile0,
                          uint64_t ntiles, uint64_t first, uint64_t end, uint16_t *__restrict__ num_out,
                          uint16_t *__restrict__ den_out, double *__restrict__ dist_out,
                          Partial *__restrict__ partials, FusedFinish fin) {
-    static_assert(KS == 1 || (kWaveSlots % KS == 0 && kPlaneGroups % KS == 0), "K-split geometry");
+    static_assert(KS == 1 || (W % KS == 0 && kPlaneGroups % KS == 0), "K-split geometry");
     const uint64_t diag_t0 = IRIS_MFMA_DIAG == 4 ? __builtin_amdgcn_s_memrealtime() : 0;
     const int lane = threadIdx.x & 63;
     const int wslot = threadIdx.x >> 6;
     const int slice = wslot % KS;
-    const uint64_t wave = (uint64_t)blockIdx.x * (kWaveSlots / KS) + wslot / KS;
+    const uint64_t wave = (uint64_t)blockIdx.x * (W / KS) + wslot / KS;
     const uint64_t tw = wave * T;  // first tile (relative to tile0) of this wave
     const bool active = tw < ntiles;  // wave-uniform
     constexpr int kG = kPlaneGroups / KS;  // chunk groups of this wave's K-slice
@@ -152,8 +154,14 @@ __global__ void __launch_bounds__(256, kMfmaWgs)
             uint4 d[T];
             uint4 q0, q1;
         };
+#ifndef IRIS_SEARCH_KROT
+#define IRIS_SEARCH_KROT 0  // 1: each wave walks K from its own starting step (order of exact integer sums: free)
+#endif
+        const int krot = (IRIS_SEARCH_KROT && KS == 1) ? (int)((wave * 37) % kG) : 0;
         auto load = [&](Stage &st, int g) {
-            g = g0 + (g < kG ? g : kG - 1);
+            g = g < kG ? g : kG - 1;
+            if (IRIS_SEARCH_KROT && KS == 1) g = g + krot >= kG ? g + krot - kG : g + krot;
+            g += g0;
 #pragma unroll
             for (int t = 0; t < T; ++t) st.d[t] = stream_load(dp[t] + g * 64);
             st.q0 = qp[(2 * g) * 64];
@@ -204,7 +212,7 @@ __global__ void __launch_bounds__(256, kMfmaWgs)
         }
     }
     if constexpr (KS > 1) {  // the K-slices' partial sums -> slice 0's accumulators (exact)
-        __shared__ float red[kWaveSlots][T][32][64];
+        __shared__ float red[W][T][32][64];
         if (slice != 0) {
 #pragma unroll
             for (int t = 0; t < T; ++t)
@@ -237,7 +245,7 @@ __global__ void __launch_bounds__(256, kMfmaWgs)
         const uint64_t t0 = (tile0 + tw + t) * kTileRecs;  // global index of the tile's first template
         const bool tv = active && (tw + t < ntiles) && slice == 0;
         if constexpr (MODE == MF_COUNTS) {
-            __shared__ __attribute__((aligned(16))) uint16_t sh_out[kWaveSlots][1024];
+            __shared__ __attribute__((aligned(16))) uint16_t sh_out[W][1024];
             uint16_t *lds = sh_out[wslot];
             if (num_out)
                 store_tile_rows(num_out, lds, t0, first, end, tv, lane,
@@ -271,13 +279,13 @@ __global__ void __launch_bounds__(256, kMfmaWgs)
             const Partial ot = partial_shfl_xor(best, off);
             if (partial_better_dev(ot, best)) best = ot;
         }
-        __shared__ Partial sh[kWaveSlots];
+        __shared__ Partial sh[W];
         if (lane == 0) sh[wslot] = best;
         __syncthreads();
         Partial b = sh[0];
         if (threadIdx.x == 0) {
 #pragma unroll
-            for (int w = 1; w < kWaveSlots; ++w)
+            for (int w = 1; w < W; ++w)
                 if (partial_better_dev(sh[w], b)) b = sh[w];
             if constexpr (!FUSED) partials[blockIdx.x] = b;
             if (IRIS_MFMA_DIAG == 4 && dist_out) {
@@ -308,7 +316,7 @@ __global__ void __launch_bounds__(256, kMfmaWgs)
 // order the units arrive in does not matter); one partial per workgroup.  *work must be 0 at launch
 // (the launcher clears it on the stream).
 #ifndef IRIS_SEARCH_DYN
-#define IRIS_SEARCH_DYN 1  // 0: large ranges launch template_mfma_kernel (one workgroup per 16 tiles)
+#define IRIS_SEARCH_DYN 0  // 1: static units, 2: units from a work counter; 0: one workgroup per 16 tiles
 #endif
 template <int T = kMfmaTiles>
 __global__ void __launch_bounds__(256, kMfmaWgs)
@@ -318,8 +326,12 @@ __global__ void __launch_bounds__(256, kMfmaWgs)
     constexpr int kG = kPlaneGroups;  // 100 steps of 2 chunks per unit
     const int lane = threadIdx.x & 63;
     const int wslot = threadIdx.x >> 6;
-    const uint32_t units = (uint32_t)((ntiles + T - 1) / T);
-#if IRIS_SEARCH_DYN == 2
+#ifndef IRIS_SEARCH_UNIT
+#define IRIS_SEARCH_UNIT 1  // sub-units of T tiles per fetched unit
+#endif
+    constexpr uint32_t H = IRIS_SEARCH_UNIT;
+    const uint32_t units = (uint32_t)((ntiles + T - 1) / T);  // sub-units of T tiles
+#if IRIS_SEARCH_DYN >= 2
     auto fetch = [&]() -> uint32_t {
         uint32_t u = 0;
         if (lane == 0) u = __hip_atomic_fetch_add(work, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -334,8 +346,44 @@ __global__ void __launch_bounds__(256, kMfmaWgs)
         return u;
     };
 #endif
-    uint32_t cur = fetch();
-    uint32_t nxt = cur < units ? fetch() : units;
+#if IRIS_SEARCH_DYN == 3
+    // guided: the counter counts sub-units; a wave claims a block sized by what it last saw remain
+    // (large blocks early: few counter round trips, each of which drains the wave's load queue;
+    // single sub-units at the end: a short, balanced tail)
+    const uint32_t nw = gridDim.x * kWaveSlots;
+    uint32_t seen = 0, cur_end = 0, nxt_end = 0;
+    auto claim = [&]() -> uint32_t {
+        const uint32_t rem = units > seen ? units - seen : 0;
+        const uint32_t sz = min(max(rem / (2 * nw), 1u), (uint32_t)IRIS_SEARCH_UNIT);
+        uint32_t b = 0;
+        if (lane == 0) b = __hip_atomic_fetch_add(work, sz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        b = __builtin_amdgcn_readfirstlane(b);
+        seen = b + sz;
+        nxt_end = min(b + sz, units);
+        return b < units ? b : units;
+    };
+    auto after = [&](uint32_t c) -> uint32_t {
+        if (c + 1 < cur_end) {
+            nxt_end = cur_end;
+            return c + 1;
+        }
+        return claim();
+    };
+    uint32_t cur = claim();
+    cur_end = nxt_end;
+    uint32_t nxt = cur < units ? after(cur) : units;
+#else
+    // cur / nxt: sub-units (T tiles); a fetch hands out H consecutive ones
+    auto fetch_sub = [&]() -> uint32_t {
+        const uint32_t u = fetch();
+        return u < (units + H - 1) / H ? u * H : units;
+    };
+    auto after = [&](uint32_t c) -> uint32_t {  // the sub-unit a wave takes after c
+        return (c % H != H - 1 && c + 1 < units) ? c + 1 : fetch_sub();
+    };
+    uint32_t cur = fetch_sub();
+    uint32_t nxt = cur < units ? after(cur) : units;
+#endif
     Partial best = partial_none();
     if (cur < units) {
         v16f den[T], sm[T];
@@ -358,6 +406,7 @@ __global__ void __launch_bounds__(256, kMfmaWgs)
         // steps ahead falls in ucur or in the prefetched unit nxt (past the last unit: ucur's last
         // step again, never consumed)
         uint32_t s_unit = 0;
+        const uint32_t krot = IRIS_SEARCH_KROT ? (uint32_t)((blockIdx.x * kWaveSlots + wslot) * 37u % kG) : 0u;
         auto load = [&](Stage &st, uint32_t step) {
             uint32_t u = cur, g = step - s_unit;
             if (g >= (uint32_t)kG) {
@@ -368,6 +417,7 @@ __global__ void __launch_bounds__(256, kMfmaWgs)
                     g = kG - 1;
                 }
             }
+            if (IRIS_SEARCH_KROT) g = g + krot >= (uint32_t)kG ? g + krot - kG : g + krot;
 #pragma unroll
             for (int t = 0; t < T; ++t) {
                 const uint64_t rel = (uint64_t)u * T + t < ntiles ? (uint64_t)u * T + t : ntiles - 1;
@@ -412,7 +462,10 @@ __global__ void __launch_bounds__(256, kMfmaWgs)
             zero();
             s_unit += kG;
             cur = nxt;
-            if (cur < units) nxt = fetch();
+#if IRIS_SEARCH_DYN == 3
+            cur_end = nxt_end;
+#endif
+            if (cur < units) nxt = after(cur);
         };
         Stage sa, sb, sc;
         load(sa, 0);
@@ -426,6 +479,144 @@ __global__ void __launch_bounds__(256, kMfmaWgs)
             load(sb, step + 4);
             compute(sc, step + 2);
             if (cur >= units) break;  // set by compute at the wave's last unit end
+        }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        const Partial o = partial_shfl_xor(best, off);
+        if (partial_better_dev(o, best)) best = o;
+    }
+    __shared__ Partial sh[kWaveSlots];
+    if (lane == 0) sh[wslot] = best;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        Partial b = sh[0];
+#pragma unroll
+        for (int w = 1; w < kWaveSlots; ++w)
+            if (partial_better_dev(sh[w], b)) b = sh[w];
+        partials[blockIdx.x] = b;
+    }
+}
+
+// IRIS_SEARCH_DYN == 4: persistent, WORKGROUP units of kWaveSlots x T tiles (wave w takes tiles
+// [u kWaveSlots T + w T, +T)) from the work counter, the 4 waves kept in step by one s_barrier per
+// unit (their query-fragment reads, at the same K step, share the CU's L1: waves that drift apart
+// -- the per-wave units above -- or start K at different steps measured 2-9 % slower,
+// profiles/r04_search_persistent.txt).  Lane 0 of wave 0 fetches unit i + 2 at the start of unit i
+// into a 3-slot LDS ring, so every wave knows the next unit two steps before it needs it.
+template <int T = kMfmaTiles>
+__global__ void __launch_bounds__(256, kMfmaWgs)
+    template_search_wg_kernel(const uint4 *__restrict__ db, const uint4 *__restrict__ qfrag, uint64_t tile0,
+                              uint64_t ntiles, uint64_t first, uint64_t end, double *__restrict__ dist_out,
+                              Partial *__restrict__ partials, uint32_t *__restrict__ work) {
+    constexpr int kG = kPlaneGroups;
+    const int lane = threadIdx.x & 63;
+    const int wslot = threadIdx.x >> 6;
+    const uint32_t units = (uint32_t)((ntiles + (uint64_t)T * kWaveSlots - 1) / ((uint64_t)T * kWaveSlots));
+    __shared__ uint32_t ring[3];
+    auto barrier = [] {
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): LDS writes landed; the stream's loads stay in flight
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    };
+    if (threadIdx.x == 0) {
+        ring[0] = __hip_atomic_fetch_add(work, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ring[1] = __hip_atomic_fetch_add(work, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    barrier();
+    uint32_t cur = ring[0], nxt = ring[1], ord = 0;  // ord: this workgroup's unit ordinal
+    Partial best = partial_none();
+    if (cur < units) {
+        v16f den[T], sm[T];
+        auto zero = [&] {
+#pragma unroll
+            for (int t = 0; t < T; ++t)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    den[t][i] = 0.f;
+                    sm[t][i] = 0.f;
+                }
+        };
+        zero();
+        const uint4 *qp = qfrag + lane;
+        struct Stage {
+            uint4 d[T];
+            uint4 q0, q1;
+        };
+        uint32_t s_unit = 0;
+        auto tile_of = [&](uint32_t u, int t) -> uint64_t {
+            const uint64_t tile = ((uint64_t)u * kWaveSlots + wslot) * T + t;
+            return tile < ntiles ? tile : ntiles - 1;
+        };
+        auto load = [&](Stage &st, uint32_t step) {
+            uint32_t u = cur, g = step - s_unit;
+            if (g >= (uint32_t)kG) {
+                if (nxt < units) {
+                    u = nxt;
+                    g -= kG;
+                } else {
+                    g = kG - 1;
+                }
+            }
+#pragma unroll
+            for (int t = 0; t < T; ++t) st.d[t] = stream_load(db + (tile0 + tile_of(u, t)) * (uint64_t)kTileUint4 + g * 64 + lane);
+            st.q0 = qp[(2 * g) * 64];
+            st.q1 = qp[(2 * g + 1) * 64];
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        auto compute = [&](const Stage &st, uint32_t step) {
+            const QFrag f0 = qfrag_of(st.q0);
+#pragma unroll
+            for (int t = 0; t < T; ++t) chunk_step(st.d[t].x, st.d[t].y, f0, den[t], sm[t]);
+            const QFrag f1 = qfrag_of(st.q1);
+#pragma unroll
+            for (int t = 0; t < T; ++t) chunk_step(st.d[t].z, st.d[t].w, f1, den[t], sm[t]);
+            const uint32_t g = step - s_unit;
+            if (g == 0 && threadIdx.x == 0)  // the unit after next, into the ring
+                ring[(ord + 2) % 3] = nxt < units ? __hip_atomic_fetch_add(work, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                                  : units;
+            if (g != (uint32_t)kG - 1) return;
+            const int h = lane >> 5;
+#pragma unroll
+            for (int t = 0; t < T; ++t) {
+                const uint64_t tile = ((uint64_t)cur * kWaveSlots + wslot) * T + t;
+                const uint64_t tg = (tile0 + tile) * kTileRecs + (lane & 31);
+                const bool valid = tile < ntiles && tg >= first && tg < end;
+                uint32_t bn, bd;
+                int br;
+                best_rotation(lane, [&](int r, uint32_t &nn, uint32_t &dd) {
+                    dd = (uint32_t)den[t][r];
+                    nn = (uint32_t)(((int)dd - (int)sm[t][r]) >> 1);  // num = (den - S) / 2
+                }, bn, bd, br);
+                if (valid && dist_out && h == 0) dist_out[tg - first] = bd ? (double)bn / (double)bd : __builtin_inf();
+                Partial c;
+                c.num = bn;
+                c.den = valid ? bd : 0;
+                c.rot = br;
+                c.pad = 0;
+                c.idx = tg - first;
+                if (partial_better_dev(c, best)) best = c;
+            }
+            zero();
+            barrier();  // the workgroup's waves leave the unit together; ring[(ord + 2) % 3] is written
+            s_unit += kG;
+            cur = nxt;
+            ++ord;
+            nxt = cur < units ? ring[(ord + 1) % 3] : units;
+        };
+        Stage sa, sb, sc;
+        load(sa, 0);
+        load(sb, 1);
+#pragma unroll 1
+        for (uint32_t step = 0;; step += 3) {
+            load(sc, step + 2);
+            compute(sa, step);
+            load(sa, step + 3);
+            compute(sb, step + 1);
+            load(sb, step + 4);
+            compute(sc, step + 2);
+            if (cur >= units) break;
         }
     }
 #pragma unroll
@@ -669,8 +860,13 @@ int launch_generate_tiles(void *stream, void *db, uint64_t t_first, uint64_t n, 
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+#ifndef IRIS_SEARCH_WG_WAVES
+#define IRIS_SEARCH_WG_WAVES 4
+#endif
 struct TileRange {
     uint64_t tile0, ntiles, grid;
+    int wg_waves = kWaveSlots;  // waves per workgroup of the plain search grid
+    bool fusable = false;       // small enough for the in-kernel reduce (4-wave workgroups)
     int tiles_per_wave;
     int ksplit;  // 4: a tile's 4 waves split K (ranges of at most kSplitTiles tiles)
     bool dyn;    // persistent search grid (template_search_dyn_kernel): grid = resident workgroups
@@ -712,6 +908,11 @@ static TileRange tile_range(const Hooks &h, LaunchRange r) {
 // the chip holds at once run the persistent kernel on exactly that many
 static TileRange search_range(const Hooks &h, LaunchRange r) {
     TileRange t = tile_range(h, r);
+    t.fusable = t.grid <= (uint64_t)kFusedReduceMax;
+    if (IRIS_SEARCH_WG_WAVES != kWaveSlots && t.ksplit == 1 && t.tiles_per_wave == kMfmaTiles && !t.fusable) {  // large ranges only: the fused small-range forms keep 4 waves
+        t.wg_waves = IRIS_SEARCH_WG_WAVES;
+        t.grid = (t.ntiles + (uint64_t)kMfmaTiles * t.wg_waves - 1) / ((uint64_t)kMfmaTiles * t.wg_waves);
+    }
     t.dyn = IRIS_SEARCH_DYN && t.ksplit == 1 && t.tiles_per_wave == kMfmaTiles &&
             t.grid > (uint64_t)resident_blocks(kMfmaWgs);
     if (t.dyn) t.grid = resident_blocks(kMfmaWgs);
@@ -760,14 +961,19 @@ int launch_template_mfma_search(const Hooks &h, void *stream, const void *db, co
     const TileRange t = search_range(h, r);
     *n_partials = (uint32_t)t.grid;
     if (r.n == 0) return 0;
-    const bool fused = fin && t.grid <= kFusedReduceMax && !t.dyn;
+    const bool fused = fin && t.fusable && !t.dyn;
     if (fin && !fused) return -1;  // the caller asks fused_search_ok() first
     if (t.dyn) {
         uint32_t *work = (uint32_t *)(partials + t.grid);
         if (hipMemsetAsync(work, 0, sizeof(uint32_t), (hipStream_t)stream) != hipSuccess) return -1;
-        hipLaunchKernelGGL(template_search_dyn_kernel<kMfmaTiles>, dim3((uint32_t)t.grid), dim3(256), 0,
-                           (hipStream_t)stream, (const uint4 *)db, (const uint4 *)qfrag, t.tile0, t.ntiles, r.first,
-                           r.first + r.n, dist_out, partials, work);
+        if (IRIS_SEARCH_DYN == 4)
+            hipLaunchKernelGGL(template_search_wg_kernel<kMfmaTiles>, dim3((uint32_t)t.grid), dim3(256), 0,
+                               (hipStream_t)stream, (const uint4 *)db, (const uint4 *)qfrag, t.tile0, t.ntiles, r.first,
+                               r.first + r.n, dist_out, partials, work);
+        else
+            hipLaunchKernelGGL(template_search_dyn_kernel<kMfmaTiles>, dim3((uint32_t)t.grid), dim3(256), 0,
+                               (hipStream_t)stream, (const uint4 *)db, (const uint4 *)qfrag, t.tile0, t.ntiles, r.first,
+                               r.first + r.n, dist_out, partials, work);
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
     auto kern = fused ? (t.ksplit > 1 ? template_mfma_kernel<MF_SEARCH, kSplitT, 4, true>
@@ -775,7 +981,8 @@ int launch_template_mfma_search(const Hooks &h, void *stream, const void *db, co
                                                  : template_mfma_kernel<MF_SEARCH, kMfmaTiles, 1, true>)
                       : (t.ksplit > 1 ? template_mfma_kernel<MF_SEARCH, kSplitT, 4>
                          : t.tiles_per_wave == 1 ? template_mfma_kernel<MF_SEARCH, 1> : template_mfma_kernel<MF_SEARCH>);
-    hipLaunchKernelGGL(kern, dim3((uint32_t)t.grid), dim3(256), 0, (hipStream_t)stream,
+    if (t.wg_waves != kWaveSlots) kern = template_mfma_kernel<MF_SEARCH, kMfmaTiles, 1, false, IRIS_SEARCH_WG_WAVES>;
+    hipLaunchKernelGGL(kern, dim3((uint32_t)t.grid), dim3(64 * t.wg_waves), 0, (hipStream_t)stream,
                        (const uint4 *)db, (const uint4 *)qfrag, t.tile0, t.ntiles, r.first, r.first + r.n,
                        (uint16_t *)nullptr, (uint16_t *)nullptr, dist_out, partials, fin ? *fin : FusedFinish{});
     return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -786,7 +993,7 @@ bool fused_search_ok(const Hooks &h, LaunchRange r) {
     if (!h.fused_reduce) return false;
     if (r.n == 0) return false;
     const TileRange t = search_range(h, r);
-    return !t.dyn && t.grid <= kFusedReduceMax;
+    return !t.dyn && t.fusable;
 }
 
 }  // namespace iris
