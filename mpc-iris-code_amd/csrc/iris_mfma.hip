@@ -318,6 +318,7 @@ __global__ void __launch_bounds__(64 * W, kMfmaWgs * kWaveSlots / W)
 #ifndef IRIS_SEARCH_DYN
 #define IRIS_SEARCH_DYN 0  // 1: static units, 2: units from a work counter; 0: one workgroup per 16 tiles
 #endif
+#if IRIS_SEARCH_DYN  // the persistent forms: build variants only (measured slower, see above)
 template <int T = kMfmaTiles>
 __global__ void __launch_bounds__(256, kMfmaWgs)
     template_search_dyn_kernel(const uint4 *__restrict__ db, const uint4 *__restrict__ qfrag, uint64_t tile0,
@@ -635,6 +636,8 @@ __global__ void __launch_bounds__(256, kMfmaWgs)
         partials[blockIdx.x] = b;
     }
 }
+
+#endif  // IRIS_SEARCH_DYN
 
 // ------------------------------------------------------------------ a few queries per pass
 
@@ -963,6 +966,7 @@ int launch_template_mfma_search(const Hooks &h, void *stream, const void *db, co
     if (r.n == 0) return 0;
     const bool fused = fin && t.fusable && !t.dyn;
     if (fin && !fused) return -1;  // the caller asks fused_search_ok() first
+#if IRIS_SEARCH_DYN
     if (t.dyn) {
         uint32_t *work = (uint32_t *)(partials + t.grid);
         if (hipMemsetAsync(work, 0, sizeof(uint32_t), (hipStream_t)stream) != hipSuccess) return -1;
@@ -976,6 +980,7 @@ int launch_template_mfma_search(const Hooks &h, void *stream, const void *db, co
                                r.first + r.n, dist_out, partials, work);
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
+#endif
     auto kern = fused ? (t.ksplit > 1 ? template_mfma_kernel<MF_SEARCH, kSplitT, 4, true>
                          : t.tiles_per_wave == 1 ? template_mfma_kernel<MF_SEARCH, 1, 1, true>
                                                  : template_mfma_kernel<MF_SEARCH, kMfmaTiles, 1, true>)
