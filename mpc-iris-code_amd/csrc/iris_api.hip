@@ -96,9 +96,15 @@ int enqueue_u16_engine(iris_engine *e, const iris_db *db, uint64_t first, uint64
     }, stream);
 }
 
+int run_u16_engine_pinned(iris_engine *e, const iris_db *db, uint64_t first, uint64_t n, uint16_t *out);
+
 // Engine kernel over [first, first+n) of db, u16 [n][31] outputs to host.
 int run_u16_engine(iris_engine *e, const iris_db *db, uint64_t first, uint64_t n, uint16_t *out) {
     iris_device *d = e->dev;
+#ifndef IRIS_PINNED_ROWS  // 0: rows through a device buffer and a copy-engine D2H (A/B builds)
+#define IRIS_PINNED_ROWS 1
+#endif
+    if (IRIS_PINNED_ROWS && db->k.layout == IRIS_LAYOUT_TILES) return run_u16_engine_pinned(e, db, first, n, out);
     CHK(ensure(d->out_a, std::min<uint64_t>(n, kU16Chunk) * kRot * 2));
     for (uint64_t done = 0; done < n; done += kU16Chunk) {
         const uint64_t m = std::min<uint64_t>(kU16Chunk, n - done);
@@ -156,6 +162,54 @@ void rows_give(iris_device *d, void *p, size_t bytes) {
     if (!p) return;
     if (d->rows_pool.size() < kRowsPoolMax) d->rows_pool.emplace_back(bytes, p);
     else (void)hipHostFree(p);
+}
+
+// records per kernel of the pinned-rows form (62 MB of rows per buffer)
+constexpr uint64_t kPinnedRowsChunk = 1ull << 20;
+
+// The host-output form for TILES databases: each chunk's kernel stores its rows straight into one
+// of two pinned host buffers (16-B runs over the host link, as the read-ahead does), and the helper
+// threads copy them to `out` while the next chunk's kernel runs.  The copy engines' D2H into a
+// caller's pageable array ran at 3-8 GB/s on some boxes (profiles/r03_host_rows.txt).
+int run_u16_engine_pinned(iris_engine *e, const iris_db *db, uint64_t first, uint64_t n, uint16_t *out) {
+    iris_device *d = e->dev;
+    const uint64_t ch = std::min<uint64_t>(n, kPinnedRowsChunk);
+    const size_t want = std::max<size_t>((size_t)ch * kRot * 2, 4096);
+    void *rows[2] = {nullptr, nullptr};
+    size_t got[2] = {0, 0};
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    const int nb = n > ch ? 2 : 1;
+    int rc = 0;
+    for (int b = 0; b < nb && rc == 0; ++b) {
+        rc = rows_take(d, want, &rows[b], &got[b]);
+        if (rc == 0 && !(ev[b] = take_event(d))) rc = fail(IRIS_E_HIP, "hipEventCreate failed");
+    }
+    // chunk c's rows go to rows[c & 1]; its kernel is enqueued before chunk c - 1's rows are
+    // copied out, and rows[c & 1] was last read by the (synchronous) copy of chunk c - 2
+    auto launch = [&](uint64_t c) -> int {
+        const uint64_t a = c * ch, m = std::min<uint64_t>(ch, n - a);
+        CHK(enqueue_u16_engine(e, db, first + a, m, (uint16_t *)rows[c & 1]));
+        HIPCHK(hipEventRecord(ev[c & 1], d->stream));
+        return 0;
+    };
+    const uint64_t chunks = (n + ch - 1) / ch;
+    if (rc == 0) rc = launch(0);
+    for (uint64_t c = 0; c < chunks && rc == 0; ++c) {
+        if (c + 1 < chunks) rc = launch(c + 1);
+        if (rc == 0 && hipEventSynchronize(ev[c & 1]) != hipSuccess) rc = fail(IRIS_E_HIP, "hipEventSynchronize");
+        if (rc == 0) {
+            const uint64_t a = c * ch, m = std::min<uint64_t>(ch, n - a);
+            parallel_copy(out + a * kRot, rows[c & 1], (size_t)m * kRot * 2);
+        }
+    }
+    // on failure a kernel may still be storing into the buffers: drain before they go back
+    if (rc != 0) (void)hipStreamSynchronize(d->stream);
+    for (int b = 0; b < nb; ++b) {
+        rows_give(d, rows[b], got[b]);
+        if (ev[b]) d->event_pool.push_back(ev[b]);
+    }
+    if (rc == 0 && d->profiling) fold_done(d);
+    return rc;
 }
 
 void ra_release(iris_engine *e) {

@@ -471,6 +471,45 @@ def test_max_capacity_masks(device):
         assert (tail == oc.masks_batch(q, oc.gen_templates(seed, n - 777, 777)[:, 200:])).all()
 
 
+def test_host_output_chunks(device):
+    """Host-output engine calls larger than one pinned-rows chunk (1M records): a resident range of
+    2.3M masks (three kernels into two alternating pinned buffers), an uploaded host slice of 1.1M
+    masks (two temporary-database chunks) and of 70k shares (two), each equal to the device-output
+    form over the same records and to the oracle on sampled rows."""
+    seed, n = 808, 2_300_000
+    q = oc.gen_templates(98, 0, 1)[0]
+    with ih.Database(device, ih.KIND_MASKS, n) as db, ih.MasksEngine(device, q[200:]) as eng:
+        db.generate(n, seed)
+        dev_out = device.alloc(n * ROT * 2)
+        try:
+            eng.batch_process_device(db, dev_out)
+            want = np.empty((n, ROT), np.uint16)
+            device.d2h(want, dev_out)
+        finally:
+            device.free(dev_out)
+        out = np.empty((n, ROT), np.uint16)
+        eng.batch_process(out, db, first=0, n=n)
+        assert (out == want).all()
+        for lo in (0, (1 << 20) - 3, 2 * (1 << 20) - 5, n - 1000):
+            assert (out[lo:lo + 1000] == oc.masks_batch(q[200:], oc.gen_templates(seed, lo, 1000)[:, 200:])).all(), lo
+        m = 1_100_000
+        host = db.read(7, m)
+        out2 = np.empty((m, ROT), np.uint16)
+        eng.batch_process(out2, host)  # not attached: uploaded per call
+        assert (out2 == want[7:7 + m]).all()
+    ns = 70_000
+    with ih.Database(device, ih.KIND_SHARES, ns) as sdb, ih.DistanceEngine(device, ih.encode(ih.Template.from_array(q))) as de:
+        shares = np.random.default_rng(5).integers(0, 65536, (ns, 12800), dtype=np.uint16)
+        sdb.append(shares)
+        want = np.empty((ns, ROT), np.uint16)
+        de.batch_process(want, sdb)
+        out = np.empty((ns, ROT), np.uint16)
+        de.batch_process(out, shares)  # not attached: uploaded per call
+        assert (out == want).all()
+        ii = np.array([0, 65535, 65536, ns - 1])
+        assert (out[ii] == oc.distance_batch(oc.encode(q), shares[ii])).all()
+
+
 # ---------------------------------------------------------------- resolver (src/main.rs:597-621)
 
 
