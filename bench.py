@@ -144,6 +144,26 @@ def batch_plant_queries(nq):
     return sorted({nq // 2, 0, nq - 1, nq // 4 + 1} & set(range(nq)))
 
 
+def pages_nodes(a, samples=32):
+    """{NUMA node: sampled pages} of a host array (move_pages query form; {} if unavailable):
+    where the caller's records live decides how fast an upload can go."""
+    import ctypes
+
+    try:
+        libc = ctypes.CDLL(None, use_errno=True)
+        base, nbytes = a.ctypes.data, a.nbytes
+        pages = (ctypes.c_void_p * samples)(*[(base + nbytes * i // samples) & ~4095 for i in range(samples)])
+        status = (ctypes.c_int * samples)()
+        if libc.syscall(279, 0, ctypes.c_ulong(samples), pages, None, status, 0) != 0:  # SYS_move_pages (x86-64)
+            return {}
+        out = {}
+        for v in status:
+            out[int(v)] = out.get(int(v), 0) + 1
+        return out
+    except (OSError, AttributeError):
+        return {}
+
+
 def gen_records(dev, kind, n, seed):
     """Host copies of records from the library's on-device generator."""
     with ih.Database(dev, kind, max(n, 1)) as g:
@@ -603,6 +623,7 @@ def run_aux(args, dev):
         chunk = args.chunk or (20_000 if args.attached else n)
         kind = ih.KIND_SHARES if shares_wl else ih.KIND_MASKS
         adb = None
+        extra["host_pages_numa"] = {"pages_by_node": pages_nodes(host), "gpu_node": dev.config().get("numa_node")}
         if args.attached:  # the mmap'd file's device copy (iris_db_attach_host), made once
             adb = ih.Database(dev, kind, n)
             t_att = time.perf_counter()

@@ -8,7 +8,10 @@
 
 #include <math.h>
 #include <stdio.h>
+#include <ctype.h>
 #include <string.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <map>
@@ -27,6 +30,91 @@ using namespace iris_api;
 
 namespace {
 
+#ifndef IRIS_PINNED_UPLOAD  // 0: every write through the runtime's staging of pageable copies (A/B builds)
+#define IRIS_PINNED_UPLOAD 1
+#endif
+constexpr size_t kUploadSlot = 64ull << 20;         // bytes per pinned upload slot (two per device)
+constexpr size_t kPinnedUploadMin = 2 * kUploadSlot;  // smaller writes: one runtime-staged copy
+
+// A large write: the helper threads copy each slot's records from the caller's pageable array
+// into one of two pinned buffers, the copy engine moves it to one of two device staging slots
+// and the pack kernel stores it, while the host already fills the other pinned buffer.  The
+// runtime's own staging of a pageable copy is one thread's memcpy, and it ran at 30 GB/s or
+// 57 GB/s depending on where the source pages live (profiles/r04_host_upload.txt).
+int db_write_pinned(iris_db *db, uint64_t index, const void *records, uint64_t n) {
+    iris_device *d = db->dev;
+    const KindInfo &k = db->k;
+    const uint64_t ch = std::max<uint64_t>(64, kUploadSlot / k.rec_bytes / 64 * 64);
+    const size_t slot = (size_t)ch * k.rec_bytes;
+    CHK(ensure(d->staging, 2 * slot));
+    if (d->upin_cap < slot) {
+        CHK(sync(d));  // no copy reads the old buffers any more
+        for (int b = 0; b < 2; ++b)
+            if (d->upin[b]) HIPCHK(hipHostFree(d->upin[b]));
+        d->upin[0] = d->upin[1] = nullptr;
+        d->upin_cap = 0;
+        for (int b = 0; b < 2; ++b) {
+            const hipError_t e = hipHostMalloc(&d->upin[b], kUploadSlot, hipHostMallocDefault);
+            if (e != hipSuccess) {
+                d->upin[b] = nullptr;
+                return fail(IRIS_E_NOMEM, std::string("hipHostMalloc upload buffer: ") + hipGetErrorString(e));
+            }
+        }
+        for (int b = 0; b < 2; ++b)
+            if (!d->upin_ev[b]) HIPCHK(hipEventCreateWithFlags(&d->upin_ev[b], hipEventDisableTiming));
+        d->upin_cap = kUploadSlot;
+    }
+    int rc = 0;
+    uint64_t c = 0;
+    for (uint64_t done = 0; done < n && rc == 0; done += ch, ++c) {
+        const uint64_t m = std::min<uint64_t>(ch, n - done);
+        const int b = (int)(c & 1);
+        // pinned buffer b was last read by the copy of slot c - 2 (this call) or by the previous
+        // call's copies (which ended with a sync)
+        if (c >= 2 && hipEventSynchronize(d->upin_ev[b]) != hipSuccess) {
+            rc = fail(IRIS_E_HIP, "hipEventSynchronize");
+            break;
+        }
+        parallel_copy(d->upin[b], (const char *)records + done * k.rec_bytes, (size_t)m * k.rec_bytes);
+        void *stage = (char *)d->staging.p + (size_t)b * slot;
+        if (hipMemcpyAsync(stage, d->upin[b], (size_t)m * k.rec_bytes, hipMemcpyHostToDevice, d->stream) != hipSuccess) {
+            rc = fail(IRIS_E_HIP, "hipMemcpyAsync upload");
+            break;
+        }
+        if (hipEventRecord(d->upin_ev[b], d->stream) != hipSuccess) {
+            rc = fail(IRIS_E_HIP, "hipEventRecord");
+            break;
+        }
+        rc = timed(d, "pack", m, [&] { return launch_pack(d->stream, k, stage, db->data, index + done, m); });
+    }
+    const int rs = sync(d);  // the pinned buffers are free again when the call returns
+    CHK(rc);
+    CHK(rs);
+    db->len = std::max(db->len, index + n);
+    return 0;
+}
+
+// Whether most of [p, p + bytes) lives on the device's NUMA node (sampled pages, move_pages
+// query form): the runtime's staged copy of such pages ran at 53 GB/s, the pinned-slot path at
+// 48-52; pages on the other node took the runtime path at 29-30 GB/s and the pinned one at 48-49
+// (profiles/r04_host_upload.txt).  Unknown placement counts as remote.
+bool host_near(const iris_device *d, const void *p, size_t bytes) {
+    if (d->numa_node < 0) return false;
+    constexpr int kSamples = 32;
+    const uintptr_t page = 4096, lo = (uintptr_t)p & ~(page - 1);
+    void *pages[kSamples];
+    int status[kSamples];
+    for (int i = 0; i < kSamples; ++i) pages[i] = (void *)((lo + (uintptr_t)((double)bytes * i / kSamples)) & ~(page - 1));
+    if (syscall(SYS_move_pages, 0, (unsigned long)kSamples, pages, nullptr, status, 0) != 0) return false;
+    int known = 0, near = 0;
+    for (int i = 0; i < kSamples; ++i)
+        if (status[i] >= 0) {
+            ++known;
+            near += status[i] == d->numa_node;
+        }
+    return known > 0 && 4 * near >= 3 * known;
+}
+
 int db_write_locked(iris_db *db, uint64_t index, const void *records, uint64_t n) {
     iris_device *d = db->dev;
     db_detach(db);
@@ -35,6 +123,10 @@ int db_write_locked(iris_db *db, uint64_t index, const void *records, uint64_t n
     if (n == 0) return 0;
     ARG(records != nullptr, "iris_db_write: records is NULL");
     const KindInfo &k = db->k;
+    const size_t bytes = (size_t)n * k.rec_bytes;
+    if (IRIS_PINNED_UPLOAD && bytes >= kPinnedUploadMin && d->hooks.upload != 2 &&
+        (d->hooks.upload == 1 || !host_near(d, records, bytes)))
+        return db_write_pinned(db, index, records, n);
     const uint64_t ch = chunk_records(k);
     CHK(ensure(d->staging, std::min<uint64_t>(n, ch) * k.rec_bytes));
     for (uint64_t done = 0; done < n; done += ch) {
@@ -407,6 +499,23 @@ int engine_from_query(iris_device *dev, int kind, const void *query, size_t qbyt
     return 0;
 }
 
+// The host NUMA node the device hangs off (sysfs of its PCI function); a one-node host is node 0;
+// -1 when unknown.
+int device_numa_node(int ordinal) {
+    char bus[64] = {0};
+    if (hipDeviceGetPCIBusId(bus, sizeof(bus) - 1, ordinal) != hipSuccess) return -1;
+    for (char *c = bus; *c; ++c) *c = (char)tolower((unsigned char)*c);
+    const std::string path = std::string("/sys/bus/pci/devices/") + bus + "/numa_node";
+    int node = -1;
+    if (FILE *f = fopen(path.c_str(), "r")) {
+        if (fscanf(f, "%d", &node) != 1) node = -1;
+        fclose(f);
+    }
+    if (node < 0 && access("/sys/devices/system/node/node1", F_OK) != 0 && access("/sys/devices/system/node/node0", F_OK) == 0)
+        node = 0;
+    return node;
+}
+
 void device_teardown(iris_device *d) {
     {
         std::lock_guard<std::recursive_mutex> g(d->mu);
@@ -419,6 +528,8 @@ void device_teardown(iris_device *d) {
             if (d->apart[b].p) (void)hipFree(d->apart[b].p);
             if (d->apart_read[b]) (void)hipEventDestroy(d->apart_read[b]);
             if (d->apart_written[b]) (void)hipEventDestroy(d->apart_written[b]);
+            if (d->upin[b]) (void)hipHostFree(d->upin[b]);
+            if (d->upin_ev[b]) (void)hipEventDestroy(d->upin_ev[b]);
         }
         if (d->aux) (void)hipStreamDestroy(d->aux);
         if (d->host_result) (void)hipHostFree(d->host_result);
@@ -478,8 +589,15 @@ int iris_config(const iris_device_t *d, char *buf, size_t len, size_t *needed) {
     ARG(buf || len == 0, "NULL buffer");
     Hooks now;
     if (!d) read_hooks(&now);
-    const size_t n = format_hooks(d ? d->hooks : now, buf, len);
-    if (needed) *needed = n;
+    std::string s(format_hooks(d ? d->hooks : now, nullptr, 0), '\0');
+    format_hooks(d ? d->hooks : now, &s[0], s.size() + 1);
+    if (d) s += " numa_node=" + std::to_string(d->numa_node);  // where large writes' pages are compared
+    if (buf && len) {
+        const size_t n = std::min(len - 1, s.size());
+        memcpy(buf, s.data(), n);
+        buf[n] = 0;
+    }
+    if (needed) *needed = s.size();
     return 0;
 }
 
@@ -525,6 +643,7 @@ int iris_device_open(int ordinal, iris_device_t **out) {
         (void)hipGetLastError();
     }
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) d->numa_node = device_numa_node(ordinal);
     if (e != hipSuccess) {
         delete d;
         return fail(IRIS_E_HIP, std::string("stream create: ") + hipGetErrorString(e));

@@ -60,6 +60,7 @@ struct DevBuf {
 
 struct iris_device {
     int ordinal = 0;
+    int numa_node = -1;  // host NUMA node of the device's PCI function (-1: unknown)
     iris::Hooks hooks;  // environment knobs, read once when the device opened
     hipStream_t stream = nullptr;
     std::recursive_mutex mu;
@@ -97,6 +98,11 @@ struct iris_device {
     std::vector<std::pair<size_t, void *>> qpool;
     // freed engines' pinned read-ahead row buffers (the participant builds an engine per request)
     std::vector<std::pair<size_t, void *>> rows_pool;
+    // pinned slots of large database writes (db_write_pinned): the host fills one while the copy
+    // engine drains the other; upin_ev[b] is recorded after the copy that read upin[b]
+    void *upin[2] = {nullptr, nullptr};
+    size_t upin_cap = 0;
+    hipEvent_t upin_ev[2] = {nullptr, nullptr};
     // recorded on the device stream before every read-ahead launch and waited for by the side
     // stream: the launch follows whatever the device stream holds (the engine's query build,
     // writes to the database)

@@ -308,7 +308,8 @@ namespace {
 // Test-only hooks in the order of Hooks::ignored's bits.
 constexpr const char *kHookNames[] = {"IRIS_TILES_PER_WAVE", "IRIS_FUSED_REDUCE", "IRIS_BATCH_KERNEL",
                                       "IRIS_BATCH_XQG",      "IRIS_SCHEDULE",     "IRIS_LOAD_PREAD",
-                                      "IRIS_GROUP_DELAY_US", "IRIS_GROUP_STALL",  "IRIS_GROUP_UNORDERED"};
+                                      "IRIS_GROUP_DELAY_US", "IRIS_GROUP_STALL",  "IRIS_GROUP_UNORDERED",
+                                      "IRIS_UPLOAD"};
 constexpr int kNumHooks = (int)(sizeof(kHookNames) / sizeof(kHookNames[0]));
 
 const char *env(const char *name) {
@@ -346,12 +347,14 @@ void read_hooks(Hooks *h) {
         case 6: h->group_delay_us = env_u32(v, 1000000); break;
         case 7: h->group_stall = v[0] != '0'; break;
         case 8: h->group_unordered = v[0] != '0'; break;
+        case 9: h->upload = !strcmp(v, "pinned") ? 1 : !strcmp(v, "runtime") ? 2 : 0; break;
         }
     }
 }
 
 size_t format_hooks(const Hooks &h, char *buf, size_t len) {
     static const char *sched[] = {"auto", "spin", "yield", "blocking"};
+    static const char *upload_names[] = {"auto", "pinned", "runtime", "auto"};
     std::string s = "readahead=" + std::to_string(h.readahead) + " group_timeout_ms=" +
                     (h.group_timeout_ms ? std::to_string(h.group_timeout_ms) : std::string("auto")) +
                     " copy_helpers=" + std::to_string(copy_helpers()) + " test_hooks=" + std::to_string(h.test);
@@ -360,7 +363,8 @@ size_t format_hooks(const Hooks &h, char *buf, size_t len) {
              " fused_reduce=" + std::to_string(h.fused_reduce) + " batch_kernel=" + std::to_string(h.batch_kernel) +
              " batch_xqg=" + std::to_string(h.batch_xqg) + " schedule=" + sched[h.schedule & 3] +
              " load_pread=" + std::to_string(h.load_pread) + " group_delay_us=" + std::to_string(h.group_delay_us) +
-             " group_stall=" + std::to_string(h.group_stall) + " group_unordered=" + std::to_string(h.group_unordered);
+             " group_stall=" + std::to_string(h.group_stall) + " group_unordered=" + std::to_string(h.group_unordered) +
+             " upload=" + upload_names[h.upload & 3];
     std::string ign;
     for (int i = 0; i < kNumHooks; ++i)
         if (h.ignored >> i & 1u) ign += (ign.empty() ? "" : ",") + std::string(kHookNames[i]);

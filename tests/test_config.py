@@ -8,7 +8,7 @@ import pytest
 import iris_hip as ih
 
 TEST_HOOKS = ["IRIS_TILES_PER_WAVE", "IRIS_FUSED_REDUCE", "IRIS_BATCH_KERNEL", "IRIS_BATCH_XQG", "IRIS_SCHEDULE",
-              "IRIS_LOAD_PREAD", "IRIS_GROUP_DELAY_US", "IRIS_GROUP_STALL", "IRIS_GROUP_UNORDERED"]
+              "IRIS_LOAD_PREAD", "IRIS_GROUP_DELAY_US", "IRIS_GROUP_STALL", "IRIS_GROUP_UNORDERED", "IRIS_UPLOAD"]
 
 
 @pytest.fixture(autouse=True)
@@ -39,11 +39,12 @@ def test_test_hooks_with_opt_in(monkeypatch):
     monkeypatch.setenv("IRIS_BATCH_KERNEL", "2")
     monkeypatch.setenv("IRIS_SCHEDULE", "spin")
     monkeypatch.setenv("IRIS_GROUP_DELAY_US", "1500")
+    monkeypatch.setenv("IRIS_UPLOAD", "pinned")
     c = ih.config()
     assert "ignored" not in c
     assert (c["test_hooks"], c["tiles_per_wave"], c["batch_kernel"], c["schedule"], c["group_delay_us"]) == \
         ("1", "1", "2", "spin", "1500")
-    assert (c["fused_reduce"], c["group_stall"], c["load_pread"]) == ("1", "0", "0")
+    assert (c["fused_reduce"], c["group_stall"], c["load_pread"], c["upload"]) == ("1", "0", "0", "pinned")
 
 
 def test_production_knobs_need_no_opt_in(monkeypatch):

@@ -811,3 +811,25 @@ def test_persistent_search_ranges_vs_oracle(device):
                 assert got.index == 7 + first + idx and bits_eq(got.distance, best), (first, m, got)
             assert eng.search(db).index == 12_345
             assert eng.search(db, first=13_000, n=n - 13_000).index == 150_000
+
+
+@pytest.mark.parametrize("path", ["pinned", "runtime"])
+def test_large_write_paths(hooked_device, path):
+    """Database writes of at least 128 MB take the pinned-slot upload or the runtime's staged copy by
+    where the caller's pages live (IRIS_UPLOAD pins one): both store the same records, including an
+    unaligned start index and a last slot shorter than the others."""
+    dev = hooked_device(IRIS_UPLOAD=path)
+    assert dev.config()["upload"] == path
+    rng = np.random.default_rng(11)
+    n = 130_000  # 208 MB of masks: four 64-MB slots, the last one partial
+    masks = rng.integers(0, 2**64, (n, 200), dtype=np.uint64)
+    with ih.Database(dev, ih.KIND_MASKS, n + 100) as db:
+        db.append(masks[:3])
+        db.append(masks[3:])
+        for lo in (0, 40_000, n - 50):
+            assert (db.read(lo, 50) == masks[lo:lo + 50]).all(), lo
+        shares = rng.integers(0, 2**16, (5_300, 12800), dtype=np.uint16)  # 136 MB, three slots
+        with ih.Database(dev, ih.KIND_SHARES, 5_300) as sdb:
+            sdb.append(shares)
+            for lo in (0, 2_559, 2_560, 5_250):
+                assert (sdb.read(lo, 50) == shares[lo:lo + 50]).all(), lo
