@@ -17,6 +17,29 @@ import bench  # noqa: E402  (pages_nodes)
 import iris_hip as ih  # noqa: E402
 
 N = 2_000_000
+
+
+def backing(a):
+    """Rss / AnonHugePages (kB) of the mappings that hold the array (/proc/self/smaps): whether its
+    pages are 2-MB transparent huge pages, 4-KB pages or a file's page cache."""
+    lo, hi = a.ctypes.data, a.ctypes.data + a.nbytes
+    rss = huge = 0
+    name = ""
+    cur = None
+    for line in open("/proc/self/smaps"):
+        f = line.split()
+        if "-" in f[0] and len(f) >= 5 and all(c in "0123456789abcdef-" for c in f[0]):
+            s0, e0 = (int(x, 16) for x in f[0].split("-"))
+            cur = s0 < hi and e0 > lo
+            if cur and len(f) >= 6:
+                name = f[5]
+        elif cur and f[0] == "Rss:":
+            rss += int(f[1])
+        elif cur and f[0] == "AnonHugePages:":
+            huge += int(f[1])
+    return {"rss_kB": rss, "anon_huge_kB": huge, "file": name}
+
+
 out_dir = pathlib.Path(sys.argv[1])
 out_dir.mkdir(parents=True, exist_ok=True)
 os.environ["IRIS_TEST_HOOKS"] = "1"
@@ -53,7 +76,7 @@ for src_name, src in (("read_back", read_back), ("fresh_copy", fresh), ("memmap"
         eng.close()
         best = min(ts)
         print(f"{src_name:10s} {path:8s} ms {best * 1e3:7.2f} GB/s {src.nbytes / best / 1e9:5.1f} "
-              f"pages {bench.pages_nodes(np.asarray(src))} gpu_node {dev.config()['numa_node']}", flush=True)
+              f"pages {bench.pages_nodes(np.asarray(src))} gpu_node {dev.config()['numa_node']} {backing(src)}", flush=True)
 del mapped
 fpath.unlink()
 for d in devs.values():
