@@ -10,7 +10,6 @@
 #include <stdio.h>
 #include <ctype.h>
 #include <string.h>
-#include <sys/syscall.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -39,8 +38,9 @@ constexpr size_t kPinnedUploadMin = 2 * kUploadSlot;  // smaller writes: one run
 // A large write: the helper threads copy each slot's records from the caller's pageable array
 // into one of two pinned buffers, the copy engine moves it to one of two device staging slots
 // and the pack kernel stores it, while the host already fills the other pinned buffer.  The
-// runtime's own staging of a pageable copy is one thread's memcpy, and it ran at 30 GB/s or
-// 57 GB/s depending on where the source pages live (profiles/r04_host_upload.txt).
+// runtime's copy of a pageable source ran at 29-30 GB/s for some caller arrays (records read
+// back from the device, on either NUMA node) and 53 GB/s for others; this path moved 48-52 GB/s
+// for both (profiles/r04_host_upload.txt).  IRIS_UPLOAD=runtime (test hook) keeps the runtime's.
 int db_write_pinned(iris_db *db, uint64_t index, const void *records, uint64_t n) {
     iris_device *d = db->dev;
     const KindInfo &k = db->k;
@@ -94,27 +94,6 @@ int db_write_pinned(iris_db *db, uint64_t index, const void *records, uint64_t n
     return 0;
 }
 
-// Whether most of [p, p + bytes) lives on the device's NUMA node (sampled pages, move_pages
-// query form): the runtime's staged copy of such pages ran at 53 GB/s, the pinned-slot path at
-// 48-52; pages on the other node took the runtime path at 29-30 GB/s and the pinned one at 48-49
-// (profiles/r04_host_upload.txt).  Unknown placement counts as remote.
-bool host_near(const iris_device *d, const void *p, size_t bytes) {
-    if (d->numa_node < 0) return false;
-    constexpr int kSamples = 32;
-    const uintptr_t page = 4096, lo = (uintptr_t)p & ~(page - 1);
-    void *pages[kSamples];
-    int status[kSamples];
-    for (int i = 0; i < kSamples; ++i) pages[i] = (void *)((lo + (uintptr_t)((double)bytes * i / kSamples)) & ~(page - 1));
-    if (syscall(SYS_move_pages, 0, (unsigned long)kSamples, pages, nullptr, status, 0) != 0) return false;
-    int known = 0, near = 0;
-    for (int i = 0; i < kSamples; ++i)
-        if (status[i] >= 0) {
-            ++known;
-            near += status[i] == d->numa_node;
-        }
-    return known > 0 && 4 * near >= 3 * known;
-}
-
 int db_write_locked(iris_db *db, uint64_t index, const void *records, uint64_t n) {
     iris_device *d = db->dev;
     db_detach(db);
@@ -124,9 +103,7 @@ int db_write_locked(iris_db *db, uint64_t index, const void *records, uint64_t n
     ARG(records != nullptr, "iris_db_write: records is NULL");
     const KindInfo &k = db->k;
     const size_t bytes = (size_t)n * k.rec_bytes;
-    if (IRIS_PINNED_UPLOAD && bytes >= kPinnedUploadMin && d->hooks.upload != 2 &&
-        (d->hooks.upload == 1 || !host_near(d, records, bytes)))
-        return db_write_pinned(db, index, records, n);
+    if (IRIS_PINNED_UPLOAD && bytes >= kPinnedUploadMin && d->hooks.upload != 2) return db_write_pinned(db, index, records, n);
     const uint64_t ch = chunk_records(k);
     CHK(ensure(d->staging, std::min<uint64_t>(n, ch) * k.rec_bytes));
     for (uint64_t done = 0; done < n; done += ch) {

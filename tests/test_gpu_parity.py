@@ -815,9 +815,9 @@ def test_persistent_search_ranges_vs_oracle(device):
 
 @pytest.mark.parametrize("path", ["pinned", "runtime"])
 def test_large_write_paths(hooked_device, path):
-    """Database writes of at least 128 MB take the pinned-slot upload or the runtime's staged copy by
-    where the caller's pages live (IRIS_UPLOAD pins one): both store the same records, including an
-    unaligned start index and a last slot shorter than the others."""
+    """Database writes of at least 128 MB go through two pinned slots filled by the helper threads, or
+    (IRIS_UPLOAD=runtime) the runtime's copy of the pageable source: both store the same records,
+    including an unaligned start index and a last slot shorter than the others."""
     dev = hooked_device(IRIS_UPLOAD=path)
     assert dev.config()["upload"] == path
     rng = np.random.default_rng(11)
