@@ -35,13 +35,15 @@ namespace {
 constexpr size_t kUploadSlot = 64ull << 20;         // bytes per pinned upload slot (two per device)
 constexpr size_t kPinnedUploadMin = 2 * kUploadSlot;  // smaller writes: one runtime-staged copy
 
+}  // namespace
+
 // A large write: the helper threads copy each slot's records from the caller's pageable array
 // into one of two pinned buffers, the copy engine moves it to one of two device staging slots
 // and the pack kernel stores it, while the host already fills the other pinned buffer.  The
 // runtime's copy of a pageable source ran at 29-30 GB/s for some caller arrays (records read
 // back from the device, on either NUMA node) and 53 GB/s for others; this path moved 48-52 GB/s
 // for both (profiles/r04_host_upload.txt).  IRIS_UPLOAD=runtime (test hook) keeps the runtime's.
-int db_write_pinned(iris_db *db, uint64_t index, const void *records, uint64_t n) {
+int iris_api::db_write_pinned(iris_db *db, uint64_t index, const void *records, uint64_t n) {
     iris_device *d = db->dev;
     const KindInfo &k = db->k;
     const uint64_t ch = std::max<uint64_t>(64, kUploadSlot / k.rec_bytes / 64 * 64);
@@ -75,7 +77,7 @@ int db_write_pinned(iris_db *db, uint64_t index, const void *records, uint64_t n
             rc = fail(IRIS_E_HIP, "hipEventSynchronize");
             break;
         }
-        parallel_copy(d->upin[b], (const char *)records + done * k.rec_bytes, (size_t)m * k.rec_bytes);
+        parallel_copy(d->upin[b], (const char *)records + done * k.rec_bytes, (size_t)m * k.rec_bytes, d->ordinal);
         void *stage = (char *)d->staging.p + (size_t)b * slot;
         if (hipMemcpyAsync(stage, d->upin[b], (size_t)m * k.rec_bytes, hipMemcpyHostToDevice, d->stream) != hipSuccess) {
             rc = fail(IRIS_E_HIP, "hipMemcpyAsync upload");
@@ -93,6 +95,8 @@ int db_write_pinned(iris_db *db, uint64_t index, const void *records, uint64_t n
     db->len = std::max(db->len, index + n);
     return 0;
 }
+
+namespace {
 
 int db_write_locked(iris_db *db, uint64_t index, const void *records, uint64_t n) {
     iris_device *d = db->dev;
@@ -268,7 +272,7 @@ int run_u16_engine_pinned(iris_engine *e, const iris_db *db, uint64_t first, uin
         if (rc == 0 && hipEventSynchronize(ev[c & 1]) != hipSuccess) rc = fail(IRIS_E_HIP, "hipEventSynchronize");
         if (rc == 0) {
             const uint64_t a = c * ch, m = std::min<uint64_t>(ch, n - a);
-            parallel_copy(out + a * kRot, rows[c & 1], (size_t)m * kRot * 2);
+            parallel_copy(out + a * kRot, rows[c & 1], (size_t)m * kRot * 2, d->ordinal);
         }
     }
     // on failure a kernel may still be storing into the buffers: drain before they go back
@@ -357,7 +361,7 @@ int readahead_u16_call(iris_engine *e, const iris_db *a, uint64_t first, uint64_
     const uint64_t next = first + n;
     if (walk && next < end) CHK(ra_launch(e, a, next, std::min<uint64_t>(n, end - next), b ^ 1));
     HIPCHK(hipEventSynchronize(ra.computed[b]));
-    parallel_copy(out, ra.rows[b], (size_t)n * kRot * 2);
+    parallel_copy(out, ra.rows[b], (size_t)n * kRot * 2, d->ordinal);
     if (d->profiling) fold_done(d);
     return 0;
 }

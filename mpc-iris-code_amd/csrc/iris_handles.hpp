@@ -370,6 +370,9 @@ int template_engine_locked(iris_device *d, const iris_template_t *query, iris_en
 int search_enqueue(iris_engine *e, const iris_db *db, uint64_t first, uint64_t n, double *dist_dev, iris::Partial *dst,
                    bool side = false, hipEvent_t done = nullptr, uint64_t idx_base = 0, uint32_t *host_done = nullptr,
                    uint32_t seq = 0, bool *flagged = nullptr);
+// Stores host records [0, n) at database index `index` through two pinned 64-MB slots the helper
+// threads fill (caller holds the device lock; the database is detached already); waits for the device.
+int db_write_pinned(iris_db *db, uint64_t index, const void *records, uint64_t n);
 // Partial (indices offset by base) -> iris_match_t; +inf / UINT64_MAX when none
 void match_from(const iris::Partial &r, bool any, uint64_t base, iris_match_t *out);
 

@@ -226,9 +226,10 @@ namespace iris {
 
 namespace {
 
-// Helper threads for copying an engine call's rows out of pinned memory into the caller's
-// buffer (read-ahead, iris_api.hip): one core reads ~25 GB/s from DRAM, so a 1.24-MB
-// participant-sized chunk costs ~45 us on one thread.  The helpers spin for a while after each
+// Helper threads (one pool per device) for copying an engine call's rows out of pinned memory
+// into the caller's buffer (read-ahead, iris_api.hip) and a large write's records into the pinned
+// upload slots: one core reads ~25 GB/s from DRAM, so a 1.24-MB participant-sized chunk costs
+// ~45 us on one thread.  The helpers spin for a while after each
 // job (calls of a chunk walk arrive every few tens of us) and then block.
 class CopyPool {
    public:
@@ -377,18 +378,22 @@ size_t format_hooks(const Hooks &h, char *buf, size_t len) {
     return s.size();
 }
 
-void parallel_copy(void *dst, const void *src, size_t bytes) {
+void parallel_copy(void *dst, const void *src, size_t bytes, int lane) {
+    // one pool per device (lane = ordinal): devices driven from their own threads (a device group's
+    // loads, concurrent host-slice calls) copy in parallel instead of queueing on one pool
+    constexpr int kLanes = 16;
     static std::mutex create_mu;
-    static CopyPool *pool = nullptr;  // leaked on purpose (detached helpers)
+    static CopyPool *pools[kLanes] = {};  // leaked on purpose (detached helpers)
     if (bytes < kParallelCopyMin) {
         memcpy(dst, src, bytes);
         return;
     }
+    const int l = ((lane % kLanes) + kLanes) % kLanes;
     CopyPool *p;
     {
-        std::lock_guard<std::mutex> l(create_mu);
-        if (!pool || pool->pid() != getpid()) pool = new CopyPool(copy_helpers());  // a forked child gets its own
-        p = pool;
+        std::lock_guard<std::mutex> g(create_mu);
+        if (!pools[l] || pools[l]->pid() != getpid()) pools[l] = new CopyPool(copy_helpers());  // a forked child gets its own
+        p = pools[l];
     }
     p->run((char *)dst, (const char *)src, bytes);
 }

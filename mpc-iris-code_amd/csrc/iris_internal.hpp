@@ -319,6 +319,6 @@ void build_masks_rotations(const uint64_t *query, uint32_t *tab);
 void build_shares_rotations(const uint16_t *query, uint32_t *tab);
 bool partial_better(const Partial &a, const Partial &b);
 // memcpy split over a few persistent helper threads (copies of at least 256 KB)
-void parallel_copy(void *dst, const void *src, size_t bytes);
+void parallel_copy(void *dst, const void *src, size_t bytes, int lane = 0);  // lane: the device ordinal
 
 }  // namespace iris

@@ -151,6 +151,20 @@ int iris_db_load_file(iris_db_t *db, const char *path, uint64_t first, uint64_t 
         const bool force_pread = db->dev->hooks.load_pread;  // test hook: the fallback path
         void *map = pch <= ch && !force_pread ? ::mmap(nullptr, (size_t)size, PROT_READ, MAP_SHARED, f.fd, 0)
                                               : MAP_FAILED;
+#ifndef IRIS_LOAD_SLOTS  // 0: DMA from registered page-cache windows (A/B builds)
+#define IRIS_LOAD_SLOTS 1
+#endif
+        if (IRIS_LOAD_SLOTS && map != MAP_FAILED) {
+            // the helper threads copy the mapping into two pinned slots while the copy engine drains
+            // the other (the path of large writes, db_write_pinned); the registered windows below
+            // moved 35-37 GB/s including their registration (profiles/r04_load_slots.txt)
+            (void)madvise(map, (size_t)size, MADV_SEQUENTIAL);
+            const int rc = db_write_pinned(db, base, (const char *)map + (size_t)first * k.rec_bytes, n);
+            ::munmap(map, (size_t)size);
+            CHK(rc);
+            if (loaded) *loaded = n;
+            return 0;
+        }
         if (map != MAP_FAILED) {
             // hipHostUnregister waits for the device, so windows stay registered (their
             // registration overlapping the previous window's copy) and are released in
