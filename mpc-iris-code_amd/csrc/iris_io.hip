@@ -26,6 +26,7 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <atomic>
 #include <cstdio>
 #include <thread>
 
@@ -154,7 +155,16 @@ int iris_db_load_file(iris_db_t *db, const char *path, uint64_t first, uint64_t 
 #ifndef IRIS_LOAD_SLOTS  // 0: DMA from registered page-cache windows (A/B builds)
 #define IRIS_LOAD_SLOTS 1
 #endif
-        if (IRIS_LOAD_SLOTS && map != MAP_FAILED) {
+        // loads running at once in this process (a device group's per-device loads): those after the
+        // first keep the registered windows, which take no host copy -- eight GPUs' slot copies
+        // would all read host memory at once (unmeasured here: one GPU per box)
+        static std::atomic<int> loads{0};
+        struct InFlight {
+            int before;
+            InFlight() : before(loads.fetch_add(1)) {}
+            ~InFlight() { loads.fetch_sub(1); }
+        } in_flight;
+        if (IRIS_LOAD_SLOTS && map != MAP_FAILED && in_flight.before == 0) {
             // the helper threads copy the mapping into two pinned slots while the copy engine drains
             // the other (the path of large writes, db_write_pinned); the registered windows below
             // moved 35-37 GB/s including their registration (profiles/r04_load_slots.txt)
