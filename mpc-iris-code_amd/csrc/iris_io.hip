@@ -8,10 +8,13 @@
 //   *.masks      concatenated Bits        (1600 B, u64 limbs)
 //   *.share-i    concatenated EncodedBits (25600 B, u16 elements)
 //   templates    concatenated Template    (3200 B, pattern then mask)
-// Loading DMAs the file straight out of the page cache (its mapped pages are
-// registered with the device chunk by chunk) into a device staging slot that
-// the pack kernel transposes into the TILES layout; if the pages cannot be
-// registered, reader threads fill two pinned buffers (pread) while the device
+// Loading maps the file and sends it through the pinned upload slots of large
+// writes (the device's helper threads copy 64-MB slots out of the mapping while
+// the copy engine drains the other into a staging slot that the pack kernel
+// transposes into the TILES layout).  A load that starts while another is in
+// flight DMAs straight out of the page cache instead (its mapped pages are
+// registered with the device chunk by chunk: no host copy); if the pages cannot
+// be registered, reader threads fill two pinned buffers (pread) while the device
 // copies the other, so the load runs at the slower of file read and PCIe.
 //
 // JSON: a top-level array of {"pattern": hex, "mask": hex} objects — serde's
