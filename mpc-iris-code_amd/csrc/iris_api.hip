@@ -32,8 +32,12 @@ namespace {
 #ifndef IRIS_PINNED_UPLOAD  // 0: every write through the runtime's staging of pageable copies (A/B builds)
 #define IRIS_PINNED_UPLOAD 1
 #endif
-constexpr size_t kUploadSlot = 64ull << 20;         // bytes per pinned upload slot (two per device)
-constexpr size_t kPinnedUploadMin = 2 * kUploadSlot;  // smaller writes: one runtime-staged copy
+#ifndef IRIS_UPLOAD_SLOT_MB
+#define IRIS_UPLOAD_SLOT_MB 64
+#endif
+constexpr size_t kUploadSlot = (size_t)IRIS_UPLOAD_SLOT_MB << 20;  // bytes per pinned upload slot
+constexpr int kUploadSlots = kUploadRing;                       // slots per device (iris_handles.hpp)
+constexpr size_t kPinnedUploadMin = 128ull << 20;                // smaller writes: one runtime-staged copy
 
 }  // namespace
 
@@ -48,21 +52,21 @@ int iris_api::db_write_pinned(iris_db *db, uint64_t index, const void *records, 
     const KindInfo &k = db->k;
     const uint64_t ch = std::max<uint64_t>(64, kUploadSlot / k.rec_bytes / 64 * 64);
     const size_t slot = (size_t)ch * k.rec_bytes;
-    CHK(ensure(d->staging, 2 * slot));
+    CHK(ensure(d->staging, kUploadSlots * slot));
     if (d->upin_cap < slot) {
         CHK(sync(d));  // no copy reads the old buffers any more
-        for (int b = 0; b < 2; ++b)
+        for (int b = 0; b < kUploadSlots; ++b)
             if (d->upin[b]) HIPCHK(hipHostFree(d->upin[b]));
-        d->upin[0] = d->upin[1] = nullptr;
+        for (int b = 0; b < kUploadSlots; ++b) d->upin[b] = nullptr;
         d->upin_cap = 0;
-        for (int b = 0; b < 2; ++b) {
+        for (int b = 0; b < kUploadSlots; ++b) {
             const hipError_t e = hipHostMalloc(&d->upin[b], kUploadSlot, hipHostMallocDefault);
             if (e != hipSuccess) {
                 d->upin[b] = nullptr;
                 return fail(IRIS_E_NOMEM, std::string("hipHostMalloc upload buffer: ") + hipGetErrorString(e));
             }
         }
-        for (int b = 0; b < 2; ++b)
+        for (int b = 0; b < kUploadSlots; ++b)
             if (!d->upin_ev[b]) HIPCHK(hipEventCreateWithFlags(&d->upin_ev[b], hipEventDisableTiming));
         d->upin_cap = kUploadSlot;
     }
@@ -70,10 +74,10 @@ int iris_api::db_write_pinned(iris_db *db, uint64_t index, const void *records, 
     uint64_t c = 0;
     for (uint64_t done = 0; done < n && rc == 0; done += ch, ++c) {
         const uint64_t m = std::min<uint64_t>(ch, n - done);
-        const int b = (int)(c & 1);
-        // pinned buffer b was last read by the copy of slot c - 2 (this call) or by the previous
+        const int b = (int)(c % kUploadSlots);
+        // pinned buffer b was last read by the copy of slot c - kUploadSlots (this call) or by the previous
         // call's copies (which ended with a sync)
-        if (c >= 2 && hipEventSynchronize(d->upin_ev[b]) != hipSuccess) {
+        if (c >= (uint64_t)kUploadSlots && hipEventSynchronize(d->upin_ev[b]) != hipSuccess) {
             rc = fail(IRIS_E_HIP, "hipEventSynchronize");
             break;
         }
@@ -509,6 +513,8 @@ void device_teardown(iris_device *d) {
             if (d->apart[b].p) (void)hipFree(d->apart[b].p);
             if (d->apart_read[b]) (void)hipEventDestroy(d->apart_read[b]);
             if (d->apart_written[b]) (void)hipEventDestroy(d->apart_written[b]);
+        }
+        for (int b = 0; b < kUploadRing; ++b) {
             if (d->upin[b]) (void)hipHostFree(d->upin[b]);
             if (d->upin_ev[b]) (void)hipEventDestroy(d->upin_ev[b]);
         }

@@ -58,6 +58,11 @@ struct DevBuf {
     size_t cap = 0;
 };
 
+#ifndef IRIS_UPLOAD_SLOTS
+#define IRIS_UPLOAD_SLOTS 2
+#endif
+constexpr int kUploadRing = IRIS_UPLOAD_SLOTS;  // pinned upload slots per device (db_write_pinned)
+
 struct iris_device {
     int ordinal = 0;
     int numa_node = -1;  // host NUMA node of the device's PCI function (-1: unknown)
@@ -99,10 +104,10 @@ struct iris_device {
     // freed engines' pinned read-ahead row buffers (the participant builds an engine per request)
     std::vector<std::pair<size_t, void *>> rows_pool;
     // pinned slots of large database writes (db_write_pinned): the host fills one while the copy
-    // engine drains the other; upin_ev[b] is recorded after the copy that read upin[b]
-    void *upin[2] = {nullptr, nullptr};
+    // engine drains the others; upin_ev[b] is recorded after the copy that read upin[b]
+    void *upin[kUploadRing] = {};
     size_t upin_cap = 0;
-    hipEvent_t upin_ev[2] = {nullptr, nullptr};
+    hipEvent_t upin_ev[kUploadRing] = {};
     // recorded on the device stream before every read-ahead launch and waited for by the side
     // stream: the launch follows whatever the device stream holds (the engine's query build,
     // writes to the database)
