@@ -37,7 +37,11 @@ namespace {
 #endif
 constexpr size_t kUploadSlot = (size_t)IRIS_UPLOAD_SLOT_MB << 20;  // bytes per pinned upload slot
 constexpr int kUploadSlots = kUploadRing;                       // slots per device (iris_handles.hpp)
-constexpr size_t kPinnedUploadMin = 128ull << 20;                // smaller writes: one runtime-staged copy
+#ifndef IRIS_PINNED_UPLOAD_MIN_MB
+#define IRIS_PINNED_UPLOAD_MIN_MB 128
+#endif
+constexpr size_t kPinnedUploadMin = (size_t)IRIS_PINNED_UPLOAD_MIN_MB << 20;  // smaller writes: one runtime-staged copy
+constexpr size_t kUploadPieceMin = 4ull << 20;  // a write is cut into at least 4 slots of at least this
 
 }  // namespace
 
@@ -50,7 +54,9 @@ constexpr size_t kPinnedUploadMin = 128ull << 20;                // smaller writ
 int iris_api::db_write_pinned(iris_db *db, uint64_t index, const void *records, uint64_t n) {
     iris_device *d = db->dev;
     const KindInfo &k = db->k;
-    const uint64_t ch = std::max<uint64_t>(64, kUploadSlot / k.rec_bytes / 64 * 64);
+    // at least four slots per write (so the host's copy of one overlaps the copy engine's of another)
+    const size_t piece = std::min(kUploadSlot, std::max(kUploadPieceMin, (size_t)n * k.rec_bytes / 4));
+    const uint64_t ch = std::max<uint64_t>(64, piece / k.rec_bytes / 64 * 64);
     const size_t slot = (size_t)ch * k.rec_bytes;
     CHK(ensure(d->staging, kUploadSlots * slot));
     if (d->upin_cap < slot) {

@@ -1,0 +1,19 @@
+# round 4: participant-sized calls that upload (the reference's 20 000-record host-slice loop without an attached
+# array): the runtime's copy (shipped below 128 MB) against the pinned slots from 8 MB (libiris_p8.so, four or more
+# slots per write), interleaved; and the large uploads for no regression
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+O=gpurun_out/r04ab; mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 200 --timeout-method thread -k "large_write or host_output or masks_engine or distance" > $O/tests.log 2>&1 || { echo "tests rc=$?"; tail -30 $O/tests.log; exit 1; }
+IRIS_HIP_LIB=$PWD/mpc-iris-code_amd/libiris_p8.so timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_attach.py -x -q --timeout 200 --timeout-method thread > $O/tests_p8.log 2>&1 || { echo "tests p8 rc=$?"; tail -30 $O/tests_p8.log; exit 1; }
+tail -1 $O/tests.log; tail -1 $O/tests_p8.log
+for i in 1 2; do
+  for v in hip p8; do
+    for spec in "host-masks 20000" "host-shares 2000" "host-masks 0"; do
+      set -- $spec; wl=$1; ch=$2; c=""; [ $ch != 0 ] && c="--chunk $ch"
+      IRIS_HIP_LIB=$PWD/mpc-iris-code_amd/libiris_$v.so timeout -k 10 200 python bench.py --workload $wl $c --steps 3 --warmup 1 --no-cpu-baseline > $O/${wl}_${ch}_${v}_$i.log 2>&1 || { echo "bench $wl $v rc=$?"; tail -5 $O/${wl}_${ch}_${v}_$i.log; exit 1; }
+      grep '^{' $O/${wl}_${ch}_${v}_$i.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$wl chunk $ch $v', 'ms_per_step', round(d['ms_per_step'],2), 'value', '%.4g'%d['value'], d['check']['ok'])"
+    done
+  done
+done
+echo all ok
