@@ -13,6 +13,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
 #include <map>
 #include <mutex>
 #include <new>
@@ -37,20 +38,18 @@ namespace {
 #endif
 constexpr size_t kUploadSlot = (size_t)IRIS_UPLOAD_SLOT_MB << 20;  // bytes per pinned upload slot
 constexpr int kUploadSlots = kUploadRing;                       // slots per device (iris_handles.hpp)
-#ifndef IRIS_PINNED_UPLOAD_MIN_MB
-#define IRIS_PINNED_UPLOAD_MIN_MB 128
-#endif
-constexpr size_t kPinnedUploadMin = (size_t)IRIS_PINNED_UPLOAD_MIN_MB << 20;  // smaller writes: one runtime-staged copy
 constexpr size_t kUploadPieceMin = 4ull << 20;  // a write is cut into at least 4 slots of at least this
+constexpr size_t kUploadTuneMin = 8ull << 20;   // writes from this size choose their path by measurement (UploadTune)
 
 }  // namespace
 
-// A large write: the helper threads copy each slot's records from the caller's pageable array
-// into one of two pinned buffers, the copy engine moves it to one of two device staging slots
-// and the pack kernel stores it, while the host already fills the other pinned buffer.  The
-// runtime's copy of a pageable source ran at 29-30 GB/s for some caller arrays (records read
-// back from the device, on either NUMA node) and 53 GB/s for others; this path moved 48-52 GB/s
-// for both (profiles/r04_host_upload.txt).  IRIS_UPLOAD=runtime (test hook) keeps the runtime's.
+// A large write through pinned slots: the helper threads copy each slot's records from the
+// caller's pageable array into one of two pinned buffers, the copy engine moves it to one of two
+// device staging slots and the pack kernel stores it, while the host already fills the other
+// pinned buffer.  The runtime's copy of a pageable source ran at 29-30 GB/s for some caller arrays
+// and 53 GB/s for others; this path moved 48-52 GB/s for both (profiles/r04_host_upload.txt).
+// Writes of 8 MB and more take whichever of the two was faster lately (UploadTune);
+// IRIS_UPLOAD=pinned|runtime (test hook) pins one.
 int iris_api::db_write_pinned(iris_db *db, uint64_t index, const void *records, uint64_t n) {
     iris_device *d = db->dev;
     const KindInfo &k = db->k;
@@ -108,6 +107,8 @@ int iris_api::db_write_pinned(iris_db *db, uint64_t index, const void *records, 
 
 namespace {
 
+int db_write_runtime(iris_db *db, uint64_t index, const void *records, uint64_t n);
+
 int db_write_locked(iris_db *db, uint64_t index, const void *records, uint64_t n) {
     iris_device *d = db->dev;
     db_detach(db);
@@ -117,7 +118,23 @@ int db_write_locked(iris_db *db, uint64_t index, const void *records, uint64_t n
     ARG(records != nullptr, "iris_db_write: records is NULL");
     const KindInfo &k = db->k;
     const size_t bytes = (size_t)n * k.rec_bytes;
-    if (IRIS_PINNED_UPLOAD && bytes >= kPinnedUploadMin && d->hooks.upload != 2) return db_write_pinned(db, index, records, n);
+    if (IRIS_PINNED_UPLOAD && d->hooks.upload == 1 && bytes >= kUploadTuneMin) return db_write_pinned(db, index, records, n);
+    if (IRIS_PINNED_UPLOAD && d->hooks.upload == 0 && bytes >= kUploadTuneMin) {
+        // the faster path for this caller's arrays, as measured on its recent writes
+        UploadTune &u = d->upload_tune;
+        const int path = u.pick();
+        const auto t0 = std::chrono::steady_clock::now();
+        CHK(path == 0 ? db_write_pinned(db, index, records, n) : db_write_runtime(db, index, records, n));
+        u.record(path, (double)bytes / std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+        return 0;
+    }
+    return db_write_runtime(db, index, records, n);
+}
+
+// The runtime's copy of the pageable source, through one 256-MB staging chunk at a time.
+int db_write_runtime(iris_db *db, uint64_t index, const void *records, uint64_t n) {
+    iris_device *d = db->dev;
+    const KindInfo &k = db->k;
     const uint64_t ch = chunk_records(k);
     CHK(ensure(d->staging, std::min<uint64_t>(n, ch) * k.rec_bytes));
     for (uint64_t done = 0; done < n; done += ch) {
@@ -584,7 +601,12 @@ int iris_config(const iris_device_t *d, char *buf, size_t len, size_t *needed) {
     if (!d) read_hooks(&now);
     std::string s(format_hooks(d ? d->hooks : now, nullptr, 0), '\0');
     format_hooks(d ? d->hooks : now, &s[0], s.size() + 1);
-    if (d) s += " numa_node=" + std::to_string(d->numa_node);  // where large writes' pages are compared
+    if (d) {
+        s += " numa_node=" + std::to_string(d->numa_node);
+        char r[96];  // large writes' measured rates (GB/s) through the pinned slots / the runtime's copy
+        snprintf(r, sizeof(r), " upload_gbps=%.1f/%.1f", d->upload_tune.gbps[0] / 1e9, d->upload_tune.gbps[1] / 1e9);
+        s += r;
+    }
     if (buf && len) {
         const size_t n = std::min(len - 1, s.size());
         memcpy(buf, s.data(), n);

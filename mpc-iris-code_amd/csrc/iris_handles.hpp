@@ -63,6 +63,28 @@ struct DevBuf {
 #endif
 constexpr int kUploadRing = IRIS_UPLOAD_SLOTS;  // pinned upload slots per device (db_write_pinned)
 
+// The path of a device's large writes (db_write_locked): the helper threads' pinned slots (0) or the
+// runtime's copy of the pageable source (1).  Which is faster depends on the caller's array -- the
+// runtime's copy ran some arrays at 29-30 GB/s and others at 53, the slots both at 48-52
+// (profiles/r04_host_upload.txt, r04_upload_participant.txt) -- so each path's recent rate is kept
+// (EWMA) and the faster one taken, the other re-measured every 16th write.
+struct UploadTune {
+    double gbps[2] = {0, 0};  // bytes per second, EWMA
+    uint32_t n[2] = {0, 0};
+    uint64_t writes = 0;
+    int pick() {
+        const uint64_t w = writes++;
+        if (n[0] == 0) return 0;
+        if (n[1] == 0) return 1;
+        const int best = gbps[0] >= gbps[1] ? 0 : 1;
+        return w % 16 == 15 ? best ^ 1 : best;
+    }
+    void record(int p, double rate) {
+        gbps[p] = n[p] == 0 ? rate : 0.75 * gbps[p] + 0.25 * rate;
+        ++n[p];
+    }
+};
+
 struct iris_device {
     int ordinal = 0;
     int numa_node = -1;  // host NUMA node of the device's PCI function (-1: unknown)
@@ -108,6 +130,7 @@ struct iris_device {
     void *upin[kUploadRing] = {};
     size_t upin_cap = 0;
     hipEvent_t upin_ev[kUploadRing] = {};
+    UploadTune upload_tune;
     // recorded on the device stream before every read-ahead launch and waited for by the side
     // stream: the launch follows whatever the device stream holds (the engine's query build,
     // writes to the database)

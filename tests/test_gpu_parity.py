@@ -815,9 +815,9 @@ def test_persistent_search_ranges_vs_oracle(device):
 
 @pytest.mark.parametrize("path", ["pinned", "runtime"])
 def test_large_write_paths(hooked_device, path):
-    """Database writes of at least 128 MB go through two pinned slots filled by the helper threads, or
-    (IRIS_UPLOAD=runtime) the runtime's copy of the pageable source: both store the same records,
-    including an unaligned start index and a last slot shorter than the others."""
+    """Database writes of at least 8 MB go through two pinned slots filled by the helper threads or the
+    runtime's copy of the pageable source (by measured rate; IRIS_UPLOAD pins one): both store the
+    same records, including an unaligned start index and a last slot shorter than the others."""
     dev = hooked_device(IRIS_UPLOAD=path)
     assert dev.config()["upload"] == path
     rng = np.random.default_rng(11)
@@ -833,3 +833,21 @@ def test_large_write_paths(hooked_device, path):
             sdb.append(shares)
             for lo in (0, 2_559, 2_560, 5_250):
                 assert (sdb.read(lo, 50) == shares[lo:lo + 50]).all(), lo
+
+
+def test_upload_path_tuning(hooked_device):
+    """Without a pinned path, writes of 8 MB and more measure both paths on their first two writes and
+    then take the faster one, re-measuring the other every 16th write; iris_config reports the rates.
+    Every write stores the same records whichever path it took."""
+    dev = hooked_device()
+    rng = np.random.default_rng(12)
+    masks = rng.integers(0, 2**64, (10_000, 200), dtype=np.uint64)  # 16 MB per write
+    with ih.Database(dev, ih.KIND_MASKS, 10_000) as db:
+        for i in range(20):
+            db.truncate(0)
+            db.append(masks if i % 2 == 0 else masks[::-1].copy())
+            want = masks if i % 2 == 0 else masks[::-1]
+            for lo in (0, 4_321, 9_950):
+                assert (db.read(lo, 50) == want[lo:lo + 50]).all(), (i, lo)
+    pinned, runtime = (float(x) for x in dev.config()["upload_gbps"].split("/"))
+    assert pinned > 0 and runtime > 0
