@@ -148,11 +148,17 @@ int db_write_runtime(iris_db *db, uint64_t index, const void *records, uint64_t 
     return 0;
 }
 
-// A transient device DB holding host records (the host-slice engine forms).
+// A transient device DB holding host records (the host-slice engine forms).  Its memory is the
+// device's cached workspace (grown on demand, kept until the device closes): a hipMalloc + hipFree
+// per call cost a participant-sized upload call ~0.1 ms.  Callers hold the device lock.
+#ifndef IRIS_TEMPDB_CACHE  // 0: allocate and free per call (A/B builds)
+#define IRIS_TEMPDB_CACHE 1
+#endif
 struct TempDb {
     iris_db db;
+    bool owned = false;
     ~TempDb() {
-        if (db.data) (void)hipFree(db.data);
+        if (owned && db.data) (void)hipFree(db.data);
     }
 };
 
@@ -162,8 +168,15 @@ int temp_db(iris_device *d, int kind, uint64_t cap, TempDb &t) {
     t.db.cap = (cap + t.db.k.block - 1) / t.db.k.block * t.db.k.block;
     t.db.len = 0;
     const size_t bytes = std::max<uint64_t>(1, t.db.cap / t.db.k.block) * block_bytes(t.db.k);
-    hipError_t e = hipMalloc(&t.db.data, bytes);
-    if (e != hipSuccess) return fail(IRIS_E_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+    if (IRIS_TEMPDB_CACHE) {
+        CHK(ensure(d->tempdb, bytes));
+        t.db.data = d->tempdb.p;
+    } else {
+        hipError_t e = hipMalloc(&t.db.data, bytes);
+        if (e != hipSuccess) return fail(IRIS_E_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+        t.owned = true;
+    }
+    // the last block's records past the range stay zero (as a fresh database's)
     HIPCHK(hipMemsetAsync(t.db.data, 0, bytes, d->stream));
     return 0;
 }
@@ -529,7 +542,7 @@ void device_teardown(iris_device *d) {
         std::lock_guard<std::recursive_mutex> g(d->mu);
         (void)hipSetDevice(d->ordinal);
         (void)hipStreamSynchronize(d->stream);
-        for (DevBuf *b : {&d->partials, &d->result, &d->staging, &d->out_a, &d->out_b, &d->ticket})
+        for (DevBuf *b : {&d->partials, &d->result, &d->staging, &d->out_a, &d->out_b, &d->ticket, &d->tempdb})
             if (b->p) (void)hipFree(b->p);
         if (d->aux) (void)hipStreamSynchronize(d->aux);
         for (int b = 0; b < 2; ++b) {

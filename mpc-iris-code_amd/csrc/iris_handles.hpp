@@ -96,6 +96,7 @@ struct iris_device {
     std::vector<Pending> pending;
     std::vector<hipEvent_t> event_pool;
     DevBuf partials, result, staging, out_a, out_b;
+    DevBuf tempdb;  // the host-slice calls' transient database (TempDb, iris_api.hip)
     // zeroed device word of the fused (last-workgroup) search reduce; searches on the stream
     // are serialised, and each launch leaves it zeroed
     DevBuf ticket;
