@@ -124,7 +124,12 @@ int db_write_locked(iris_db *db, uint64_t index, const void *records, uint64_t n
         UploadTune &u = d->upload_tune;
         const int path = u.pick();
         const auto t0 = std::chrono::steady_clock::now();
-        CHK(path == 0 ? db_write_pinned(db, index, records, n) : db_write_runtime(db, index, records, n));
+        int rc = path == 0 ? db_write_pinned(db, index, records, n) : db_write_runtime(db, index, records, n);
+        if (rc == IRIS_E_NOMEM && path == 0) {  // no pinned host memory for the slots: the runtime's copy from now on
+            u.no_pinned = true;
+            return db_write_runtime(db, index, records, n);
+        }
+        CHK(rc);
         u.record(path, (double)bytes / std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
         return 0;
     }
@@ -217,7 +222,11 @@ int run_u16_engine(iris_engine *e, const iris_db *db, uint64_t first, uint64_t n
 #ifndef IRIS_PINNED_ROWS  // 0: rows through a device buffer and a copy-engine D2H (A/B builds)
 #define IRIS_PINNED_ROWS 1
 #endif
-    if (IRIS_PINNED_ROWS && db->k.layout == IRIS_LAYOUT_TILES) return run_u16_engine_pinned(e, db, first, n, out);
+    if (IRIS_PINNED_ROWS && db->k.layout == IRIS_LAYOUT_TILES) {
+        // out of pinned host memory for the row buffers (nothing launched yet): the device-buffer form
+        const int rc = run_u16_engine_pinned(e, db, first, n, out);
+        if (rc != IRIS_E_NOMEM) return rc;
+    }
     CHK(ensure(d->out_a, std::min<uint64_t>(n, kU16Chunk) * kRot * 2));
     for (uint64_t done = 0; done < n; done += kU16Chunk) {
         const uint64_t m = std::min<uint64_t>(kU16Chunk, n - done);

@@ -72,8 +72,10 @@ struct UploadTune {
     double gbps[2] = {0, 0};  // bytes per second, EWMA
     uint32_t n[2] = {0, 0};
     uint64_t writes = 0;
+    bool no_pinned = false;  // the slots' pinned buffers could not be allocated
     int pick() {
         const uint64_t w = writes++;
+        if (no_pinned) return 1;
         if (n[0] == 0) return 0;
         if (n[1] == 0) return 1;
         const int best = gbps[0] >= gbps[1] ? 0 : 1;
