@@ -41,6 +41,26 @@ constexpr int kUploadSlots = kUploadRing;                       // slots per dev
 constexpr size_t kUploadPieceMin = 4ull << 20;  // a write is cut into at least 4 slots of at least this
 constexpr size_t kUploadTuneMin = 8ull << 20;   // writes from this size choose their path by measurement (UploadTune)
 
+// The device's pinned upload slots (kUploadSlot bytes each) and their events, allocated once.
+int ensure_upin(iris_device *d) {
+    if (d->upin_cap >= kUploadSlot) return 0;
+    CHK(sync(d));  // no copy uses the old buffers any more
+    for (int b = 0; b < kUploadSlots; ++b)
+        if (d->upin[b]) HIPCHK(hipHostFree(d->upin[b]));
+    for (int b = 0; b < kUploadSlots; ++b) d->upin[b] = nullptr;
+    for (int b = 0; b < kUploadSlots; ++b) {
+        const hipError_t e = hipHostMalloc(&d->upin[b], kUploadSlot, hipHostMallocDefault);
+        if (e != hipSuccess) {
+            d->upin[b] = nullptr;
+            return fail(IRIS_E_NOMEM, std::string("hipHostMalloc upload buffer: ") + hipGetErrorString(e));
+        }
+    }
+    for (int b = 0; b < kUploadSlots; ++b)
+        if (!d->upin_ev[b]) HIPCHK(hipEventCreateWithFlags(&d->upin_ev[b], hipEventDisableTiming));
+    d->upin_cap = kUploadSlot;
+    return 0;
+}
+
 }  // namespace
 
 // A large write through pinned slots: the helper threads copy each slot's records from the
@@ -58,23 +78,7 @@ int iris_api::db_write_pinned(iris_db *db, uint64_t index, const void *records, 
     const uint64_t ch = std::max<uint64_t>(64, piece / k.rec_bytes / 64 * 64);
     const size_t slot = (size_t)ch * k.rec_bytes;
     CHK(ensure(d->staging, kUploadSlots * slot));
-    if (d->upin_cap < slot) {
-        CHK(sync(d));  // no copy reads the old buffers any more
-        for (int b = 0; b < kUploadSlots; ++b)
-            if (d->upin[b]) HIPCHK(hipHostFree(d->upin[b]));
-        for (int b = 0; b < kUploadSlots; ++b) d->upin[b] = nullptr;
-        d->upin_cap = 0;
-        for (int b = 0; b < kUploadSlots; ++b) {
-            const hipError_t e = hipHostMalloc(&d->upin[b], kUploadSlot, hipHostMallocDefault);
-            if (e != hipSuccess) {
-                d->upin[b] = nullptr;
-                return fail(IRIS_E_NOMEM, std::string("hipHostMalloc upload buffer: ") + hipGetErrorString(e));
-            }
-        }
-        for (int b = 0; b < kUploadSlots; ++b)
-            if (!d->upin_ev[b]) HIPCHK(hipEventCreateWithFlags(&d->upin_ev[b], hipEventDisableTiming));
-        d->upin_cap = kUploadSlot;
-    }
+    CHK(ensure_upin(d));
     int rc = 0;
     uint64_t c = 0;
     for (uint64_t done = 0; done < n && rc == 0; done += ch, ++c) {
@@ -897,6 +901,40 @@ int iris_db_read(const iris_db_t *db, uint64_t first, uint64_t n, void *records)
     if (n == 0) return 0;
     ARG(records, "records is NULL");
     const KindInfo &k = db->k;
+#ifndef IRIS_PINNED_READ  // 0: every read through the runtime's copy into the pageable array (A/B builds)
+#define IRIS_PINNED_READ 1
+#endif
+    if (IRIS_PINNED_READ && (size_t)n * k.rec_bytes >= kUploadTuneMin && ensure_upin(d) == 0) {
+        // the upload slots run backwards: slot c is unpacked and copied into pinned buffer c % 2 by the
+        // device while the helper threads copy slot c - 1 into the caller's array
+        const uint64_t ch = std::max<uint64_t>(64, kUploadSlot / k.rec_bytes / 64 * 64);
+        const size_t slot = (size_t)ch * k.rec_bytes;
+        CHK(ensure(d->staging, kUploadSlots * slot));
+        const uint64_t chunks = (n + ch - 1) / ch;
+        int rc = 0;
+        auto enqueue = [&](uint64_t c) -> int {
+            const int b = (int)(c % kUploadSlots);
+            const uint64_t a = c * ch, m = std::min<uint64_t>(ch, n - a);
+            void *stage = (char *)d->staging.p + (size_t)b * slot;
+            CHK(timed(d, "unpack", m, [&] { return launch_unpack(d->stream, k, db->data, stage, first + a, m); }));
+            HIPCHK(hipMemcpyAsync(d->upin[b], stage, (size_t)m * k.rec_bytes, hipMemcpyDeviceToHost, d->stream));
+            HIPCHK(hipEventRecord(d->upin_ev[b], d->stream));
+            return 0;
+        };
+        rc = enqueue(0);
+        for (uint64_t c = 0; c < chunks && rc == 0; ++c) {
+            // pinned buffer (c + 1) % slots was last read by the (synchronous) copy-out of slot c + 1 - slots
+            if (c + 1 < chunks) rc = enqueue(c + 1);
+            if (rc == 0 && hipEventSynchronize(d->upin_ev[c % kUploadSlots]) != hipSuccess) rc = fail(IRIS_E_HIP, "hipEventSynchronize");
+            if (rc == 0) {
+                const uint64_t a = c * ch, m = std::min<uint64_t>(ch, n - a);
+                parallel_copy((char *)records + a * k.rec_bytes, d->upin[c % kUploadSlots], (size_t)m * k.rec_bytes, d->ordinal);
+            }
+        }
+        const int rs = sync(d);
+        CHK(rc);
+        return rs;
+    }
     const uint64_t ch = chunk_records(k);
     CHK(ensure(d->staging, std::min<uint64_t>(n, ch) * k.rec_bytes));
     for (uint64_t done = 0; done < n; done += ch) {
