@@ -93,12 +93,16 @@ const char *iris_version(void);
 /* Runtime configuration, read from the environment once when a device opens:
  * "key=value ..." into buf (NUL-terminated, truncated to len); *needed (may be
  * NULL) receives the full length without the NUL.  dev == NULL: what a device
- * opened now would use.  Production knobs: IRIS_READAHEAD, IRIS_GROUP_TIMEOUT_MS,
- * IRIS_COPY_HELPERS (process-wide).  Test-only hooks (IRIS_TILES_PER_WAVE,
- * IRIS_FUSED_REDUCE, IRIS_BATCH_KERNEL, IRIS_BATCH_XQG, IRIS_SCHEDULE,
- * IRIS_LOAD_PREAD, IRIS_GROUP_DELAY_US, IRIS_GROUP_STALL, IRIS_GROUP_UNORDERED)
- * take effect only with IRIS_TEST_HOOKS=1; otherwise they are ignored and listed
- * as "ignored=...". */
+ * opened now would use.  Production knobs: IRIS_READAHEAD, IRIS_AUTO_RESIDENT,
+ * IRIS_GROUP_TIMEOUT_MS, IRIS_COPY_HELPERS (process-wide).  Test-only hooks
+ * (IRIS_TILES_PER_WAVE, IRIS_FUSED_REDUCE, IRIS_BATCH_KERNEL, IRIS_SCHEDULE,
+ * IRIS_LOAD_PREAD, IRIS_LOAD_WINDOWS, IRIS_GROUP_DELAY_US, IRIS_GROUP_STALL,
+ * IRIS_GROUP_UNORDERED, IRIS_UPLOAD) take effect only with IRIS_TEST_HOOKS=1;
+ * otherwise they are ignored and listed as "ignored=...".  With dev != NULL the
+ * device's own facts follow: numa_node= (host NUMA node of its PCI function, -1
+ * unknown), upload_gbps=P/R (recent rates of large writes through the pinned
+ * slots / the runtime's copy, GB/s; 0 = not measured yet) and resident= (the
+ * record files it keeps resident for host-slice calls: count and bytes). */
 int iris_config(const iris_device_t *dev, char *buf, size_t len, size_t *needed);
 
 /* --------------------------------------------------------------- devices */

@@ -30,13 +30,7 @@ using namespace iris_api;
 
 namespace {
 
-#ifndef IRIS_PINNED_UPLOAD  // 0: every write through the runtime's staging of pageable copies (A/B builds)
-#define IRIS_PINNED_UPLOAD 1
-#endif
-#ifndef IRIS_UPLOAD_SLOT_MB
-#define IRIS_UPLOAD_SLOT_MB 64
-#endif
-constexpr size_t kUploadSlot = (size_t)IRIS_UPLOAD_SLOT_MB << 20;  // bytes per pinned upload slot
+constexpr size_t kUploadSlot = 64ull << 20;  // bytes per pinned upload slot
 constexpr int kUploadSlots = kUploadRing;                       // slots per device (iris_handles.hpp)
 constexpr size_t kUploadPieceMin = 4ull << 20;  // a write is cut into at least 4 slots of at least this
 constexpr size_t kUploadTuneMin = 8ull << 20;   // writes from this size choose their path by measurement (UploadTune)
@@ -70,7 +64,7 @@ int ensure_upin(iris_device *d) {
 // and 53 GB/s for others; this path moved 48-52 GB/s for both (profiles/r04_host_upload.txt).
 // Writes of 8 MB and more take whichever of the two was faster lately (UploadTune);
 // IRIS_UPLOAD=pinned|runtime (test hook) pins one.
-int iris_api::db_write_pinned(iris_db *db, uint64_t index, const void *records, uint64_t n) {
+int iris_api::db_write_pinned(iris_db *db, uint64_t index, const void *records, uint64_t n, const SlotFill *fill) {
     iris_device *d = db->dev;
     const KindInfo &k = db->k;
     // at least four slots per write (so the host's copy of one overlaps the copy engine's of another)
@@ -90,7 +84,14 @@ int iris_api::db_write_pinned(iris_db *db, uint64_t index, const void *records, 
             rc = fail(IRIS_E_HIP, "hipEventSynchronize");
             break;
         }
-        parallel_copy(d->upin[b], (const char *)records + done * k.rec_bytes, (size_t)m * k.rec_bytes, d->ordinal);
+        if (fill) {
+            if (!(*fill)(d->upin[b], (size_t)done * k.rec_bytes, (size_t)m * k.rec_bytes)) {
+                rc = fail(IRIS_E_IO, "read failed (I/O error, or the file shrank under the load)");
+                break;
+            }
+        } else {
+            parallel_copy(d->upin[b], (const char *)records + done * k.rec_bytes, (size_t)m * k.rec_bytes, d->ordinal);
+        }
         void *stage = (char *)d->staging.p + (size_t)b * slot;
         if (hipMemcpyAsync(stage, d->upin[b], (size_t)m * k.rec_bytes, hipMemcpyHostToDevice, d->stream) != hipSuccess) {
             rc = fail(IRIS_E_HIP, "hipMemcpyAsync upload");
@@ -122,8 +123,8 @@ int db_write_locked(iris_db *db, uint64_t index, const void *records, uint64_t n
     ARG(records != nullptr, "iris_db_write: records is NULL");
     const KindInfo &k = db->k;
     const size_t bytes = (size_t)n * k.rec_bytes;
-    if (IRIS_PINNED_UPLOAD && d->hooks.upload == 1 && bytes >= kUploadTuneMin) return db_write_pinned(db, index, records, n);
-    if (IRIS_PINNED_UPLOAD && d->hooks.upload == 0 && bytes >= kUploadTuneMin) {
+    if (d->hooks.upload == 1 && bytes >= kUploadTuneMin) return db_write_pinned(db, index, records, n);
+    if (d->hooks.upload == 0 && bytes >= kUploadTuneMin) {
         // the faster path for this caller's arrays, as measured on its recent writes
         UploadTune &u = d->upload_tune;
         const int path = u.pick();
@@ -160,15 +161,8 @@ int db_write_runtime(iris_db *db, uint64_t index, const void *records, uint64_t 
 // A transient device DB holding host records (the host-slice engine forms).  Its memory is the
 // device's cached workspace (grown on demand, kept until the device closes): a hipMalloc + hipFree
 // per call cost a participant-sized upload call ~0.1 ms.  Callers hold the device lock.
-#ifndef IRIS_TEMPDB_CACHE  // 0: allocate and free per call (A/B builds)
-#define IRIS_TEMPDB_CACHE 1
-#endif
 struct TempDb {
     iris_db db;
-    bool owned = false;
-    ~TempDb() {
-        if (owned && db.data) (void)hipFree(db.data);
-    }
 };
 
 int temp_db(iris_device *d, int kind, uint64_t cap, TempDb &t) {
@@ -177,14 +171,8 @@ int temp_db(iris_device *d, int kind, uint64_t cap, TempDb &t) {
     t.db.cap = (cap + t.db.k.block - 1) / t.db.k.block * t.db.k.block;
     t.db.len = 0;
     const size_t bytes = std::max<uint64_t>(1, t.db.cap / t.db.k.block) * block_bytes(t.db.k);
-    if (IRIS_TEMPDB_CACHE) {
-        CHK(ensure(d->tempdb, bytes));
-        t.db.data = d->tempdb.p;
-    } else {
-        hipError_t e = hipMalloc(&t.db.data, bytes);
-        if (e != hipSuccess) return fail(IRIS_E_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
-        t.owned = true;
-    }
+    CHK(ensure(d->tempdb, bytes));
+    t.db.data = d->tempdb.p;
     // the last block's records past the range stay zero (as a fresh database's)
     HIPCHK(hipMemsetAsync(t.db.data, 0, bytes, d->stream));
     return 0;
@@ -223,10 +211,7 @@ int run_u16_engine_pinned(iris_engine *e, const iris_db *db, uint64_t first, uin
 // Engine kernel over [first, first+n) of db, u16 [n][31] outputs to host.
 int run_u16_engine(iris_engine *e, const iris_db *db, uint64_t first, uint64_t n, uint16_t *out) {
     iris_device *d = e->dev;
-#ifndef IRIS_PINNED_ROWS  // 0: rows through a device buffer and a copy-engine D2H (A/B builds)
-#define IRIS_PINNED_ROWS 1
-#endif
-    if (IRIS_PINNED_ROWS && db->k.layout == IRIS_LAYOUT_TILES) {
+    if (db->k.layout == IRIS_LAYOUT_TILES) {
         // out of pinned host memory for the row buffers (nothing launched yet): the device-buffer form
         const int rc = run_u16_engine_pinned(e, db, first, n, out);
         if (rc != IRIS_E_NOMEM) return rc;
@@ -901,10 +886,7 @@ int iris_db_read(const iris_db_t *db, uint64_t first, uint64_t n, void *records)
     if (n == 0) return 0;
     ARG(records, "records is NULL");
     const KindInfo &k = db->k;
-#ifndef IRIS_PINNED_READ  // 0: every read through the runtime's copy into the pageable array (A/B builds)
-#define IRIS_PINNED_READ 1
-#endif
-    if (IRIS_PINNED_READ && (size_t)n * k.rec_bytes >= kUploadTuneMin && ensure_upin(d) == 0) {
+    if ((size_t)n * k.rec_bytes >= kUploadTuneMin && ensure_upin(d) == 0) {
         // the upload slots run backwards: slot c is unpacked and copied into pinned buffer c % 2 by the
         // device while the helper threads copy slot c - 1 into the caller's array
         const uint64_t ch = std::max<uint64_t>(64, kUploadSlot / k.rec_bytes / 64 * 64);
@@ -1116,10 +1098,7 @@ int iris_engine_batch_process_device(iris_engine_t *e, const iris_db_t *db, uint
     // host memory once every row is stored, and the call returns when it lands (as the small
     // search does) -- later work on the device stream, the rows' consumers, follows the kernel
     DoneSignal sig{};
-#ifndef IRIS_DEVICE_OUT_DONE  // 0: wait for the stream instead (A/B builds)
-#define IRIS_DEVICE_OUT_DONE 1
-#endif
-    if (IRIS_DEVICE_OUT_DONE && db->k.layout == IRIS_LAYOUT_TILES) {
+    if (db->k.layout == IRIS_LAYOUT_TILES) {
         CHK(ensure_ticket(d));
         CHK(ensure_host_done(d));
         sig.ticket = (uint32_t *)d->ticket.p;

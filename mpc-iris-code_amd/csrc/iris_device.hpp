@@ -42,14 +42,10 @@ __device__ __forceinline__ void store16_wt(uint4 *dst, const uint4 &v) {
 // through L2 (sc1), so once the storing wave's vmcnt(0) wait returns the rows are in memory, where a
 // reader on any XCD -- a kernel on another stream, a copy engine -- finds them without this launch's
 // end-of-kernel write-back (nontemporal and plain stores stay dirty in the XCD's L2 until then).
-#ifndef IRIS_ROWS_WT
-#define IRIS_ROWS_WT 1  // 0: the signalling kernels store like the others (A/B builds of the visibility test)
-#endif
 template <class F>
 __device__ __forceinline__ void store_tile_rows(uint16_t *__restrict__ out, uint16_t *lds, uint64_t tile_t0,
                                                 uint64_t first, uint64_t end, bool tile_valid, int lane, F val,
                                                 bool wt = false) {
-    wt = wt && IRIS_ROWS_WT;
     const int h = lane >> 5;
     const bool full = tile_valid && tile_t0 >= first && tile_t0 + 32 <= end && ((tile_t0 - first) & 7) == 0 &&
                       (((uintptr_t)out & 15) == 0);
@@ -62,26 +58,15 @@ __device__ __forceinline__ void store_tile_rows(uint16_t *__restrict__ out, uint
         uint4 *dst = (uint4 *)(out + (tile_t0 - first) * kRot);
         const uint4 *src = (const uint4 *)lds;
         // streamed out with nontemporal stores: the rows are not re-read by this launch
-#ifndef IRIS_STORE_PLAIN
-#define IRIS_STORE_PLAIN 0  // 1: plain (write-back) stores instead of nontemporal
-#endif
-#ifndef IRIS_STORE_DIAG
-#define IRIS_STORE_DIAG 0
-#endif
-        // diagnostic builds only (results wrong by design): 1 = half the row bytes, 2 = none
-        constexpr int kStores = IRIS_STORE_DIAG == 0 ? 32 * kRot * 2 / 16 : IRIS_STORE_DIAG == 1 ? 32 * kRot / 16 : 0;
+        constexpr int kStores = 32 * kRot * 2 / 16;
         if (wt) {  // wave-uniform
             for (int i = lane; i < kStores; i += 64) store16_wt(&dst[i], src[i]);
             return;
         }
         for (int i = lane; i < kStores; i += 64) {
             const uint4 v = src[i];
-#if IRIS_STORE_PLAIN
-            dst[i] = v;
-#else
             const u32x4_nt w = {v.x, v.y, v.z, v.w};
             __builtin_nontemporal_store(w, (u32x4_nt *)&dst[i]);
-#endif
         }
     } else {
         const uint64_t tg = tile_t0 + (lane & 31);
@@ -198,12 +183,8 @@ __device__ __forceinline__ Partial partial_none() {
 // visibility: the first hand-off row), folds them in the
 // search order (exact fraction, then lowest index), writes the winner with idx + idx_base to
 // fin.dst (pinned host or device memory) and resets the ticket for the next launch.
-// agent scope (sc1 stores / loads, the form of MI355X_MICROARCH.md's first hand-off row) or
-// system scope (sc0 sc1: through to memory); IRIS_FUSED_SYSTEM=1 selects the latter
-#ifndef IRIS_FUSED_SYSTEM
-#define IRIS_FUSED_SYSTEM 0
-#endif
-#define IRIS_FUSED_SCOPE (IRIS_FUSED_SYSTEM ? __HIP_MEMORY_SCOPE_SYSTEM : __HIP_MEMORY_SCOPE_AGENT)
+// at agent scope (sc1 stores / loads, the form of MI355X_MICROARCH.md's first hand-off row)
+#define IRIS_FUSED_SCOPE __HIP_MEMORY_SCOPE_AGENT
 __device__ __forceinline__ void publish_partial(Partial *p, const Partial &b) {
     uint64_t *w = (uint64_t *)p;
     __hip_atomic_store(w, (uint64_t)b.num | ((uint64_t)b.den << 32), __ATOMIC_RELAXED, IRIS_FUSED_SCOPE);

@@ -27,40 +27,25 @@ typedef float v16f __attribute__((ext_vector_type(16)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kTile = 32;
-#ifndef IRIS_MASKS_T
-#define IRIS_MASKS_T 7
-#endif
-#ifndef IRIS_MASKS_BPC
-#define IRIS_MASKS_BPC 2
-#endif
 // tiles per wave: 7 for the [u16;31] output (longer groups, fewer store bursts than 4:
 // round 2 measured 8 at 2.88-2.98 vs 2.98-3.03 ms per 10M for 4; but 8 tiles need 29 VGPRs
 // of scratch spills at two waves per SIMD, and 7 -- 252 VGPRs, none spilled -- runs 2.894-2.896
 // vs 2.916-2.919 ms for 8, 2.894-2.900 for 6, 2.910-2.912 for 5, interleaved on one box,
 // profiles/r04_masks_variants.txt); the fused resolver keeps 4 (its epilogue state at 8 tiles
 // costs registers: 5.1 vs 2.7 ms)
-constexpr int kMasksTiles = IRIS_MASKS_T;
+constexpr int kMasksTiles = 7;
 constexpr int kResolveTiles = 4;
 template <int MODE>
 constexpr int masks_tiles() { return MODE == 0 ? kMasksTiles : kResolveTiles; }
-constexpr int kMasksBlocksPerCu = IRIS_MASKS_BPC;  // persistent grid: workgroups per CU
-// 1: the compact query (51 KB) is staged in LDS per workgroup; 0: read from L2 by every wave
-// (no LDS for it, so three workgroups fit a CU)
-#ifndef IRIS_MASKS_QLDS
-#define IRIS_MASKS_QLDS 1
-#endif
-// The fused resolver (4 tiles per wave, 168 VGPRs) runs three workgroups per CU with the query
-// read from L2: 2.78 vs 2.87 ms per 10M masks + 3 x 10M share rows, interleaved on one box
-// (profiles/r04_masks_variants.txt); for the [u16;31] output the same shape measured even (2.90-3.01
-// vs 2.93-3.00 ms), so MasksEngine keeps 8 tiles per wave at two workgroups per CU.
-#ifndef IRIS_RESOLVE_BPC
-#define IRIS_RESOLVE_BPC 3
-#endif
-#ifndef IRIS_RESOLVE_QLDS
-#define IRIS_RESOLVE_QLDS 0
-#endif
+constexpr int kMasksBlocksPerCu = 2;  // persistent grid: workgroups per CU
+// MasksEngine stages the compact query (51 KB) in LDS per workgroup (two workgroups per CU); the
+// fused resolver (4 tiles per wave, 168 VGPRs) runs three workgroups per CU with the query read
+// from L2 by every wave: 2.78 vs 2.87 ms per 10M masks + 3 x 10M share rows, interleaved on one
+// box (profiles/r04_masks_variants.txt); for the [u16;31] output the same shape measured even
+// (2.90-3.01 vs 2.93-3.00 ms).
+constexpr int kResolveBlocksPerCu = 3;
 template <int MODE>
-constexpr int masks_blocks_per_cu() { return MODE == 0 ? kMasksBlocksPerCu : IRIS_RESOLVE_BPC; }
+constexpr int masks_blocks_per_cu() { return MODE == 0 ? kMasksBlocksPerCu : kResolveBlocksPerCu; }
 constexpr int kSharesTiles = 2;
 
 __device__ __forceinline__ uint4 nt_load(const uint4 *p) {
@@ -101,11 +86,6 @@ __device__ __forceinline__ void mask_chunk(uint32_t x, const v8i &a, v16f &acc) 
     acc = mfma_fp4(a, b, acc);
 }
 
-// share-row loads of the fused resolver: plain by default (nontemporal measured the same,
-// 2.75-2.79 ms per 10M either way); 1 selects nontemporal
-#ifndef IRIS_RESOLVE_NT
-#define IRIS_RESOLVE_NT 0
-#endif
 // Fused resolver operands (MASKS_RESOLVE): the participants' [n][31] u16
 // outputs, row i = record first + i (src/main.rs:597-607).
 struct MaskResolve {
@@ -136,7 +116,7 @@ __global__ void __launch_bounds__(256, masks_blocks_per_cu<MODE>())
                       uint64_t first, uint64_t end, uint16_t *__restrict__ out, MaskResolve rs) {
     constexpr uint32_t kSteps = kMaskChunks / 4;  // 50 steps of 4 chunks
     const uint4 *sq = qfrag;  // the query's compact fragments: in LDS, or read from L2
-    if constexpr ((MODE == MASKS_OUT && IRIS_MASKS_QLDS) || (MODE != MASKS_OUT && IRIS_RESOLVE_QLDS)) {
+    if constexpr (MODE == MASKS_OUT) {
         __shared__ uint4 sq_lds[kMaskFragUint4];
         for (int i = threadIdx.x; i < (int)kMaskFragUint4; i += blockDim.x) sq_lds[i] = qfrag[i];
         __syncthreads();
@@ -167,12 +147,9 @@ __global__ void __launch_bounds__(256, masks_blocks_per_cu<MODE>())
         if (full) {  // wave-uniform: 124 16-B words per share array
             typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
             for (int i = lane; i < 32 * kRot / 8; i += 64) {
-                // read once: nontemporal, like the masks stream
-                u16x8 v = IRIS_RESOLVE_NT ? __builtin_nontemporal_load((const u16x8 *)(rs.shares[0] + e0 + 8 * i))
-                                          : *(const u16x8 *)(rs.shares[0] + e0 + 8 * i);
-                for (uint32_t p = 1; p < rs.parts; ++p)
-                    v += IRIS_RESOLVE_NT ? __builtin_nontemporal_load((const u16x8 *)(rs.shares[p] + e0 + 8 * i))
-                                         : *(const u16x8 *)(rs.shares[p] + e0 + 8 * i);
+                // plain loads (nontemporal measured the same, 2.75-2.79 ms per 10M either way)
+                u16x8 v = *(const u16x8 *)(rs.shares[0] + e0 + 8 * i);
+                for (uint32_t p = 1; p < rs.parts; ++p) v += *(const u16x8 *)(rs.shares[p] + e0 + 8 * i);
                 *(u16x8 *)&lds[8 * i] = v;
             }
         } else {

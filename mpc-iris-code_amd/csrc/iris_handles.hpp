@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <functional>
 #include <map>
 #include <mutex>
 #include <string>
@@ -58,10 +59,7 @@ struct DevBuf {
     size_t cap = 0;
 };
 
-#ifndef IRIS_UPLOAD_SLOTS
-#define IRIS_UPLOAD_SLOTS 2
-#endif
-constexpr int kUploadRing = IRIS_UPLOAD_SLOTS;  // pinned upload slots per device (db_write_pinned)
+constexpr int kUploadRing = 2;  // pinned upload slots per device (db_write_pinned)
 
 // The path of a device's large writes (db_write_locked): the helper threads' pinned slots (0) or the
 // runtime's copy of the pageable source (1).  Which is faster depends on the caller's array -- the
@@ -401,9 +399,13 @@ int template_engine_locked(iris_device *d, const iris_template_t *query, iris_en
 int search_enqueue(iris_engine *e, const iris_db *db, uint64_t first, uint64_t n, double *dist_dev, iris::Partial *dst,
                    bool side = false, hipEvent_t done = nullptr, uint64_t idx_base = 0, uint32_t *host_done = nullptr,
                    uint32_t seq = 0, bool *flagged = nullptr);
+// Fills dst with the source bytes [off, off + bytes) of a write; false on a read error (errno set).
+using SlotFill = std::function<bool(void *dst, size_t off, size_t bytes)>;
 // Stores host records [0, n) at database index `index` through two pinned 64-MB slots the helper
 // threads fill (caller holds the device lock; the database is detached already); waits for the device.
-int db_write_pinned(iris_db *db, uint64_t index, const void *records, uint64_t n);
+// fill (optional) fills the slots instead of a copy from `records` (e.g. pread from a file).
+// IRIS_E_NOMEM only before anything was written (the pinned slots or the staging buffer).
+int db_write_pinned(iris_db *db, uint64_t index, const void *records, uint64_t n, const SlotFill *fill = nullptr);
 // Partial (indices offset by base) -> iris_match_t; +inf / UINT64_MAX when none
 void match_from(const iris::Partial &r, bool any, uint64_t base, iris_match_t *out);
 

@@ -307,10 +307,10 @@ int copy_helpers() {  // IRIS_COPY_HELPERS (0..15) overrides, read when the pool
 namespace {
 
 // Test-only hooks in the order of Hooks::ignored's bits.
-constexpr const char *kHookNames[] = {"IRIS_TILES_PER_WAVE", "IRIS_FUSED_REDUCE", "IRIS_BATCH_KERNEL",
-                                      "IRIS_BATCH_XQG",      "IRIS_SCHEDULE",     "IRIS_LOAD_PREAD",
-                                      "IRIS_GROUP_DELAY_US", "IRIS_GROUP_STALL",  "IRIS_GROUP_UNORDERED",
-                                      "IRIS_UPLOAD"};
+constexpr const char *kHookNames[] = {"IRIS_TILES_PER_WAVE",  "IRIS_FUSED_REDUCE", "IRIS_BATCH_KERNEL",
+                                      "IRIS_SCHEDULE",        "IRIS_LOAD_PREAD",   "IRIS_GROUP_DELAY_US",
+                                      "IRIS_GROUP_STALL",     "IRIS_GROUP_UNORDERED", "IRIS_UPLOAD",
+                                      "IRIS_LOAD_WINDOWS"};
 constexpr int kNumHooks = (int)(sizeof(kHookNames) / sizeof(kHookNames[0]));
 
 const char *env(const char *name) {
@@ -341,14 +341,14 @@ void read_hooks(Hooks *h) {
         switch (i) {
         case 0: h->tiles_per_wave = atoi(v) == 1 ? 1 : 4; break;
         case 1: h->fused_reduce = v[0] != '0'; break;
-        case 2: h->batch_kernel = atoi(v) >= 1 && atoi(v) <= 4 ? atoi(v) : 4; break;
-        case 3: h->batch_xqg = env_u32(v, 32); break;
-        case 4: h->schedule = !strcmp(v, "spin") ? 1 : !strcmp(v, "yield") ? 2 : !strcmp(v, "blocking") ? 3 : 0; break;
-        case 5: h->load_pread = v[0] != '0'; break;
-        case 6: h->group_delay_us = env_u32(v, 1000000); break;
-        case 7: h->group_stall = v[0] != '0'; break;
-        case 8: h->group_unordered = v[0] != '0'; break;
-        case 9: h->upload = !strcmp(v, "pinned") ? 1 : !strcmp(v, "runtime") ? 2 : 0; break;
+        case 2: h->batch_kernel = atoi(v) == 2 ? 2 : 4; break;
+        case 3: h->schedule = !strcmp(v, "spin") ? 1 : !strcmp(v, "yield") ? 2 : !strcmp(v, "blocking") ? 3 : 0; break;
+        case 4: h->load_pread = v[0] != '0'; break;
+        case 5: h->group_delay_us = env_u32(v, 1000000); break;
+        case 6: h->group_stall = v[0] != '0'; break;
+        case 7: h->group_unordered = v[0] != '0'; break;
+        case 8: h->upload = !strcmp(v, "pinned") ? 1 : !strcmp(v, "runtime") ? 2 : 0; break;
+        case 9: h->load_windows = v[0] != '0'; break;
         }
     }
 }
@@ -362,8 +362,9 @@ size_t format_hooks(const Hooks &h, char *buf, size_t len) {
     if (h.test)
         s += " tiles_per_wave=" + (h.tiles_per_wave ? std::to_string(h.tiles_per_wave) : std::string("auto")) +
              " fused_reduce=" + std::to_string(h.fused_reduce) + " batch_kernel=" + std::to_string(h.batch_kernel) +
-             " batch_xqg=" + std::to_string(h.batch_xqg) + " schedule=" + sched[h.schedule & 3] +
-             " load_pread=" + std::to_string(h.load_pread) + " group_delay_us=" + std::to_string(h.group_delay_us) +
+             " schedule=" + sched[h.schedule & 3] +
+             " load_pread=" + std::to_string(h.load_pread) +
+             " load_windows=" + std::to_string(h.load_windows) + " group_delay_us=" + std::to_string(h.group_delay_us) +
              " group_stall=" + std::to_string(h.group_stall) + " group_unordered=" + std::to_string(h.group_unordered) +
              " upload=" + upload_names[h.upload & 3];
     std::string ign;

@@ -20,16 +20,6 @@
 #define IRIS_HD
 #endif
 
-// The shipped library (Makefile: LIB = libiris_hip.so) never carries a diagnostic knob:
-// those build kernels that drop work on purpose (tools/build_variant.sh variants only).
-#if defined(IRIS_SHIPPED_BUILD)
-#if (defined(IRIS_MFMA_DIAG) && IRIS_MFMA_DIAG) || (defined(IRIS_BATCH_DIAG) && IRIS_BATCH_DIAG) || \
-    (defined(IRIS_BATCH2_DIAG) && IRIS_BATCH2_DIAG) || (defined(IRIS_STORE_DIAG) && IRIS_STORE_DIAG) || \
-    (defined(IRIS_PREP_DIAG) && IRIS_PREP_DIAG)
-#error "diagnostic knob in the shipped libiris_hip.so"
-#endif
-#endif
-
 namespace iris {
 
 constexpr int kLanes = 64;            // records per block (= wavefront width)
@@ -187,10 +177,10 @@ struct Hooks {
     bool test = false;
     int tiles_per_wave = 0;          // IRIS_TILES_PER_WAVE=1|4: pins the TILES kernels' variant (0: by range)
     bool fused_reduce = true;        // IRIS_FUSED_REDUCE=0: small searches launch the separate reduce
-    int batch_kernel = 4;            // IRIS_BATCH_KERNEL=1..4: batched-query kernel form (iris_batch.hip)
-    uint32_t batch_xqg = 0;          // IRIS_BATCH_XQG: XCD-aware grid of batch kernel 1
+    int batch_kernel = 4;            // IRIS_BATCH_KERNEL=2|4: batched-query kernel shape (iris_batch.hip)
     int schedule = 0;                // IRIS_SCHEDULE=spin|yield|blocking (1|2|3): host wait mode
     bool load_pread = false;         // IRIS_LOAD_PREAD=1: file loads through the pinned-buffer path
+    bool load_windows = false;       // IRIS_LOAD_WINDOWS=1: file loads DMA from registered page-cache windows
     uint32_t group_delay_us = 0;     // IRIS_GROUP_DELAY_US: side-stream spin before each group all-gather
     bool group_stall = false;        // IRIS_GROUP_STALL=1: a group all-gather waits on a peer that never comes
     bool group_unordered = false;    // IRIS_GROUP_UNORDERED=1: drop the exchange-buffer ordering (shows the race)
@@ -282,10 +272,9 @@ struct BatchGeometry {
     uint64_t tile0, ntiles;
     uint32_t nqg, G;  // query groups, workgroups per query group
     uint32_t qper;    // queries per query group (nqg * qper results; at most the engine's padding)
-    uint32_t xqg;     // > 0: XCD-aware grid, xqg query groups per XCD at a time (iris_batch.hip)
 };
 BatchGeometry batch_geometry(const Hooks &h, LaunchRange r, uint32_t nq);
-uint32_t batch_query_group();  // queries per batch_kernel query group (padding unit)
+uint32_t batch_query_group();  // padding unit of a batched engine's queries
 int launch_batch(const Hooks &h, void *stream, const void *db, const void *qtiles, LaunchRange r, const BatchGeometry &g,
                  Partial *partials, Partial *out, uint64_t idx_base = 0);
 int launch_resolver(void *stream, const uint16_t *const *shares, uint32_t parts, const uint16_t *denoms, uint64_t n,

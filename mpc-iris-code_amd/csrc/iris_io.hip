@@ -155,9 +155,6 @@ int iris_db_load_file(iris_db_t *db, const char *path, uint64_t first, uint64_t 
         const bool force_pread = db->dev->hooks.load_pread;  // test hook: the fallback path
         void *map = pch <= ch && !force_pread ? ::mmap(nullptr, (size_t)size, PROT_READ, MAP_SHARED, f.fd, 0)
                                               : MAP_FAILED;
-#ifndef IRIS_LOAD_SLOTS  // 0: DMA from registered page-cache windows (A/B builds)
-#define IRIS_LOAD_SLOTS 1
-#endif
         // loads running at once in this process (a device group's per-device loads): those after the
         // first keep the registered windows, which take no host copy -- eight GPUs' slot copies
         // would all read host memory at once (unmeasured here: one GPU per box)
@@ -167,16 +164,23 @@ int iris_db_load_file(iris_db_t *db, const char *path, uint64_t first, uint64_t 
             InFlight() : before(loads.fetch_add(1)) {}
             ~InFlight() { loads.fetch_sub(1); }
         } in_flight;
-        if (IRIS_LOAD_SLOTS && map != MAP_FAILED && in_flight.before == 0) {
-            // the helper threads copy the mapping into two pinned slots while the copy engine drains
-            // the other (the path of large writes, db_write_pinned); the registered windows below
-            // moved 35-37 GB/s including their registration (profiles/r04_load_slots.txt)
-            (void)madvise(map, (size_t)size, MADV_SEQUENTIAL);
-            const int rc = db_write_pinned(db, base, (const char *)map + (size_t)first * k.rec_bytes, n);
-            ::munmap(map, (size_t)size);
-            CHK(rc);
-            if (loaded) *loaded = n;
-            return 0;
+        if (map != MAP_FAILED && in_flight.before == 0 && !d->hooks.load_windows) {
+            // reader threads pread the file into two pinned slots while the copy engine drains the
+            // other (the path of large writes, db_write_pinned); the registered windows below
+            // moved 35-37 GB/s including their registration (profiles/r04_load_slots.txt).  pread,
+            // not a copy out of the mapping: a file truncated under the load or a failing page is
+            // an IRIS_E_IO return, not a SIGBUS
+            const off_t off0 = (off_t)first * (off_t)k.rec_bytes;
+            const SlotFill fill = [&](void *dst, size_t off, size_t bytes) {
+                return parallel_io(f.fd, (char *)dst, bytes, off0 + (off_t)off, false);
+            };
+            const int rc = db_write_pinned(db, base, nullptr, n, &fill);
+            if (rc != IRIS_E_NOMEM) {  // no pinned memory for the slots: the registered windows below
+                ::munmap(map, (size_t)size);
+                CHK(rc);
+                if (loaded) *loaded = n;
+                return 0;
+            }
         }
         if (map != MAP_FAILED) {
             // hipHostUnregister waits for the device, so windows stay registered (their

@@ -32,24 +32,12 @@ typedef float v16f __attribute__((ext_vector_type(16)));
 
 constexpr int kTileRecs = 32;
 constexpr int kTileUint4 = kPlaneGroups * 64;  // 6400 uint4 = 102400 B per tile
-#ifndef IRIS_MFMA_TILES
-#define IRIS_MFMA_TILES 4
-#endif
-#ifndef IRIS_MFMA_WGS
-#define IRIS_MFMA_WGS 2
-#endif
-constexpr int kMfmaTiles = IRIS_MFMA_TILES;    // tiles per wave (4: 128 templates)
-constexpr int kMfmaWgs = IRIS_MFMA_WGS;        // workgroups per CU the register budget allows
-#ifndef IRIS_SPLIT_STAGES
-#define IRIS_SPLIT_STAGES 6
-#endif
-constexpr int kSplitStages = IRIS_SPLIT_STAGES;  // load ring depth of the K-split (small-range) form
-#ifndef IRIS_SPLIT_T
-#define IRIS_SPLIT_T 2
-#endif
+constexpr int kMfmaTiles = 4;    // tiles per wave (128 templates)
+constexpr int kMfmaWgs = 2;      // workgroups per CU the register budget allows
+constexpr int kSplitStages = 6;  // load ring depth of the K-split (small-range) form
 // tiles per workgroup of the K-split form: every query-fragment load (2 per chunk pair and
 // wave, from L2) feeds this many tiles -- at 1 the query stream is twice the template stream
-constexpr int kSplitT = IRIS_SPLIT_T;
+constexpr int kSplitT = 2;
 
 __device__ __forceinline__ v16f mfma_fp4(const v8i &a, const v8i &b, const v16f &c) {
     // cbsz = blgp = 4: both operands e2m1; scales 127 = 2^0 (e8m0)
@@ -75,26 +63,8 @@ __device__ __forceinline__ void chunk_step(uint32_t x0, uint32_t x1, const QFrag
                     (int)(x1 & 0x11111111u), 0, 0, 0, 0};
     const v8i be = {(int)(x0 & 0xAAAAAAAAu), (int)((x0 << 1) & 0xAAAAAAAAu), (int)(x1 & 0xAAAAAAAAu),
                     (int)((x1 << 1) & 0xAAAAAAAAu), 0, 0, 0, 0};
-#ifndef IRIS_MFMA_DIAG
-#define IRIS_MFMA_DIAG 0
-#endif
-    // diagnostic builds only (tools/, results wrong by design): 1 = no den MFMA, 2 = no
-    // MFMAs (operands kept live by an empty asm), 3 = no operand expansion (raw dwords);
-    // 4 = the shipped arithmetic, but a search's dist_out receives each workgroup's timeline
-    // (start / end of the constant-rate clock, XCD id: 3 u64 per workgroup) instead of distances
-    if constexpr (IRIS_MFMA_DIAG == 0 || IRIS_MFMA_DIAG == 4) {
-        den = mfma_fp4(q.am, bm, den);
-        s = mfma_fp4(q.ae, be, s);
-    } else if constexpr (IRIS_MFMA_DIAG == 1) {
-        asm volatile("" ::"v"(bm));
-        s = mfma_fp4(q.ae, be, s);
-    } else if constexpr (IRIS_MFMA_DIAG == 2) {
-        asm volatile("" ::"v"(bm), "v"(be), "v"(q.am), "v"(q.ae));
-    } else {
-        const v8i raw = {(int)x0, (int)x1, (int)x0, (int)x1, 0, 0, 0, 0};
-        den = mfma_fp4(q.am, raw, den);
-        s = mfma_fp4(q.ae, raw, s);
-    }
+    den = mfma_fp4(q.am, bm, den);
+    s = mfma_fp4(q.ae, be, s);
 }
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -111,16 +81,14 @@ enum { MF_COUNTS = 0, MF_SEARCH = 1 };
 // a few hundred tiles still puts several waves on every SIMD.
 // FUSED (search, small grids): the last workgroup to finish folds every workgroup's
 // partial and writes the winner to fin.dst itself (iris_device.hpp, fold_partials_last).
-// W: waves per workgroup (IRIS_SEARCH_WG_WAVES = 8 for large searches: one 8-wave workgroup per CU,
-// all of whose waves start at the same K step and share the query fragments in L1)
-template <int MODE, int T = kMfmaTiles, int KS = 1, bool FUSED = false, int W = kWaveSlots>
-__global__ void __launch_bounds__(64 * W, kMfmaWgs * kWaveSlots / W)
+template <int MODE, int T = kMfmaTiles, int KS = 1, bool FUSED = false>
+__global__ void __launch_bounds__(64 * kWaveSlots, kMfmaWgs)
     template_mfma_kernel(const uint4 *__restrict__ db, const uint4 *__restrict__ qfrag, uint64_t tile0,
                          uint64_t ntiles, uint64_t first, uint64_t end, uint16_t *__restrict__ num_out,
                          uint16_t *__restrict__ den_out, double *__restrict__ dist_out,
                          Partial *__restrict__ partials, FusedFinish fin) {
+    constexpr int W = kWaveSlots;
     static_assert(KS == 1 || (W % KS == 0 && kPlaneGroups % KS == 0), "K-split geometry");
-    const uint64_t diag_t0 = IRIS_MFMA_DIAG == 4 ? __builtin_amdgcn_s_memrealtime() : 0;
     const int lane = threadIdx.x & 63;
     const int wslot = threadIdx.x >> 6;
     const int slice = wslot % KS;
@@ -154,14 +122,8 @@ __global__ void __launch_bounds__(64 * W, kMfmaWgs * kWaveSlots / W)
             uint4 d[T];
             uint4 q0, q1;
         };
-#ifndef IRIS_SEARCH_KROT
-#define IRIS_SEARCH_KROT 0  // 1: each wave walks K from its own starting step (order of exact integer sums: free)
-#endif
-        const int krot = (IRIS_SEARCH_KROT && KS == 1) ? (int)((wave * 37) % kG) : 0;
         auto load = [&](Stage &st, int g) {
-            g = g < kG ? g : kG - 1;
-            if (IRIS_SEARCH_KROT && KS == 1) g = g + krot >= kG ? g + krot - kG : g + krot;
-            g += g0;
+            g = (g < kG ? g : kG - 1) + g0;
 #pragma unroll
             for (int t = 0; t < T; ++t) st.d[t] = stream_load(dp[t] + g * 64);
             st.q0 = qp[(2 * g) * 64];
@@ -263,7 +225,7 @@ __global__ void __launch_bounds__(64 * W, kMfmaWgs * kWaveSlots / W)
                 dd = (uint32_t)den[t][r];
                 nn = (uint32_t)(((int)dd - (int)s[t][r]) >> 1);  // num = (den - S) / 2
             }, bn, bd, br);
-            if (IRIS_MFMA_DIAG != 4 && valid && dist_out && h == 0) dist_out[o] = bd ? (double)bn / (double)bd : __builtin_inf();
+            if (valid && dist_out && h == 0) dist_out[o] = bd ? (double)bn / (double)bd : __builtin_inf();
             Partial c;
             c.num = bn;
             c.den = valid ? bd : 0;
@@ -288,356 +250,10 @@ __global__ void __launch_bounds__(64 * W, kMfmaWgs * kWaveSlots / W)
             for (int w = 1; w < W; ++w)
                 if (partial_better_dev(sh[w], b)) b = sh[w];
             if constexpr (!FUSED) partials[blockIdx.x] = b;
-            if (IRIS_MFMA_DIAG == 4 && dist_out) {
-                uint32_t xcc;
-                asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-                uint64_t *tl = (uint64_t *)dist_out + 3 * (uint64_t)blockIdx.x;
-                tl[0] = diag_t0;
-                tl[1] = __builtin_amdgcn_s_memrealtime();
-                tl[2] = xcc;
-            }
         }
         if constexpr (FUSED) fold_partials_last(partials, b, fin);
     }
 }
-
-// ------------------------------------------------------------------ persistent search (large ranges)
-//
-// A grid that launches every workgroup the chip holds at once (kMfmaWgs per CU) and keeps it: each
-// wave takes its next unit of T tiles from a work counter (one agent-scope atomic add per unit, by
-// lane 0), fetched one unit AHEAD, so the 3-stage load pipeline streams on across the unit boundary
-// and the unit's epilogue overlaps the next unit's loads.  Why: with one short-lived workgroup per
-// 16 tiles (template_mfma_kernel), the per-workgroup timeline of a 10M search
-// (tools/search_timeline.py, -DIRIS_MFMA_DIAG=4) held only ~88 % of the 512 workgroup slots busy on
-// average -- workgroups are dealt to the XCDs in order, so a slot that frees on one XCD waits while
-// the next workgroup in line is bound for a full one -- and the XCDs finished 100-200 us apart.
-// Dynamic units fill every slot until the counter runs out, on every XCD alike.  Each wave folds its
-// units' winners into a running best (exact fraction, then lowest index: a total order, so the
-// order the units arrive in does not matter); one partial per workgroup.  *work must be 0 at launch
-// (the launcher clears it on the stream).
-#ifndef IRIS_SEARCH_DYN
-#define IRIS_SEARCH_DYN 0  // 1: static units, 2: units from a work counter; 0: one workgroup per 16 tiles
-#endif
-#if IRIS_SEARCH_DYN  // the persistent forms: build variants only (measured slower, see above)
-template <int T = kMfmaTiles>
-__global__ void __launch_bounds__(256, kMfmaWgs)
-    template_search_dyn_kernel(const uint4 *__restrict__ db, const uint4 *__restrict__ qfrag, uint64_t tile0,
-                               uint64_t ntiles, uint64_t first, uint64_t end, double *__restrict__ dist_out,
-                               Partial *__restrict__ partials, uint32_t *__restrict__ work) {
-    constexpr int kG = kPlaneGroups;  // 100 steps of 2 chunks per unit
-    const int lane = threadIdx.x & 63;
-    const int wslot = threadIdx.x >> 6;
-#ifndef IRIS_SEARCH_UNIT
-#define IRIS_SEARCH_UNIT 1  // sub-units of T tiles per fetched unit
-#endif
-    constexpr uint32_t H = IRIS_SEARCH_UNIT;
-    const uint32_t units = (uint32_t)((ntiles + T - 1) / T);  // sub-units of T tiles
-#if IRIS_SEARCH_DYN >= 2
-    auto fetch = [&]() -> uint32_t {
-        uint32_t u = 0;
-        if (lane == 0) u = __hip_atomic_fetch_add(work, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return __builtin_amdgcn_readfirstlane(u);
-    };
-#else  // static: wave w takes units w, w + nwaves, ... (no counter)
-    const uint32_t nwaves = gridDim.x * kWaveSlots;
-    uint32_t ticket = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaveSlots + wslot);
-    auto fetch = [&]() -> uint32_t {
-        const uint32_t u = ticket;
-        ticket += nwaves;
-        return u;
-    };
-#endif
-#if IRIS_SEARCH_DYN == 3
-    // guided: the counter counts sub-units; a wave claims a block sized by what it last saw remain
-    // (large blocks early: few counter round trips, each of which drains the wave's load queue;
-    // single sub-units at the end: a short, balanced tail)
-    const uint32_t nw = gridDim.x * kWaveSlots;
-    uint32_t seen = 0, cur_end = 0, nxt_end = 0;
-    auto claim = [&]() -> uint32_t {
-        const uint32_t rem = units > seen ? units - seen : 0;
-        const uint32_t sz = min(max(rem / (2 * nw), 1u), (uint32_t)IRIS_SEARCH_UNIT);
-        uint32_t b = 0;
-        if (lane == 0) b = __hip_atomic_fetch_add(work, sz, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        b = __builtin_amdgcn_readfirstlane(b);
-        seen = b + sz;
-        nxt_end = min(b + sz, units);
-        return b < units ? b : units;
-    };
-    auto after = [&](uint32_t c) -> uint32_t {
-        if (c + 1 < cur_end) {
-            nxt_end = cur_end;
-            return c + 1;
-        }
-        return claim();
-    };
-    uint32_t cur = claim();
-    cur_end = nxt_end;
-    uint32_t nxt = cur < units ? after(cur) : units;
-#else
-    // cur / nxt: sub-units (T tiles); a fetch hands out H consecutive ones
-    auto fetch_sub = [&]() -> uint32_t {
-        const uint32_t u = fetch();
-        return u < (units + H - 1) / H ? u * H : units;
-    };
-    auto after = [&](uint32_t c) -> uint32_t {  // the sub-unit a wave takes after c
-        return (c % H != H - 1 && c + 1 < units) ? c + 1 : fetch_sub();
-    };
-    uint32_t cur = fetch_sub();
-    uint32_t nxt = cur < units ? after(cur) : units;
-#endif
-    Partial best = partial_none();
-    if (cur < units) {
-        v16f den[T], sm[T];
-        auto zero = [&] {
-#pragma unroll
-            for (int t = 0; t < T; ++t)
-#pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    den[t][i] = 0.f;
-                    sm[t][i] = 0.f;
-                }
-        };
-        zero();
-        const uint4 *qp = qfrag + lane;
-        struct Stage {
-            uint4 d[T];
-            uint4 q0, q1;
-        };
-        // step s of this wave's walk: unit ucur covers steps [s_unit, s_unit + kG); a load at most two
-        // steps ahead falls in ucur or in the prefetched unit nxt (past the last unit: ucur's last
-        // step again, never consumed)
-        uint32_t s_unit = 0;
-        const uint32_t krot = IRIS_SEARCH_KROT ? (uint32_t)((blockIdx.x * kWaveSlots + wslot) * 37u % kG) : 0u;
-        auto load = [&](Stage &st, uint32_t step) {
-            uint32_t u = cur, g = step - s_unit;
-            if (g >= (uint32_t)kG) {
-                if (nxt < units) {
-                    u = nxt;
-                    g -= kG;
-                } else {
-                    g = kG - 1;
-                }
-            }
-            if (IRIS_SEARCH_KROT) g = g + krot >= (uint32_t)kG ? g + krot - kG : g + krot;
-#pragma unroll
-            for (int t = 0; t < T; ++t) {
-                const uint64_t rel = (uint64_t)u * T + t < ntiles ? (uint64_t)u * T + t : ntiles - 1;
-                st.d[t] = stream_load(db + (tile0 + rel) * (uint64_t)kTileUint4 + g * 64 + lane);
-            }
-            st.q0 = qp[(2 * g) * 64];
-            st.q1 = qp[(2 * g + 1) * 64];
-            __builtin_amdgcn_sched_barrier(0);
-        };
-        // after the wave's last unit, cur >= units: the (at most two) steps still computed add into
-        // zeroed accumulators nobody reads
-        auto compute = [&](const Stage &st, uint32_t step) {
-            const QFrag f0 = qfrag_of(st.q0);
-#pragma unroll
-            for (int t = 0; t < T; ++t) chunk_step(st.d[t].x, st.d[t].y, f0, den[t], sm[t]);
-            const QFrag f1 = qfrag_of(st.q1);
-#pragma unroll
-            for (int t = 0; t < T; ++t) chunk_step(st.d[t].z, st.d[t].w, f1, den[t], sm[t]);
-            if (step - s_unit != (uint32_t)kG - 1) return;
-            // unit done: its tiles' winners into the running best, then the next unit
-            const int h = lane >> 5;
-#pragma unroll
-            for (int t = 0; t < T; ++t) {
-                const uint64_t tile = (uint64_t)cur * T + t;
-                const uint64_t tg = (tile0 + tile) * kTileRecs + (lane & 31);
-                const bool valid = tile < ntiles && tg >= first && tg < end;
-                uint32_t bn, bd;
-                int br;
-                best_rotation(lane, [&](int r, uint32_t &nn, uint32_t &dd) {
-                    dd = (uint32_t)den[t][r];
-                    nn = (uint32_t)(((int)dd - (int)sm[t][r]) >> 1);  // num = (den - S) / 2
-                }, bn, bd, br);
-                if (valid && dist_out && h == 0) dist_out[tg - first] = bd ? (double)bn / (double)bd : __builtin_inf();
-                Partial c;
-                c.num = bn;
-                c.den = valid ? bd : 0;
-                c.rot = br;
-                c.pad = 0;
-                c.idx = tg - first;
-                if (partial_better_dev(c, best)) best = c;
-            }
-            zero();
-            s_unit += kG;
-            cur = nxt;
-#if IRIS_SEARCH_DYN == 3
-            cur_end = nxt_end;
-#endif
-            if (cur < units) nxt = after(cur);
-        };
-        Stage sa, sb, sc;
-        load(sa, 0);
-        load(sb, 1);
-#pragma unroll 1
-        for (uint32_t step = 0;; step += 3) {
-            load(sc, step + 2);
-            compute(sa, step);
-            load(sa, step + 3);
-            compute(sb, step + 1);
-            load(sb, step + 4);
-            compute(sc, step + 2);
-            if (cur >= units) break;  // set by compute at the wave's last unit end
-        }
-    }
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        const Partial o = partial_shfl_xor(best, off);
-        if (partial_better_dev(o, best)) best = o;
-    }
-    __shared__ Partial sh[kWaveSlots];
-    if (lane == 0) sh[wslot] = best;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        Partial b = sh[0];
-#pragma unroll
-        for (int w = 1; w < kWaveSlots; ++w)
-            if (partial_better_dev(sh[w], b)) b = sh[w];
-        partials[blockIdx.x] = b;
-    }
-}
-
-// IRIS_SEARCH_DYN == 4: persistent, WORKGROUP units of kWaveSlots x T tiles (wave w takes tiles
-// [u kWaveSlots T + w T, +T)) from the work counter, the 4 waves kept in step by one s_barrier per
-// unit (their query-fragment reads, at the same K step, share the CU's L1: waves that drift apart
-// -- the per-wave units above -- or start K at different steps measured 2-9 % slower,
-// profiles/r04_search_persistent.txt).  Lane 0 of wave 0 fetches unit i + 2 at the start of unit i
-// into a 3-slot LDS ring, so every wave knows the next unit two steps before it needs it.
-template <int T = kMfmaTiles>
-__global__ void __launch_bounds__(256, kMfmaWgs)
-    template_search_wg_kernel(const uint4 *__restrict__ db, const uint4 *__restrict__ qfrag, uint64_t tile0,
-                              uint64_t ntiles, uint64_t first, uint64_t end, double *__restrict__ dist_out,
-                              Partial *__restrict__ partials, uint32_t *__restrict__ work) {
-    constexpr int kG = kPlaneGroups;
-    const int lane = threadIdx.x & 63;
-    const int wslot = threadIdx.x >> 6;
-    const uint32_t units = (uint32_t)((ntiles + (uint64_t)T * kWaveSlots - 1) / ((uint64_t)T * kWaveSlots));
-    __shared__ uint32_t ring[3];
-    auto barrier = [] {
-        asm volatile("" ::: "memory");
-        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): LDS writes landed; the stream's loads stay in flight
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-    };
-    if (threadIdx.x == 0) {
-        ring[0] = __hip_atomic_fetch_add(work, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ring[1] = __hip_atomic_fetch_add(work, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    barrier();
-    uint32_t cur = ring[0], nxt = ring[1], ord = 0;  // ord: this workgroup's unit ordinal
-    Partial best = partial_none();
-    if (cur < units) {
-        v16f den[T], sm[T];
-        auto zero = [&] {
-#pragma unroll
-            for (int t = 0; t < T; ++t)
-#pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    den[t][i] = 0.f;
-                    sm[t][i] = 0.f;
-                }
-        };
-        zero();
-        const uint4 *qp = qfrag + lane;
-        struct Stage {
-            uint4 d[T];
-            uint4 q0, q1;
-        };
-        uint32_t s_unit = 0;
-        auto tile_of = [&](uint32_t u, int t) -> uint64_t {
-            const uint64_t tile = ((uint64_t)u * kWaveSlots + wslot) * T + t;
-            return tile < ntiles ? tile : ntiles - 1;
-        };
-        auto load = [&](Stage &st, uint32_t step) {
-            uint32_t u = cur, g = step - s_unit;
-            if (g >= (uint32_t)kG) {
-                if (nxt < units) {
-                    u = nxt;
-                    g -= kG;
-                } else {
-                    g = kG - 1;
-                }
-            }
-#pragma unroll
-            for (int t = 0; t < T; ++t) st.d[t] = stream_load(db + (tile0 + tile_of(u, t)) * (uint64_t)kTileUint4 + g * 64 + lane);
-            st.q0 = qp[(2 * g) * 64];
-            st.q1 = qp[(2 * g + 1) * 64];
-            __builtin_amdgcn_sched_barrier(0);
-        };
-        auto compute = [&](const Stage &st, uint32_t step) {
-            const QFrag f0 = qfrag_of(st.q0);
-#pragma unroll
-            for (int t = 0; t < T; ++t) chunk_step(st.d[t].x, st.d[t].y, f0, den[t], sm[t]);
-            const QFrag f1 = qfrag_of(st.q1);
-#pragma unroll
-            for (int t = 0; t < T; ++t) chunk_step(st.d[t].z, st.d[t].w, f1, den[t], sm[t]);
-            const uint32_t g = step - s_unit;
-            if (g == 0 && threadIdx.x == 0)  // the unit after next, into the ring
-                ring[(ord + 2) % 3] = nxt < units ? __hip_atomic_fetch_add(work, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                                  : units;
-            if (g != (uint32_t)kG - 1) return;
-            const int h = lane >> 5;
-#pragma unroll
-            for (int t = 0; t < T; ++t) {
-                const uint64_t tile = ((uint64_t)cur * kWaveSlots + wslot) * T + t;
-                const uint64_t tg = (tile0 + tile) * kTileRecs + (lane & 31);
-                const bool valid = tile < ntiles && tg >= first && tg < end;
-                uint32_t bn, bd;
-                int br;
-                best_rotation(lane, [&](int r, uint32_t &nn, uint32_t &dd) {
-                    dd = (uint32_t)den[t][r];
-                    nn = (uint32_t)(((int)dd - (int)sm[t][r]) >> 1);  // num = (den - S) / 2
-                }, bn, bd, br);
-                if (valid && dist_out && h == 0) dist_out[tg - first] = bd ? (double)bn / (double)bd : __builtin_inf();
-                Partial c;
-                c.num = bn;
-                c.den = valid ? bd : 0;
-                c.rot = br;
-                c.pad = 0;
-                c.idx = tg - first;
-                if (partial_better_dev(c, best)) best = c;
-            }
-            zero();
-            barrier();  // the workgroup's waves leave the unit together; ring[(ord + 2) % 3] is written
-            s_unit += kG;
-            cur = nxt;
-            ++ord;
-            nxt = cur < units ? ring[(ord + 1) % 3] : units;
-        };
-        Stage sa, sb, sc;
-        load(sa, 0);
-        load(sb, 1);
-#pragma unroll 1
-        for (uint32_t step = 0;; step += 3) {
-            load(sc, step + 2);
-            compute(sa, step);
-            load(sa, step + 3);
-            compute(sb, step + 1);
-            load(sb, step + 4);
-            compute(sc, step + 2);
-            if (cur >= units) break;
-        }
-    }
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        const Partial o = partial_shfl_xor(best, off);
-        if (partial_better_dev(o, best)) best = o;
-    }
-    __shared__ Partial sh[kWaveSlots];
-    if (lane == 0) sh[wslot] = best;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        Partial b = sh[0];
-#pragma unroll
-        for (int w = 1; w < kWaveSlots; ++w)
-            if (partial_better_dev(sh[w], b)) b = sh[w];
-        partials[blockIdx.x] = b;
-    }
-}
-
-#endif  // IRIS_SEARCH_DYN
 
 // ------------------------------------------------------------------ a few queries per pass
 
@@ -863,16 +479,11 @@ int launch_generate_tiles(void *stream, void *db, uint64_t t_first, uint64_t n, 
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-#ifndef IRIS_SEARCH_WG_WAVES
-#define IRIS_SEARCH_WG_WAVES 4
-#endif
 struct TileRange {
     uint64_t tile0, ntiles, grid;
-    int wg_waves = kWaveSlots;  // waves per workgroup of the plain search grid
-    bool fusable = false;       // small enough for the in-kernel reduce (4-wave workgroups)
+    bool fusable = false;  // small enough for the in-kernel reduce
     int tiles_per_wave;
     int ksplit;  // 4: a tile's 4 waves split K (ranges of at most kSplitTiles tiles)
-    bool dyn;    // persistent search grid (template_search_dyn_kernel): grid = resident workgroups
 };
 
 // Below this many tiles, 4 tiles per wave would leave CUs idle (fewer than 2
@@ -903,30 +514,19 @@ static TileRange tile_range(const Hooks &h, LaunchRange r) {
     }
     const uint64_t waves = (t.ntiles + t.tiles_per_wave - 1) / t.tiles_per_wave;
     t.grid = (waves + kWaveSlots - 1) / kWaveSlots;
-    t.dyn = false;
     return t;
 }
 
-// the search's form of tile_range: ranges of 4 tiles per wave that would take more workgroups than
-// the chip holds at once run the persistent kernel on exactly that many
+// the search's form of tile_range: one workgroup per 16 tiles (a persistent grid measured
+// slower)
 static TileRange search_range(const Hooks &h, LaunchRange r) {
     TileRange t = tile_range(h, r);
     t.fusable = t.grid <= (uint64_t)kFusedReduceMax;
-    if (IRIS_SEARCH_WG_WAVES != kWaveSlots && t.ksplit == 1 && t.tiles_per_wave == kMfmaTiles && !t.fusable) {  // large ranges only: the fused small-range forms keep 4 waves
-        t.wg_waves = IRIS_SEARCH_WG_WAVES;
-        t.grid = (t.ntiles + (uint64_t)kMfmaTiles * t.wg_waves - 1) / ((uint64_t)kMfmaTiles * t.wg_waves);
-    }
-    t.dyn = IRIS_SEARCH_DYN && t.ksplit == 1 && t.tiles_per_wave == kMfmaTiles &&
-            t.grid > (uint64_t)resident_blocks(kMfmaWgs);
-    if (t.dyn) t.grid = resident_blocks(kMfmaWgs);
     return t;
 }
 
-// partial records a search writes; the persistent form keeps its work counter one record further
-uint32_t mfma_search_partials(const Hooks &h, LaunchRange r) {
-    const TileRange t = search_range(h, r);
-    return (uint32_t)t.grid + (t.dyn ? 1u : 0u);
-}
+// partial records a search writes
+uint32_t mfma_search_partials(const Hooks &h, LaunchRange r) { return (uint32_t)search_range(h, r).grid; }
 
 uint32_t multi_search_partials(LaunchRange r, int nq) {
     const uint64_t tile0 = r.first / kTileRecs, tile1 = (r.first + r.n + kTileRecs - 1) / kTileRecs;
@@ -964,30 +564,14 @@ int launch_template_mfma_search(const Hooks &h, void *stream, const void *db, co
     const TileRange t = search_range(h, r);
     *n_partials = (uint32_t)t.grid;
     if (r.n == 0) return 0;
-    const bool fused = fin && t.fusable && !t.dyn;
+    const bool fused = fin && t.fusable;
     if (fin && !fused) return -1;  // the caller asks fused_search_ok() first
-#if IRIS_SEARCH_DYN
-    if (t.dyn) {
-        uint32_t *work = (uint32_t *)(partials + t.grid);
-        if (hipMemsetAsync(work, 0, sizeof(uint32_t), (hipStream_t)stream) != hipSuccess) return -1;
-        if (IRIS_SEARCH_DYN == 4)
-            hipLaunchKernelGGL(template_search_wg_kernel<kMfmaTiles>, dim3((uint32_t)t.grid), dim3(256), 0,
-                               (hipStream_t)stream, (const uint4 *)db, (const uint4 *)qfrag, t.tile0, t.ntiles, r.first,
-                               r.first + r.n, dist_out, partials, work);
-        else
-            hipLaunchKernelGGL(template_search_dyn_kernel<kMfmaTiles>, dim3((uint32_t)t.grid), dim3(256), 0,
-                               (hipStream_t)stream, (const uint4 *)db, (const uint4 *)qfrag, t.tile0, t.ntiles, r.first,
-                               r.first + r.n, dist_out, partials, work);
-        return hipGetLastError() == hipSuccess ? 0 : -1;
-    }
-#endif
     auto kern = fused ? (t.ksplit > 1 ? template_mfma_kernel<MF_SEARCH, kSplitT, 4, true>
                          : t.tiles_per_wave == 1 ? template_mfma_kernel<MF_SEARCH, 1, 1, true>
                                                  : template_mfma_kernel<MF_SEARCH, kMfmaTiles, 1, true>)
                       : (t.ksplit > 1 ? template_mfma_kernel<MF_SEARCH, kSplitT, 4>
                          : t.tiles_per_wave == 1 ? template_mfma_kernel<MF_SEARCH, 1> : template_mfma_kernel<MF_SEARCH>);
-    if (t.wg_waves != kWaveSlots) kern = template_mfma_kernel<MF_SEARCH, kMfmaTiles, 1, false, IRIS_SEARCH_WG_WAVES>;
-    hipLaunchKernelGGL(kern, dim3((uint32_t)t.grid), dim3(64 * t.wg_waves), 0, (hipStream_t)stream,
+    hipLaunchKernelGGL(kern, dim3((uint32_t)t.grid), dim3(64 * kWaveSlots), 0, (hipStream_t)stream,
                        (const uint4 *)db, (const uint4 *)qfrag, t.tile0, t.ntiles, r.first, r.first + r.n,
                        (uint16_t *)nullptr, (uint16_t *)nullptr, dist_out, partials, fin ? *fin : FusedFinish{});
     return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -997,8 +581,7 @@ int launch_template_mfma_search(const Hooks &h, void *stream, const void *db, co
 bool fused_search_ok(const Hooks &h, LaunchRange r) {
     if (!h.fused_reduce) return false;
     if (r.n == 0) return false;
-    const TileRange t = search_range(h, r);
-    return !t.dyn && t.fusable;
+    return search_range(h, r).fusable;
 }
 
 }  // namespace iris

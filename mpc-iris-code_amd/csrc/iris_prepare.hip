@@ -28,10 +28,6 @@
 
 namespace iris {
 
-#ifndef IRIS_PREP_DIAG
-#define IRIS_PREP_DIAG 0
-#endif
-
 struct ChachaKey {
     uint32_t k[8];
 };
@@ -60,7 +56,7 @@ __device__ __forceinline__ void chacha_block(const ChachaKey &key, uint64_t nonc
 #pragma unroll
     for (int i = 0; i < 16; ++i) x[i] = in[i];
 #pragma unroll 2
-    for (int r = 0; r < (IRIS_PREP_DIAG == 2 ? 0 : DR); ++r) {
+    for (int r = 0; r < DR; ++r) {
         CC_QR(x[0], x[4], x[8], x[12]);
         CC_QR(x[1], x[5], x[9], x[13]);
         CC_QR(x[2], x[6], x[10], x[14]);
@@ -136,23 +132,9 @@ struct ShareDsts {
 // parties, interleaved runs on one box).  Loading the next block's template pair ahead of
 // the stores (vmcnt counts stores too on gfx9) measured no change; write-through policies
 // (sc1, sc0 sc1, nt sc1) were 0.5-2 % slower than nt.
-#ifndef IRIS_PREP_NT
-#define IRIS_PREP_NT 1
-#endif
-// Diagnostic builds (tools/build_variant.sh, results wrong by design): IRIS_PREP_DIAG = 1 drops
-// the share stores (the values stay live), 2 replaces the ChaCha rounds by the block input
-// (the keystream's VALU gone, every store kept) -- the two halves of the kernel's time.
 __device__ __forceinline__ void st_share(uint4 *p, const uint4 v) {
-    if (IRIS_PREP_DIAG == 1) {
-        asm volatile("" ::"v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
-        return;
-    }
-    if (IRIS_PREP_NT) {
-        const u32x4_nt w = {v.x, v.y, v.z, v.w};
-        __builtin_nontemporal_store(w, (u32x4_nt *)p);
-    } else {
-        *p = v;
-    }
+    const u32x4_nt w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, (u32x4_nt *)p);
 }
 
 __device__ __forceinline__ void store_share_block(uint4 *db, uint64_t t, int b, const uint32_t w[16]) {

@@ -27,10 +27,6 @@ struct ResolverArgs {
 
 typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
 
-#ifndef IRIS_RESOLVER_NT
-#define IRIS_RESOLVER_NT 1
-#endif
-
 // One wave's 64 rows of a [n][31] u16 array as 16-B words: 64 rows = 3968 B =
 // 248 words, 16-B aligned when the array is (row0 is a multiple of 64).  Word
 // i of the wave's block -> lane i % 64, slot i / 64 (4 slots).  Words past the
@@ -41,8 +37,7 @@ __device__ __forceinline__ u16x8 load_word(const uint16_t *__restrict__ src, uin
     if (aligned && e + 8 <= ne) {
         // read once: nontemporal loads (the plain-load stream tops out lower, measured in
         // profiles/r01_ubench_read_stream_warm.txt: tools/ubench_stream.hip)
-        if (IRIS_RESOLVER_NT) return __builtin_nontemporal_load((const u16x8 *)(src + e0 + e));
-        return *(const u16x8 *)(src + e0 + e);
+        return __builtin_nontemporal_load((const u16x8 *)(src + e0 + e));
     }
     u16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll

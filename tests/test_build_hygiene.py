@@ -1,9 +1,10 @@
-"""CPU: the shipped library never carries a diagnostic compile knob.  Diagnostic knobs
-(IRIS_*_DIAG, IRIS_STORE_DIAG) build kernels that drop work on purpose;
-the Makefile refuses them for libiris_hip.so (variants go through tools/build_variant.sh
-under their own names), the sources refuse them under IRIS_SHIPPED_BUILD, and
-iris_version() names every -DIRIS_* knob a build was given."""
+"""CPU: the shipped library is the one configuration the tests and the bench measure.  Kernel
+shapes and host paths are compile-time constants, not -D knobs (round 5 removed the A/B and
+diagnostic knobs; git history keeps the variant builds DESIGN.md's appendix cites), so
+`#ifndef IRIS_` appears in the sources only for what the Makefile itself defines, and
+iris_version() names any -DIRIS_* a build was given."""
 import pathlib
+import re
 import subprocess
 
 import iris_hip as ih
@@ -16,27 +17,19 @@ def _make(*args):
     return subprocess.run(["make", "-C", str(PKG), *args], capture_output=True, text=True, timeout=120)
 
 
-def test_shipped_target_refuses_diag_knobs(tmp_path):
-    for knob in ("-DIRIS_MFMA_DIAG=1", "-DIRIS_STORE_DIAG", "-DIRIS_BATCH2_DIAG=5", "-DIRIS_PREP_DIAG=2"):
-        r = _make("-n", f"BUILD={tmp_path}/b", f"HIPFLAGS=-O3 --offload-arch=gfx950 {knob}")
-        assert r.returncode != 0 and "refusing to build the shipped libiris_hip.so" in r.stderr, (knob, r.stderr)
+def test_no_compile_time_variant_knobs():
+    knobs = {}
+    for f in sorted((PKG / "csrc").iterdir()):
+        if f.suffix in (".hip", ".hpp", ".cpp"):
+            for m in re.finditer(r"^#ifndef (IRIS_\w+)", f.read_text(), re.M):
+                knobs.setdefault(m.group(1), []).append(f.name)
+    assert set(knobs) <= {"IRIS_BUILD_KNOBS"}, knobs
 
 
-def test_variant_and_zero_knobs_are_allowed(tmp_path):
-    # a variant library may carry a diagnostic knob; a knob set to 0 is the default
-    r = _make("-n", f"BUILD={tmp_path}/v", "LIB=libiris_variant_test.so", "HIPFLAGS=-O3 -DIRIS_MFMA_DIAG=1")
+def test_build_defines_reach_the_version_string(tmp_path):
+    r = _make("-n", f"BUILD={tmp_path}/v", "LIB=libiris_variant_test.so", "HIPFLAGS=-O3 -DIRIS_EXAMPLE=1")
     assert r.returncode == 0, r.stderr
-    assert "IRIS_SHIPPED_BUILD" not in r.stdout and "-DIRIS_BUILD_KNOBS='\"-DIRIS_MFMA_DIAG=1\"'" in r.stdout
-    r = _make("-n", f"BUILD={tmp_path}/z", "HIPFLAGS=-O3 -DIRIS_MFMA_DIAG=0")
-    assert r.returncode == 0 and "-DIRIS_SHIPPED_BUILD=1" in r.stdout, r.stderr
-
-
-def test_source_guard_refuses_diag_knob_in_shipped_build(tmp_path):
-    """Even past the Makefile, a shipped-build compile with a diagnostic knob stops at #error."""
-    r = subprocess.run(["/opt/rocm/bin/hipcc", "-std=c++17", "-fsyntax-only", "-x", "c++", "--offload-arch=gfx950",
-                        "-DIRIS_SHIPPED_BUILD=1", "-DIRIS_BATCH_DIAG=3", "-I", str(PKG / "csrc"),
-                        str(PKG / "csrc" / "iris_internal.hpp")], capture_output=True, text=True, timeout=120)
-    assert r.returncode != 0 and "diagnostic knob in the shipped" in r.stderr, r.stderr[-2000:]
+    assert "-DIRIS_BUILD_KNOBS='\"-DIRIS_EXAMPLE=1\"'" in r.stdout, r.stdout[-2000:]
 
 
 def test_shipped_library_reports_no_knobs():

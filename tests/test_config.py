@@ -7,8 +7,9 @@ import pytest
 
 import iris_hip as ih
 
-TEST_HOOKS = ["IRIS_TILES_PER_WAVE", "IRIS_FUSED_REDUCE", "IRIS_BATCH_KERNEL", "IRIS_BATCH_XQG", "IRIS_SCHEDULE",
-              "IRIS_LOAD_PREAD", "IRIS_GROUP_DELAY_US", "IRIS_GROUP_STALL", "IRIS_GROUP_UNORDERED", "IRIS_UPLOAD"]
+TEST_HOOKS = ["IRIS_TILES_PER_WAVE", "IRIS_FUSED_REDUCE", "IRIS_BATCH_KERNEL", "IRIS_SCHEDULE",
+              "IRIS_LOAD_PREAD", "IRIS_GROUP_DELAY_US", "IRIS_GROUP_STALL", "IRIS_GROUP_UNORDERED", "IRIS_UPLOAD",
+              "IRIS_LOAD_WINDOWS"]
 
 
 @pytest.fixture(autouse=True)
@@ -45,6 +46,7 @@ def test_test_hooks_with_opt_in(monkeypatch):
     assert (c["test_hooks"], c["tiles_per_wave"], c["batch_kernel"], c["schedule"], c["group_delay_us"]) == \
         ("1", "1", "2", "spin", "1500")
     assert (c["fused_reduce"], c["group_stall"], c["load_pread"], c["upload"]) == ("1", "0", "0", "pinned")
+    assert c["load_windows"] == "0"
 
 
 def test_production_knobs_need_no_opt_in(monkeypatch):

@@ -59,11 +59,11 @@ def check_all(got, queries, recs, base=0):
             assert (g.num, g.den, g.rotation) == (num, den, rot), (qi, g)
 
 
-@pytest.mark.parametrize("kernel", ["2", "3", "4", "1"], ids=["batch_lds_kernel", "batch_lds_2x2", "batch_lds_q2", "batch_kernel"])
+@pytest.mark.parametrize("kernel", ["4", "2"], ids=["batch_lds_q2", "batch_lds_q4"])
 def test_batch_1024_queries_vs_oracle(device, hooked_device, kernel):
     """Q = 1024 (256 query groups) over 4099 templates and a ragged sub-range: every query's
-    distance bits, index, winning fraction and rotation equal the oracle's (every batched
-    kernel: the IRIS_BATCH_KERNEL test hook; 4 is the default)."""
+    distance bits, index, winning fraction and rotation equal the oracle's (both batched
+    kernel shapes: the IRIS_BATCH_KERNEL test hook; 4 is the default, 2 the cross-check)."""
     if kernel != "4":
         device = hooked_device(IRIS_BATCH_KERNEL=kernel)
     n, nq = 4099, 1024
@@ -88,7 +88,7 @@ def test_batch_1024_queries_vs_oracle(device, hooked_device, kernel):
     assert got[600].index == NONE and got[600].distance == np.inf
 
 
-@pytest.mark.parametrize("kernel", ["2", "3", "4", "1"], ids=["batch_lds_kernel", "batch_lds_2x2", "batch_lds_q2", "batch_kernel"])
+@pytest.mark.parametrize("kernel", ["4", "2"], ids=["batch_lds_q2", "batch_lds_q4"])
 @pytest.mark.parametrize("nq", [64, 1024])
 def test_batch_many_groups_200k(device, hooked_device, nq, kernel):
     """Q = 64 and 1024 over 200 003 templates (6252 tiles: many N-groups per workgroup and a
