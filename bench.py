@@ -106,7 +106,13 @@ def parse():
     ap.add_argument("--chunk", type=int, default=None,
                     help="host-shares / host-masks: records per batch_process call (the reference's "
                          "participant / resolver use 20 000, src/main.rs:428,473; default: 20 000 with "
-                         "--attached, else the whole array in one call)")
+                         "--attached or --mmap, else the whole array in one call)")
+    ap.add_argument("--mmap", action="store_true",
+                    help="host-shares / host-masks: the records are a file mapped read-only (np.memmap, as "
+                         "the participant / resolver map theirs, src/main.rs:386-391, 455-460) and the calls "
+                         "walk its slices with no attach call (the library keeps the file resident)")
+    ap.add_argument("--no-auto-resident", action="store_true",
+                    help="open the device with IRIS_AUTO_RESIDENT=0 (slices of file mappings upload per call)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher rehearsal without a GPU: start / join the ranks, check the world size, "
                          "exchange and merge a synthetic per-rank result over gloo, print the line (value null)")
@@ -620,9 +626,22 @@ def run_aux(args, dev):
             host = gen_records(dev, ih.KIND_MASKS, n, SEED)
             eng = ih.MasksEngine(dev, qt[200:])
         hout = np.empty((n, ROT), np.uint16)
-        chunk = args.chunk or (20_000 if args.attached else n)
+        chunk = args.chunk or (20_000 if (args.attached or args.mmap) else n)
         kind = ih.KIND_SHARES if shares_wl else ih.KIND_MASKS
         adb = None
+        mpath = None
+        if args.mmap:  # the record file the participant / resolver maps (page-cached after the write)
+            mpath = pathlib.Path(tempfile.gettempdir()) / f"iris_bench_{os.getpid()}.records"
+            host.tofile(mpath)
+            arr = host
+            host = np.memmap(mpath, dtype=arr.dtype, mode="r", shape=arr.shape)
+            del arr
+            # the first walk makes the file resident (granule uploads): timed apart from the steps
+            t_first = time.perf_counter()
+            for a in range(0, n, chunk):
+                eng.batch_process(hout[a:a + chunk], host[a:a + chunk])
+            extra["first_walk_s"] = time.perf_counter() - t_first
+            extra["resident"] = dict(zip(("count", "bytes"), dev.resident()))
         extra["host_pages_numa"] = {"pages_by_node": pages_nodes(host), "gpu_node": dev.config().get("numa_node")}
         if args.attached:  # the mmap'd file's device copy (iris_db_attach_host), made once
             adb = ih.Database(dev, kind, n)
@@ -641,6 +660,11 @@ def run_aux(args, dev):
                     "src/main.rs:426-431, 511-516): "
                     + ("the host array is attached to its resident copy (iris_db_attach_host): no upload"
                        if args.attached else
+                       ("slices of a read-only file mapping, no attach call: "
+                        + ("IRIS_AUTO_RESIDENT=0, every slice uploaded (PCIe-inclusive)" if args.no_auto_resident
+                           else "served from the library's resident copy of the file (made by an untimed first "
+                                "walk, first_walk_s), re-validated on every call"))
+                       if args.mmap else
                        "H2D of the pageable slice (runtime-staged) + TILES pack per 256-MB chunk, then the "
                        "engine kernel; PCIe-inclusive"))
     elif args.workload == "criterion":
@@ -757,6 +781,9 @@ def run_aux(args, dev):
                 if args.workload == "host-shares" else check_masks_rows(qt[200:], host[sample]))
         ok = bool((hout[sample] == want).all())
         check = {"sampled_outputs_checked": len(sample), "ok": ok}
+        if mpath is not None:
+            del host
+            mpath.unlink()
     elif args.workload == "load":
         sample = [0, n // 3, n - 1]
         ok = m == n and all((tdb.read(i, 1) == src.read(i, 1)).all() for i in sample)
@@ -802,7 +829,8 @@ def run_aux(args, dev):
                   "criterion": "fp4 e2m1 MFMA -> f32 (0/+-1 products)"}[args.workload],
         "data": "synthetic (uniform random u16 / on-device generated templates)",
         "config": {"workload": workload, "records_per_gpu": n, "parties": P,
-                   **({"chunk": chunk, "attached": bool(args.attached)}
+                   **({"chunk": chunk, "attached": bool(args.attached), "mmap": bool(args.mmap),
+                       "auto_resident": not args.no_auto_resident}
                       if args.workload in ("host-shares", "host-masks") else {})},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
@@ -814,7 +842,8 @@ def run_aux(args, dev):
                    "bytes_per_record": rec_bytes},
         "file_GBps": (n * 3200 * args.steps / elapsed / 1e9) if args.workload == "load" else None,
         "host_input_GBps": (n * rec_bytes * args.steps / elapsed / 1e9)
-        if args.workload in ("host-shares", "host-masks") and not args.attached else None,
+        if args.workload in ("host-shares", "host-masks") and not args.attached
+        and not (args.mmap and not args.no_auto_resident) else None,
         "cpu_baseline": cpu,
         "check": check,
         **extra,
@@ -845,6 +874,8 @@ def main():
     if args.workload in AUX_WORKLOADS:
         if world_gpus > 1:
             raise SystemExit(f"workload {args.workload} is a single-GPU line (run without --gpus / torchrun)")
+        if args.no_auto_resident:
+            os.environ["IRIS_AUTO_RESIDENT"] = "0"  # read when the device opens
         return run_aux(args, ih.Device(0))
     if args.single_process and args.workload not in ("search", "batch"):
         raise SystemExit("--single-process runs the group search (--workload search / batch)")

@@ -117,6 +117,7 @@ extern "C" {
     pub fn iris_device_reset_stats(dev: *mut IrisDevice) -> c_int;
     pub fn iris_device_alloc(dev: *mut IrisDevice, bytes: usize, ptr: *mut *mut c_void) -> c_int;
     pub fn iris_device_free(dev: *mut IrisDevice, ptr: *mut c_void) -> c_int;
+    pub fn iris_device_drop_resident(dev: *mut IrisDevice) -> c_int;
     pub fn iris_memcpy_d2h(dev: *mut IrisDevice, host: *mut c_void, device: *const c_void, bytes: usize) -> c_int;
     pub fn iris_memcpy_h2d(dev: *mut IrisDevice, device: *mut c_void, host: *const c_void, bytes: usize) -> c_int;
 

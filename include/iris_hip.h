@@ -249,9 +249,19 @@ int iris_engine_batch_process_device(iris_engine_t *engine, const iris_db_t *db,
                                      uint16_t *out_device);
 /* Host-slice form with exactly the reference signature: `db` is a host array
  * of n reference-layout records, `out` a host array of n*31 uint16_t.  A slice
- * of an attached host array (iris_db_attach_host) runs on the resident copy;
- * any other slice is uploaded (PCIe) and packed first. */
+ * of an attached host array (iris_db_attach_host) runs on the resident copy.
+ * A slice inside a read-only shared mapping of a regular file -- what the
+ * participant and resolver walk (src/main.rs:386-391, 426-431; 455-460,
+ * 511-516) -- runs on the device's copy of that file's records, made on first
+ * use (256-MB granules as calls reach them) and kept; every call re-checks the
+ * file behind the mapping (device, inode, size, mtime, ctime) and probes three
+ * records of the slice, and a changed file is copied afresh.  Files that do not
+ * fit the device's free memory (less a reserve) and IRIS_AUTO_RESIDENT=0 keep
+ * the upload path.  Any other slice is uploaded (PCIe) and packed first. */
 int iris_engine_batch_process_host(iris_engine_t *engine, const void *db, uint64_t n, uint16_t *out);
+/* Frees the device's resident file copies (a failing iris_db_create does so too
+ * before it retries); iris_config reports them as resident=count/bytes. */
+int iris_device_drop_resident(iris_device_t *dev);
 
 /* Template engine, per template and rotation k: num = popcount((qp^ep)&qm&em),
  * den = popcount(qm&em) with q rotated by k-15 (src/template.rs:49-64).

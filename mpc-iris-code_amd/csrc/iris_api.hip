@@ -114,9 +114,10 @@ namespace {
 
 int db_write_runtime(iris_db *db, uint64_t index, const void *records, uint64_t n);
 
-int db_write_locked(iris_db *db, uint64_t index, const void *records, uint64_t n) {
+}  // namespace
+
+int iris_api::db_store_locked(iris_db *db, uint64_t index, const void *records, uint64_t n) {
     iris_device *d = db->dev;
-    db_detach(db);
     if (index > db->len) return fail(IRIS_E_RANGE, "iris_db_write: index beyond the end of the database");
     if (n > db->cap - index) return fail(IRIS_E_RANGE, "iris_db_write: database capacity exceeded");
     if (n == 0) return 0;
@@ -139,6 +140,13 @@ int db_write_locked(iris_db *db, uint64_t index, const void *records, uint64_t n
         return 0;
     }
     return db_write_runtime(db, index, records, n);
+}
+
+namespace {
+
+int db_write_locked(iris_db *db, uint64_t index, const void *records, uint64_t n) {
+    db_detach(db);
+    return db_store_locked(db, index, records, n);
 }
 
 // The runtime's copy of the pageable source, through one 256-MB staging chunk at a time.
@@ -539,6 +547,7 @@ void device_teardown(iris_device *d) {
     {
         std::lock_guard<std::recursive_mutex> g(d->mu);
         (void)hipSetDevice(d->ordinal);
+        resident_drop_all(d);
         (void)hipStreamSynchronize(d->stream);
         for (DevBuf *b : {&d->partials, &d->result, &d->staging, &d->out_a, &d->out_b, &d->ticket, &d->tempdb})
             if (b->p) (void)hipFree(b->p);
@@ -617,6 +626,12 @@ int iris_config(const iris_device_t *d, char *buf, size_t len, size_t *needed) {
         char r[96];  // large writes' measured rates (GB/s) through the pinned slots / the runtime's copy
         snprintf(r, sizeof(r), " upload_gbps=%.1f/%.1f", d->upload_tune.gbps[0] / 1e9, d->upload_tune.gbps[1] / 1e9);
         s += r;
+        uint64_t rc = 0, rbytes = 0;
+        {
+            std::lock_guard<std::recursive_mutex> g(const_cast<iris_device *>(d)->mu);
+            resident_stats(d, &rc, &rbytes);
+        }
+        s += " resident=" + std::to_string(rc) + "/" + std::to_string(rbytes);
     }
     if (buf && len) {
         const size_t n = std::min(len - 1, s.size());
@@ -801,6 +816,11 @@ int iris_db_create_ex(iris_device_t *d, int kind, uint64_t capacity, int layout,
     }
     db->cap = capacity == 0 ? 0 : blocks * db->k.block;
     hipError_t e = hipMalloc(&db->data, bytes);
+    if (e != hipSuccess && !d->resident.empty()) {  // the caller's database before cached file copies
+        (void)hipGetLastError();
+        resident_drop_all(d);
+        e = hipMalloc(&db->data, bytes);
+    }
     if (e != hipSuccess) {
         delete db;
         return fail(IRIS_E_NOMEM, std::string("hipMalloc database (") + std::to_string(bytes) +
@@ -1132,6 +1152,16 @@ int iris_engine_batch_process_host(iris_engine_t *e, const void *records, uint64
         if (readahead_ok(a, n)) return readahead_u16_call(e, a, off / k.rec_bytes, n, a->host_n, out);
         CHK(ra_wait(e));
         return run_u16_engine(e, a, off / k.rec_bytes, n, out);
+    }
+    // a slice of a read-only record file mapping (the reference's participant / resolver walk):
+    // run on the device's resident copy of the file (iris_resident.hip)
+    iris_db *rdb = nullptr;
+    uint64_t rfirst = 0, rend = 0;
+    CHK(resident_slice(d, e->kind, records, n, &rdb, &rfirst, &rend));
+    if (rdb) {
+        if (readahead_ok(rdb, n)) return readahead_u16_call(e, rdb, rfirst, n, rend, out);
+        CHK(ra_wait(e));
+        return run_u16_engine(e, rdb, rfirst, n, out);
     }
     const uint64_t ch = std::min<uint64_t>(n, 1ull << 20 >> (e->kind == IRIS_KIND_SHARES ? 4 : 0));
     TempDb t;

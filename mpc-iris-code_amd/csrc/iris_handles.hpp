@@ -139,6 +139,11 @@ struct iris_device {
     // databases attached to a host array (iris_db_attach_host): host-slice engine calls
     // on a range inside one of them run on the resident copy
     std::vector<struct iris_db *> attached;
+    // read-only file mappings kept resident for host-slice calls (iris_resident.hip), the address
+    // ranges found ineligible, and the use counter of their LRU eviction
+    std::vector<struct Resident *> resident;
+    std::vector<std::pair<uintptr_t, uintptr_t>> not_resident;
+    uint64_t resident_clock = 0;
 };
 
 struct iris_db {
@@ -406,6 +411,17 @@ using SlotFill = std::function<bool(void *dst, size_t off, size_t bytes)>;
 // fill (optional) fills the slots instead of a copy from `records` (e.g. pread from a file).
 // IRIS_E_NOMEM only before anything was written (the pinned slots or the staging buffer).
 int db_write_pinned(iris_db *db, uint64_t index, const void *records, uint64_t n, const SlotFill *fill = nullptr);
+// db_write's store without the detach: host records [0, n) at index (index <= len; grows len).
+int db_store_locked(iris_db *db, uint64_t index, const void *records, uint64_t n);
+// A host slice [ptr, ptr + n records of `kind`) inside a read-only shared mapping of a regular
+// file: *db = the device's resident copy of that mapping's records (uploaded granule by granule
+// on first use), *first = the slice's record index in it, *end = the end of the resident run
+// from there (a read-ahead bound).  *db = nullptr: not such a slice, IRIS_AUTO_RESIDENT=0, or
+// the file does not fit the device -- the caller uploads.  Caller holds the device lock.
+int resident_slice(iris_device *d, int kind, const void *ptr, uint64_t n, iris_db **db, uint64_t *first,
+                   uint64_t *end);
+void resident_drop_all(iris_device *d);  // frees every resident copy (waits for the device's streams)
+void resident_stats(const iris_device *d, uint64_t *count, uint64_t *bytes);
 // Partial (indices offset by base) -> iris_match_t; +inf / UINT64_MAX when none
 void match_from(const iris::Partial &r, bool any, uint64_t base, iris_match_t *out);
 

@@ -328,6 +328,7 @@ uint32_t env_u32(const char *v, uint32_t max) {
 void read_hooks(Hooks *h) {
     *h = Hooks{};
     if (const char *v = env("IRIS_READAHEAD")) h->readahead = v[0] != '0';
+    if (const char *v = env("IRIS_AUTO_RESIDENT")) h->auto_resident = v[0] != '0';
     if (const char *v = env("IRIS_GROUP_TIMEOUT_MS")) h->group_timeout_ms = env_u32(v, 24u * 3600 * 1000);
     const char *t = env("IRIS_TEST_HOOKS");
     h->test = t && t[0] == '1';
@@ -356,7 +357,8 @@ void read_hooks(Hooks *h) {
 size_t format_hooks(const Hooks &h, char *buf, size_t len) {
     static const char *sched[] = {"auto", "spin", "yield", "blocking"};
     static const char *upload_names[] = {"auto", "pinned", "runtime", "auto"};
-    std::string s = "readahead=" + std::to_string(h.readahead) + " group_timeout_ms=" +
+    std::string s = "readahead=" + std::to_string(h.readahead) + " auto_resident=" + std::to_string(h.auto_resident) +
+                    " group_timeout_ms=" +
                     (h.group_timeout_ms ? std::to_string(h.group_timeout_ms) : std::string("auto")) +
                     " copy_helpers=" + std::to_string(copy_helpers()) + " test_hooks=" + std::to_string(h.test);
     if (h.test)

@@ -172,6 +172,7 @@ IRIS_HD inline uint64_t gen_limb(uint64_t key, uint64_t ctr) {
 struct Hooks {
     // production knobs
     bool readahead = true;           // IRIS_READAHEAD=0: no read-ahead of host-output engine calls
+    bool auto_resident = true;       // IRIS_AUTO_RESIDENT=0: host slices of read-only file mappings upload per call
     uint32_t group_timeout_ms = 0;   // IRIS_GROUP_TIMEOUT_MS: bound of a group exchange wait (0: auto)
     // test-only hooks (IRIS_TEST_HOOKS=1)
     bool test = false;

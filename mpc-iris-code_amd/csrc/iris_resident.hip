@@ -1,0 +1,298 @@
+// iris_resident.hip — record files kept resident for the reference's unchanged call sites.
+//
+// The participant and the resolver mmap their record file once (src/main.rs:386-391, 455-460)
+// and call batch_process(out, chunk) on 20 000-record slices of that mapping for every request
+// (src/main.rs:426-431, 511-516).  Through iris_engine_batch_process_host each such call would
+// move its slice over PCIe, which cannot beat a CPU scan of the same bytes from DRAM
+// (profiles/r04ae_bench_host-masks_chunk20k.jsonl: 0.72x the 16-thread CPU port).  Not moving
+// the bytes is what helps: a slice that lies inside a read-only, shared, file-backed mapping of a
+// regular file is served from a device copy of the whole mapping, made granule by granule (256 MB)
+// the first time a call touches it, so the first walk costs what the upload path costs and every
+// later walk reads HBM only.
+//
+// Staleness: the copy stands for (st_dev, st_ino, st_size, st_mtim, st_ctim) of the mapped file,
+// re-checked on every call with one stat of /proc/self/map_files/<lo>-<hi> (the kernel's link to
+// the file behind exactly that mapping: a mapping that went away or was replaced fails or shows
+// another inode; ~2.5 us), plus a probe of three records of the slice against 64-byte snapshots
+// taken when their granule was uploaded (a write the timestamps miss: their granularity is the
+// kernel's tick).  A changed file drops its copy; the call then starts over.
+//
+// Not made resident: anonymous or writable memory, private mappings, files larger than the
+// device's free memory (less a reserve; older copies are evicted first, least recently used),
+// IRIS_AUTO_RESIDENT=0.  Those slices keep the upload path.  A device allocation that fails
+// (iris_db_create) drops every resident copy and retries.
+#include <errno.h>
+#include <stdio.h>
+#include <string.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "iris_handles.hpp"
+
+using namespace iris;
+using namespace iris_api;
+
+namespace {
+
+constexpr size_t kGranuleBytes = 256ull << 20;  // upload unit of a resident copy
+constexpr size_t kSnapBytes = 64;              // probe snapshot of every 64th record
+constexpr uint64_t kSnapStride = 64;
+constexpr size_t kNotResidentMax = 4096;       // remembered ineligible address ranges
+
+}  // namespace
+
+struct Resident {
+    int kind = 0;
+    uintptr_t lo = 0, hi = 0;  // the mapping (one VMA)
+    uintptr_t base = 0;        // address of record 0 (the first whole record of the slices seen)
+    uint64_t nrec = 0;
+    std::string link;          // /proc/self/map_files/<lo>-<hi>
+    struct stat st {};
+    iris_db *db = nullptr;
+    size_t dev_bytes = 0;
+    uint64_t gran = 0;              // records per granule
+    std::vector<uint8_t> have;      // granule uploaded
+    std::vector<uint8_t> snap;      // kSnapBytes of record i * kSnapStride
+    uint64_t last_use = 0;
+};
+
+namespace {
+
+bool same_time(const struct timespec &a, const struct timespec &b) {
+    return a.tv_sec == b.tv_sec && a.tv_nsec == b.tv_nsec;
+}
+
+void free_copy(iris_device *d, Resident *r) {
+    // a read-ahead kernel on the side stream may still read the copy
+    (void)hipStreamSynchronize(d->stream);
+    if (d->aux) (void)hipStreamSynchronize(d->aux);
+    if (r->db) {
+        if (r->db->data) (void)hipFree(r->db->data);
+        delete r->db;
+    }
+    delete r;
+}
+
+void drop(iris_device *d, Resident *r) {
+    auto &v = d->resident;
+    v.erase(std::remove(v.begin(), v.end(), r), v.end());
+    free_copy(d, r);
+}
+
+void remember_not_resident(iris_device *d, uintptr_t lo, uintptr_t hi) {
+    if (d->not_resident.size() >= kNotResidentMax) d->not_resident.clear();
+    d->not_resident.emplace_back(lo, hi);
+}
+
+// The mapping of /proc/self/maps that holds address p.
+struct Vma {
+    uintptr_t lo = 0, hi = 0;
+    char perms[8] = {0};
+    uint64_t off = 0;
+    uint64_t inode = 0;
+    std::string path;
+};
+
+bool find_vma(uintptr_t p, Vma *out) {
+    FILE *f = fopen("/proc/self/maps", "re");
+    if (!f) return false;
+    char line[4352];
+    bool found = false;
+    while (fgets(line, sizeof(line), f)) {
+        unsigned long lo, hi, off, ino;
+        unsigned int maj, mnr;
+        char perms[8];
+        int pos = 0;
+        if (sscanf(line, "%lx-%lx %7s %lx %x:%x %lu %n", &lo, &hi, perms, &off, &maj, &mnr, &ino, &pos) < 7) continue;
+        if (p < lo || p >= hi) continue;
+        out->lo = lo;
+        out->hi = hi;
+        memcpy(out->perms, perms, sizeof(perms));
+        out->off = off;
+        out->inode = ino;
+        std::string path = line + pos;
+        while (!path.empty() && (path.back() == '\n' || path.back() == ' ')) path.pop_back();
+        out->path = path;
+        found = true;
+        break;
+    }
+    fclose(f);
+    return found;
+}
+
+// A new resident copy of the file mapping that holds the slice [p, p + n records), or nullptr
+// (not eligible: remembered as such).  Errors are not reported: the caller uploads instead.
+Resident *make_resident(iris_device *d, int kind, uintptr_t p, uint64_t n) {
+    const KindInfo k = kind_info(kind, IRIS_LAYOUT_TILES);
+    const size_t rb = k.rec_bytes;
+    Vma v;
+    if (!find_vma(p, &v)) return nullptr;
+    auto ineligible = [&]() -> Resident * {
+        remember_not_resident(d, v.lo, v.hi);
+        return nullptr;
+    };
+    // read-only (not writable), shared, backed by a named file
+    if (v.perms[0] != 'r' || v.perms[1] != '-' || v.perms[3] != 's' || v.inode == 0 || v.path.empty() ||
+        v.path[0] != '/' || v.path.find(" (deleted)") != std::string::npos)
+        return ineligible();
+    char link[96];
+    snprintf(link, sizeof(link), "/proc/self/map_files/%lx-%lx", (unsigned long)v.lo, (unsigned long)v.hi);
+    struct stat st;
+    if (stat(link, &st) != 0 || !S_ISREG(st.st_mode) || (uint64_t)st.st_ino != v.inode) return ineligible();
+    if ((uint64_t)st.st_size <= v.off) return ineligible();
+    const uintptr_t data_end = v.lo + std::min<uint64_t>(v.hi - v.lo, (uint64_t)st.st_size - v.off);
+    const uintptr_t base = v.lo + (p - v.lo) % rb;
+    if (data_end < base + rb) return ineligible();
+    const uint64_t nrec = (data_end - base) / rb;
+    if ((p - base) / rb + n > nrec) return nullptr;  // the slice runs past the file's records
+    const uint64_t blocks = (nrec + k.block - 1) / k.block;
+    const size_t dev_bytes = (size_t)blocks * block_bytes(k);
+    // copies of mappings that are gone (unmapped, or their file replaced) free their memory first
+    for (size_t i = d->resident.size(); i-- > 0;) {
+        Resident *o = d->resident[i];
+        struct stat ost;
+        if (stat(o->link.c_str(), &ost) != 0 || ost.st_ino != o->st.st_ino || ost.st_dev != o->st.st_dev) drop(d, o);
+    }
+    // room: the device's free memory less a reserve, after evicting older copies if need be
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return ineligible();
+    const size_t reserve = std::max<size_t>(2ull << 30, total_b / 32);
+    size_t evictable = 0;
+    for (Resident *r : d->resident) evictable += r->dev_bytes;
+    if (dev_bytes + reserve > free_b + evictable) return ineligible();
+    while (dev_bytes + reserve > free_b && !d->resident.empty()) {
+        auto lru = std::min_element(d->resident.begin(), d->resident.end(),
+                                    [](const Resident *a, const Resident *b) { return a->last_use < b->last_use; });
+        drop(d, *lru);
+        if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return nullptr;
+    }
+    Resident *r = new (std::nothrow) Resident();
+    if (!r) return nullptr;
+    r->db = new (std::nothrow) iris_db();
+    if (!r->db || hipMalloc(&r->db->data, dev_bytes) != hipSuccess) {
+        (void)hipGetLastError();
+        if (r->db) r->db->data = nullptr;
+        free_copy(d, r);
+        return ineligible();
+    }
+    // zeroed: the last block's padding records are never candidates
+    if (hipMemsetAsync(r->db->data, 0, dev_bytes, d->stream) != hipSuccess) {
+        free_copy(d, r);
+        return nullptr;
+    }
+    r->db->dev = d;
+    r->db->k = k;
+    r->db->cap = blocks * k.block;
+    r->db->len = nrec;  // every record is addressable; only uploaded granules are ever computed on
+    r->db->version = next_db_version();
+    r->kind = kind;
+    r->lo = v.lo;
+    r->hi = v.hi;
+    r->base = base;
+    r->nrec = nrec;
+    r->link = link;
+    r->st = st;
+    r->dev_bytes = dev_bytes;
+    r->gran = std::max<uint64_t>(64, kGranuleBytes / rb / 64 * 64);
+    r->have.assign((nrec + r->gran - 1) / r->gran, 0);
+    r->snap.assign((nrec + kSnapStride - 1) / kSnapStride * kSnapBytes, 0);
+    d->resident.push_back(r);
+    return r;
+}
+
+// Uploads the granules of [first, first + n) that are not resident yet.
+int fill(Resident *r, uint64_t first, uint64_t n) {
+    const size_t rb = r->db->k.rec_bytes;
+    for (uint64_t g = first / r->gran; g * r->gran < first + n; ++g) {
+        if (r->have[g]) continue;
+        const uint64_t a = g * r->gran, m = std::min<uint64_t>(r->gran, r->nrec - a);
+        const char *src = (const char *)r->base + a * rb;
+        CHK(db_store_locked(r->db, a, src, m));
+        for (uint64_t i = (a + kSnapStride - 1) / kSnapStride * kSnapStride; i < a + m; i += kSnapStride)
+            memcpy(&r->snap[i / kSnapStride * kSnapBytes], (const char *)r->base + i * rb, std::min(kSnapBytes, rb));
+        r->have[g] = 1;
+    }
+    return 0;
+}
+
+// The slice's probe: up to three snapshotted records inside [first, first + n) still equal the mapping.
+bool probe_ok(const Resident *r, uint64_t first, uint64_t n) {
+    const size_t rb = r->db->k.rec_bytes, cmp = std::min(kSnapBytes, rb);
+    const uint64_t p0 = (first + kSnapStride - 1) / kSnapStride, p2 = (first + n - 1) / kSnapStride;
+    if (p0 > p2) return true;  // no snapshotted record in a slice this short
+    const uint64_t ps[3] = {p0, (p0 + p2) / 2, p2};
+    for (uint64_t q : ps)
+        if (memcmp(&r->snap[q * kSnapBytes], (const char *)r->base + q * kSnapStride * rb, cmp) != 0) return false;
+    return true;
+}
+
+}  // namespace
+
+int iris_api::resident_slice(iris_device *d, int kind, const void *ptr, uint64_t n, iris_db **db, uint64_t *first,
+                             uint64_t *end) {
+    *db = nullptr;
+    if (!d->hooks.auto_resident || n == 0) return 0;
+    const uintptr_t p = (uintptr_t)ptr;
+    const size_t rb = kind_info(kind, IRIS_LAYOUT_TILES).rec_bytes;
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        Resident *r = nullptr;
+        for (Resident *c : d->resident)
+            if (c->kind == kind && p >= c->lo && p < c->hi) {
+                r = c;
+                break;
+            }
+        if (!r) {
+            for (const auto &x : d->not_resident)
+                if (p >= x.first && p < x.second) return 0;
+            r = make_resident(d, kind, p, n);
+            if (!r) return 0;
+        }
+        // whole records of this copy's record grid, inside the file's records
+        if (p < r->base || (p - r->base) % rb != 0 || (p - r->base) / rb + n > r->nrec) return 0;
+        struct stat st;
+        if (stat(r->link.c_str(), &st) != 0 || st.st_dev != r->st.st_dev || st.st_ino != r->st.st_ino ||
+            st.st_size != r->st.st_size || !same_time(st.st_mtim, r->st.st_mtim) ||
+            !same_time(st.st_ctim, r->st.st_ctim)) {
+            drop(d, r);  // the mapping went away or its file changed: start over
+            continue;
+        }
+        const uint64_t f = (p - r->base) / rb;
+        CHK(fill(r, f, n));
+        if (!probe_ok(r, f, n)) {  // written without a timestamp change: start over
+            drop(d, r);
+            continue;
+        }
+        r->last_use = ++d->resident_clock;
+        uint64_t g = f / r->gran;
+        while (g < r->have.size() && r->have[g]) ++g;
+        *db = r->db;
+        *first = f;
+        *end = std::min<uint64_t>(r->nrec, g * r->gran);
+        return 0;
+    }
+    return 0;  // changed twice in one call: this call uploads
+}
+
+void iris_api::resident_drop_all(iris_device *d) {
+    while (!d->resident.empty()) drop(d, d->resident.back());
+    d->not_resident.clear();
+}
+
+void iris_api::resident_stats(const iris_device *d, uint64_t *count, uint64_t *bytes) {
+    *count = d->resident.size();
+    *bytes = 0;
+    for (const Resident *r : d->resident) *bytes += r->dev_bytes;
+}
+
+extern "C" int iris_device_drop_resident(iris_device_t *d) {
+    IRIS_KEEP_DEVICE();
+    ARG(d, "device is NULL");
+    std::lock_guard<std::recursive_mutex> g(d->mu);
+    CHK(set_device(d));
+    resident_drop_all(d);
+    return 0;
+}

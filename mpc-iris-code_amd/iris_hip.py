@@ -90,6 +90,7 @@ def load_library(path=None):
             "iris_device_reset_stats": ([P], ctypes.c_int),
             "iris_device_alloc": ([P, ctypes.c_size_t, PP], ctypes.c_int),
             "iris_device_free": ([P, P], ctypes.c_int),
+            "iris_device_drop_resident": ([P], ctypes.c_int),
             "iris_memcpy_d2h": ([P, P, P, ctypes.c_size_t], ctypes.c_int),
             "iris_db_create": ([P, ctypes.c_int, u64, PP], ctypes.c_int),
             "iris_db_create_ex": ([P, ctypes.c_int, u64, ctypes.c_int, PP], ctypes.c_int),
@@ -177,7 +178,8 @@ def exported_symbols():
     return [
         "iris_last_error", "iris_version", "iris_config", "iris_device_count", "iris_device_open", "iris_device_close",
         "iris_device_synchronize", "iris_device_stream", "iris_device_set_profiling", "iris_device_kernel_stats",
-        "iris_device_reset_stats", "iris_device_alloc", "iris_device_free", "iris_memcpy_d2h", "iris_db_create",
+        "iris_device_reset_stats", "iris_device_alloc", "iris_device_free", "iris_device_drop_resident",
+        "iris_memcpy_d2h", "iris_db_create",
         "iris_db_create_ex", "iris_db_layout",
         "iris_db_destroy", "iris_db_len", "iris_db_capacity", "iris_db_kind", "iris_db_append", "iris_db_write",
         "iris_db_read", "iris_db_generate", "iris_db_clear", "iris_masks_engine_new", "iris_distance_engine_new",
@@ -484,6 +486,15 @@ class Device:
         f, t = ctypes.c_size_t(), ctypes.c_size_t()
         _check(load_library().iris_device_memory(self.handle, ctypes.byref(f), ctypes.byref(t)))
         return f.value, t.value
+
+    def resident(self):
+        """(count, bytes) of the record-file copies this device keeps resident for host-slice calls."""
+        c, b = self.config()["resident"].split("/")
+        return int(c), int(b)
+
+    def drop_resident(self):
+        """Frees the device's resident record-file copies (iris_device_drop_resident)."""
+        _check(load_library().iris_device_drop_resident(self.handle))
 
     def stream(self):
         s = ctypes.c_void_p()

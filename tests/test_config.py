@@ -14,13 +14,15 @@ TEST_HOOKS = ["IRIS_TILES_PER_WAVE", "IRIS_FUSED_REDUCE", "IRIS_BATCH_KERNEL", "
 
 @pytest.fixture(autouse=True)
 def clean_env(monkeypatch):
-    for k in TEST_HOOKS + ["IRIS_TEST_HOOKS", "IRIS_READAHEAD", "IRIS_GROUP_TIMEOUT_MS", "IRIS_COPY_HELPERS"]:
+    for k in TEST_HOOKS + ["IRIS_TEST_HOOKS", "IRIS_READAHEAD", "IRIS_AUTO_RESIDENT", "IRIS_GROUP_TIMEOUT_MS",
+                           "IRIS_COPY_HELPERS"]:
         monkeypatch.delenv(k, raising=False)
 
 
 def test_defaults():
     c = ih.config()
-    assert c == {"readahead": "1", "group_timeout_ms": "auto", "copy_helpers": "3", "test_hooks": "0"}
+    assert c == {"readahead": "1", "auto_resident": "1", "group_timeout_ms": "auto", "copy_helpers": "3",
+                 "test_hooks": "0"}
 
 
 def test_test_hooks_ignored_without_opt_in(monkeypatch):
@@ -51,10 +53,12 @@ def test_test_hooks_with_opt_in(monkeypatch):
 
 def test_production_knobs_need_no_opt_in(monkeypatch):
     monkeypatch.setenv("IRIS_READAHEAD", "0")
+    monkeypatch.setenv("IRIS_AUTO_RESIDENT", "0")
     monkeypatch.setenv("IRIS_GROUP_TIMEOUT_MS", "45000")
     monkeypatch.setenv("IRIS_COPY_HELPERS", "5")
     c = ih.config()
-    assert (c["readahead"], c["group_timeout_ms"], c["copy_helpers"], c["test_hooks"]) == ("0", "45000", "5", "0")
+    assert (c["readahead"], c["auto_resident"], c["group_timeout_ms"], c["copy_helpers"], c["test_hooks"]) == \
+        ("0", "0", "45000", "5", "0")
     assert "ignored" not in c
 
 
