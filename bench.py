@@ -98,7 +98,7 @@ def parse():
                     help="ChaCha rounds for --workload prepare (12 = the reference's thread_rng, rand 0.8.5)")
     ap.add_argument("--single-process", action="store_true",
                     help="search / batch: ONE process drives --gpus devices as a library device group "
-                         "(iris_group_*: ncclCommInitAll, RCCL all-gather of the shard winners) instead of "
+                         "(iris_group_*: one RCCL communicator per device, all-gather of the shard winners) instead of "
                          "one torchrun rank per GPU")
     ap.add_argument("--attached", action="store_true",
                     help="host-shares / host-masks: the host array is attached to a resident database "
@@ -456,7 +456,7 @@ class Ranks:
             if "WORLD_SIZE" in os.environ and self.world > 1:
                 raise SystemExit("error: --single-process drives every GPU from one process; do not launch ranks")
             self.world, self.rank = 1, 0
-            self.backend = "rccl (library group, ncclCommInitAll)"
+            self.backend = "rccl (library group, one process: non-blocking ncclCommInitRankConfig per device)"
             return
         if self.world != args.gpus:
             raise SystemExit(f"error: --gpus {args.gpus} but the launcher started WORLD_SIZE={self.world} ranks")
@@ -476,11 +476,17 @@ class Ranks:
             if backend == "nccl" and self.local >= have and not own:
                 raise SystemExit(f"error: rank {self.rank} (local {self.local}) has no GPU of its own: {have} visible")
             self.ordinal = 0 if own else self.local % max(1, have)
-        dist.init_process_group("gloo", rank=self.rank, world_size=self.world)
+        # bounded: a rank that never starts fails the others here instead of holding them for
+        # torch's default 30 minutes (IRIS_DIST_TIMEOUT_S overrides)
+        import datetime
+
+        dist.init_process_group("gloo", rank=self.rank, world_size=self.world,
+                                timeout=datetime.timedelta(seconds=float(os.environ.get("IRIS_DIST_TIMEOUT_S", "300"))))
         if dist.get_world_size() != args.gpus:
             raise SystemExit(f"error: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
         self.dist = dist
-        self.backend = "gloo" if backend == "gloo" else "rccl (library group, ncclCommInitRank; gloo control)"
+        self.backend = ("gloo" if backend == "gloo" else
+                        "rccl (library group, non-blocking ncclCommInitRankConfig; gloo control)")
         self.rccl = backend == "nccl"
 
     def join_group(self, args):
@@ -1124,6 +1130,10 @@ def main():
             "value_per_gpu": value / world_gpus,
             "n_gpus": world_gpus,
             "ranks_seen": ranks.dist.get_world_size() if ranks.dist is not None else 1,
+            # what the library's RCCL communicator itself reports (ncclCommCount, and every rank's
+            # device PCI bus id gathered over that communicator), not torch's view
+            "rccl_nranks": group.rccl_nranks if group is not None else None,
+            "rccl_devices": group.rccl_devices if group is not None else None,
             "processes": ranks.world,
             "backend": ranks.backend,
             "launcher": launcher_name() if not args.single_process else "none (one process, library device group)",
@@ -1210,10 +1220,20 @@ def main():
     else:
         db.close()
         dev.close()
+    # the run is the claimed one only if RCCL saw --gpus ranks on as many distinct devices
+    rccl_bad = None
+    if group is not None:
+        if group.rccl_nranks != world_gpus:
+            rccl_bad = f"RCCL communicator holds {group.rccl_nranks} ranks, --gpus {world_gpus}"
+        elif len(set(group.rccl_devices)) != len(group.rccl_devices):
+            rccl_bad = f"two RCCL ranks on one device: {group.rccl_devices}"
     ranks.close()
     if not ok:
         print(f"result check failed: {check}", file=sys.stderr)
         sys.exit(3)
+    if rccl_bad:
+        print(f"RCCL check failed: {rccl_bad}", file=sys.stderr)
+        sys.exit(4)
 
 
 if __name__ == "__main__":

@@ -39,6 +39,7 @@ pub const IRIS_LAYOUT_TILES: c_int = 2;
 
 /// Bytes of a device group's RCCL id (`iris_group_unique_id`).
 pub const IRIS_GROUP_ID_BYTES: usize = 128;
+pub const IRIS_GROUP_BUS_ID_BYTES: usize = 32;
 
 /// Opaque handles (`iris_device_t`, `iris_db_t`, `iris_engine_t`, `iris_pending_t`).
 #[repr(C)]
@@ -332,6 +333,7 @@ extern "C" {
         ranks: *mut u32,
         first_rank: *mut u32,
     ) -> c_int;
+    pub fn iris_group_rccl_info(group: *const IrisGroup, comm_ranks: *mut u32, bus_ids: *mut c_char, len: usize) -> c_int;
     pub fn iris_group_device(group: *const IrisGroup, i: u32, dev: *mut *mut IrisDevice) -> c_int;
     pub fn iris_group_db_create(
         group: *mut IrisGroup,

@@ -373,12 +373,18 @@ int iris_match_merge(const iris_match_t *records, uint64_t count, iris_match_t *
  * (exact fraction, then the lowest global index).
  *
  * Two ways to form a group:
- *  - iris_group_create: ONE process drives `n` devices (ncclCommInitAll).
+ *  - iris_group_create: ONE process drives `n` devices (ncclCommInitAll's form:
+ *    one id, every device a rank, created inside one RCCL group).
  *  - iris_group_create_rank: one device per process (e.g. a torchrun rank):
  *    rank 0 calls iris_group_unique_id and hands the 128 id bytes to every
  *    rank (any side channel); each rank then calls iris_group_create_rank with
- *    the same id (ncclCommInitRank).  Every rank makes the same group calls
- *    (SPMD); each holds and fills only its own shards.
+ *    the same id.  Every rank makes the same group calls (SPMD); each holds
+ *    and fills only its own shards.
+ * Forming a group is bounded: the communicators are created non-blocking
+ * (ncclCommInitRankConfig, blocking = 0) and polled until ready, then every
+ * rank's PCI bus id is all-gathered over them; if a peer never arrives the call
+ * aborts its communicators and fails (IRIS_E_HIP) within IRIS_GROUP_TIMEOUT_MS
+ * (default 120 s) instead of hanging, and the device stays usable.
  * Group calls are blocking and serialised per group, like the device calls.
  *
  * Failure: waiting for an exchange is bounded.  The clock starts when every
@@ -404,6 +410,13 @@ int iris_group_set_timeout(iris_group_t *group, uint32_t ms);
 /* local_devices: devices this process drives; ranks: RCCL ranks in the group
  * (all processes); first_rank: the rank of local device 0. */
 int iris_group_info(const iris_group_t *group, uint32_t *local_devices, uint32_t *ranks, uint32_t *first_rank);
+/* What RCCL itself reports for the group: *comm_ranks = ncclCommCount of its
+ * communicators, and (bus_ids may be NULL; len >= ranks * IRIS_GROUP_BUS_ID_BYTES)
+ * every rank's device PCI bus id ("0000:05:00.0", NUL-terminated) at
+ * bus_ids + rank * IRIS_GROUP_BUS_ID_BYTES, gathered over the group's own RCCL
+ * all-gather when it formed. */
+#define IRIS_GROUP_BUS_ID_BYTES 32
+int iris_group_rccl_info(const iris_group_t *group, uint32_t *comm_ranks, char *bus_ids, size_t len);
 /* Local device i of the group (borrowed: valid until iris_group_destroy), e.g.
  * for iris_device_set_profiling / iris_device_kernel_stats. */
 int iris_group_device(const iris_group_t *group, uint32_t i, iris_device_t **dev);

@@ -27,7 +27,13 @@
 // (which waits for the peers) and the merge are left; RCCL's asynchronous error
 // is polled meanwhile.  On expiry or error the group's communicators are
 // aborted (ncclCommAbort) and the call returns IRIS_E_HIP; the group then
-// refuses every further call except the destroys.
+// refuses every further call except the destroys.  Forming the group is bounded
+// the same way: the communicators are created non-blocking
+// (ncclCommInitRankConfig, config.blocking = 0) and polled until ready, and a
+// rank whose peers never arrive aborts them and fails instead of hanging.  With
+// non-blocking communicators ncclGroupEnd may return ncclInProgress (RCCL
+// launches the group's work from a helper thread): the exchange then waits,
+// bounded, for the launch before it orders anything after the all-gather.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <string.h>
@@ -54,6 +60,10 @@ struct iris_group {
     std::vector<iris_device *> devs;  // local devices (owned)
     std::vector<ncclComm_t> comms;    // comms[i]: local device i, RCCL rank rank0 + i
     uint32_t ranks = 0, rank0 = 0;
+    // what RCCL itself reports: ncclCommCount of the communicators, and every rank's PCI bus id
+    // (gathered over the group's own all-gather when it formed)
+    uint32_t comm_count = 0;
+    std::vector<std::string> bus_ids;
     std::mutex mu;                    // serialises group calls
     std::atomic<int> refs{1};         // the group handle + each database and pending search
     uint32_t timeout_ms = 0;          // exchange wait bound (0: auto, group_timeout)
@@ -309,11 +319,17 @@ int group_wait(iris_group *g, const std::vector<hipEvent_t> &reached, const std:
             }
         }
         if (why.empty() && (it & 255) == 255) {
-            for (size_t i = 0; i < g->comms.size() && why.empty(); ++i) {
-                ncclResult_t ae = ncclSuccess;
-                if (g->comms[i] && ncclCommGetAsyncError(g->comms[i], &ae) == ncclSuccess && ae != ncclSuccess &&
-                    ae != ncclInProgress)
-                    why = std::string("RCCL asynchronous error: ") + ncclGetErrorString(ae);
+            // the communicators are polled under g->mu: another thread's abort (holding it) frees
+            // them; a caller without the lock skips the poll while someone else holds it
+            std::unique_lock<std::mutex> gl(g->mu, std::defer_lock);
+            if (locked || gl.try_lock()) {
+                if (g->broken.load(std::memory_order_acquire)) why = "the device group was aborted (" + g->broken_msg + ")";
+                for (size_t i = 0; i < g->comms.size() && why.empty(); ++i) {
+                    ncclResult_t ae = ncclSuccess;
+                    if (g->comms[i] && ncclCommGetAsyncError(g->comms[i], &ae) == ncclSuccess && ae != ncclSuccess &&
+                        ae != ncclInProgress)
+                        why = std::string("RCCL asynchronous error: ") + ncclGetErrorString(ae);
+                }
             }
             if (why.empty() && at_exchange && clk::now() - t_reached > std::chrono::milliseconds(timeout_ms))
                 why = "the exchange did not complete within " + std::to_string(timeout_ms) +
@@ -331,6 +347,168 @@ int group_wait(iris_group *g, const std::vector<hipEvent_t> &reached, const std:
         else
             std::this_thread::sleep_for(std::chrono::microseconds(20));
     }
+}
+
+// Waits until every communicator of g is ready -- a non-blocking init, or the launch of a group
+// whose ncclGroupEnd returned ncclInProgress -- at most `ms`; fails with the first asynchronous
+// error or on expiry (the caller aborts).
+int comms_ready(iris_group *g, uint32_t ms, const std::string &what) {
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    for (;;) {
+        bool all = true;
+        for (size_t i = 0; i < g->comms.size(); ++i) {
+            if (!g->comms[i]) continue;
+            ncclResult_t st = ncclSuccess;
+            const ncclResult_t r = ncclCommGetAsyncError(g->comms[i], &st);
+            if (r != ncclSuccess) return fail(IRIS_E_HIP, what + ": ncclCommGetAsyncError: " + ncclGetErrorString(r));
+            if (st == ncclInProgress)
+                all = false;
+            else if (st != ncclSuccess)
+                return fail(IRIS_E_HIP, what + ": " + ncclGetErrorString(st) + " (" + ncclGetLastError(g->comms[i]) + ")");
+        }
+        if (all) return 0;
+        const auto dt = clk::now() - t0;
+        if (dt > std::chrono::milliseconds(ms))
+            return fail(IRIS_E_HIP, what + " did not complete within " + std::to_string(ms) +
+                                        " ms (a peer rank failed, never started, or is unreachable)");
+        if (dt < std::chrono::milliseconds(2))
+            __builtin_ia32_pause();
+        else
+            std::this_thread::sleep_for(std::chrono::microseconds(100));
+    }
+}
+
+// The bound of forming a group: IRIS_GROUP_TIMEOUT_MS / iris_group_set_timeout's knob, else 120 s
+// (eight ranks' bootstrap and topology discovery take seconds).
+uint32_t init_timeout(const iris_group *g) {
+    const uint32_t h = g->devs.empty() ? 0 : g->devs[0]->hooks.group_timeout_ms;
+    return h ? h : 120000;
+}
+
+// Creates the communicators of the local devices as RCCL ranks rank0 + i of nranks, non-blocking,
+// and waits (bounded) until every one is ready; on failure aborts whatever was created.
+int comm_init(iris_group *g, const ncclUniqueId &u) {
+    const size_t L = g->devs.size();
+    g->comms.assign(L, nullptr);
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    ncclResult_t r = ncclGroupStart();
+    for (size_t i = 0; r == ncclSuccess && i < L; ++i) {
+        if (hipSetDevice(g->devs[i]->ordinal) != hipSuccess) {
+            r = ncclInvalidArgument;
+            break;
+        }
+        r = ncclCommInitRankConfig(&g->comms[i], (int)g->ranks, u, (int)(g->rank0 + i), &cfg);
+        if (r == ncclInProgress) r = ncclSuccess;
+    }
+    ncclResult_t r2 = ncclGroupEnd();
+    if (r2 == ncclInProgress) r2 = ncclSuccess;
+    int rc = 0;
+    if (r != ncclSuccess || r2 != ncclSuccess)
+        rc = fail(IRIS_E_HIP, std::string("ncclCommInitRankConfig: ") + ncclGetErrorString(r != ncclSuccess ? r : r2));
+    else
+        rc = comms_ready(g, init_timeout(g), "RCCL communicator init (" + std::to_string(g->ranks) + " ranks)");
+    if (rc != 0) {
+        const std::string m = g_err;
+        for (size_t i = 0; i < L; ++i)
+            if (g->comms[i]) {
+                (void)hipSetDevice(g->devs[i]->ordinal);
+                (void)ncclCommAbort(g->comms[i]);
+            }
+        g->comms.assign(L, nullptr);
+        return fail(rc, m);
+    }
+    return 0;
+}
+
+// ncclGroupEnd of an exchange: ncclInProgress (non-blocking communicators) waits, bounded, for the
+// group's launch, so that work enqueued after it on the streams follows the all-gather.
+ncclResult_t group_end_launched(iris_group *g, uint32_t ms, int *rc) {
+    const ncclResult_t r = ncclGroupEnd();
+    if (r == ncclInProgress) {
+        *rc = comms_ready(g, ms, "RCCL all-gather launch");
+        return *rc == 0 ? ncclSuccess : ncclInternalError;
+    }
+    return r;
+}
+
+// What RCCL's ranks are: ncclCommCount of the new communicators, and every rank's device PCI bus
+// id over the group's own all-gather (bounded like a search's exchange).
+int gather_bus_ids(iris_group *g) {
+    const size_t L = g->devs.size();
+    constexpr size_t B = IRIS_GROUP_BUS_ID_BYTES;
+    for (size_t i = 0; i < L; ++i) {
+        int count = 0;
+        NCCLCHK(ncclCommCount(g->comms[i], &count));
+        if (i == 0) g->comm_count = (uint32_t)count;
+        if ((uint32_t)count != g->comm_count || g->comm_count != g->ranks)
+            return fail(IRIS_E_HIP, "RCCL communicator holds " + std::to_string(count) + " ranks, the group " +
+                                        std::to_string(g->ranks));
+    }
+    struct Bufs {
+        std::vector<void *> p;
+        ~Bufs() {
+            for (void *q : p)
+                if (q) (void)hipFree(q);
+        }
+    } bufs;
+    std::vector<void *> send(L, nullptr), recv(L, nullptr);
+    std::vector<hipEvent_t> reached(L, nullptr), done(L, nullptr);
+    auto give_events = [&] {
+        for (size_t i = 0; i < L; ++i) {
+            if (reached[i]) g->devs[i]->event_pool.push_back(reached[i]);
+            if (done[i]) g->devs[i]->event_pool.push_back(done[i]);
+        }
+    };
+    int rc = 0;
+    for (size_t i = 0; i < L && rc == 0; ++i) {
+        iris_device *d = g->devs[i];
+        rc = set_device(d);
+        char bus[B] = {0};
+        if (rc == 0 && hipDeviceGetPCIBusId(bus, (int)B - 1, d->ordinal) != hipSuccess) rc = fail(IRIS_E_HIP, "hipDeviceGetPCIBusId");
+        if (rc == 0 && (hipMalloc(&send[i], B) != hipSuccess || hipMalloc(&recv[i], B * g->ranks) != hipSuccess))
+            rc = fail(IRIS_E_NOMEM, "hipMalloc bus id buffers");
+        bufs.p.push_back(send[i]);
+        bufs.p.push_back(recv[i]);
+        if (rc == 0 && hipMemcpyAsync(send[i], bus, B, hipMemcpyHostToDevice, d->aux) != hipSuccess) rc = fail(IRIS_E_HIP, "hipMemcpyAsync");
+        if (rc == 0 && hipStreamSynchronize(d->aux) != hipSuccess) rc = fail(IRIS_E_HIP, "hipStreamSynchronize");
+        if (rc == 0 && !((reached[i] = take_event(d)) && (done[i] = take_event(d)))) rc = fail(IRIS_E_HIP, "hipEventCreate failed");
+        if (rc == 0 && hipEventRecord(reached[i], d->aux) != hipSuccess) rc = fail(IRIS_E_HIP, "hipEventRecord");
+    }
+    if (rc != 0) {
+        give_events();
+        return rc;
+    }
+    ncclResult_t r = ncclGroupStart();
+    for (size_t i = 0; r == ncclSuccess && i < L; ++i) {
+        r = ncclAllGather(send[i], recv[i], B, ncclUint8, g->comms[i], g->devs[i]->aux);
+        if (r == ncclInProgress) r = ncclSuccess;
+    }
+    const ncclResult_t r2 = group_end_launched(g, init_timeout(g), &rc);
+    if (rc == 0 && r == ncclSuccess) r = r2;
+    if (rc == 0 && r != ncclSuccess) rc = fail(IRIS_E_HIP, std::string("ncclAllGather (bus ids): ") + ncclGetErrorString(r));
+    for (size_t i = 0; i < L && rc == 0; ++i) {
+        (void)hipSetDevice(g->devs[i]->ordinal);
+        if (hipEventRecord(done[i], g->devs[i]->aux) != hipSuccess) rc = fail(IRIS_E_HIP, "hipEventRecord");
+    }
+    bool drained = true;
+    if (rc != 0) {
+        const std::string m = g_err;
+        drained = group_abort(g, "bus id exchange: " + m);
+        rc = fail(rc, m);
+    } else {
+        rc = group_wait(g, reached, done, init_timeout(g), false, &drained);
+    }
+    if (rc == 0) {
+        std::vector<char> all(B * g->ranks);
+        (void)hipSetDevice(g->devs[0]->ordinal);
+        if (hipMemcpy(all.data(), recv[0], all.size(), hipMemcpyDeviceToHost) != hipSuccess) rc = fail(IRIS_E_HIP, "hipMemcpy bus ids");
+        for (uint32_t k = 0; rc == 0 && k < g->ranks; ++k) g->bus_ids.emplace_back(all.data() + k * B, strnlen(all.data() + k * B, B));
+    }
+    if (!drained) bufs.p.clear();  // aborted work may still write them: leaked rather than freed
+    else give_events();
+    return rc;
 }
 
 bool same_partial(const Partial &a, const Partial &b) {
@@ -389,14 +567,12 @@ int iris_group_create(const int *ordinals, uint32_t n, iris_group_t **out) {
     g->ranks = n;
     g->rank0 = 0;
     int rc = open_devices(g, ordinals, n);
-    if (rc == 0) {
-        g->comms.assign(n, nullptr);
-        const ncclResult_t r = ncclCommInitAll(g->comms.data(), (int)n, ordinals);
-        if (r != ncclSuccess) {
-            g->comms.assign(n, nullptr);
-            rc = fail(IRIS_E_HIP, std::string("ncclCommInitAll: ") + ncclGetErrorString(r));
-        }
+    if (rc == 0) {  // ncclCommInitAll's form: one id, every local device a rank, in one RCCL group
+        ncclUniqueId u;
+        const ncclResult_t r = ncclGetUniqueId(&u);
+        rc = r == ncclSuccess ? comm_init(g, u) : fail(IRIS_E_HIP, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
     }
+    if (rc == 0) rc = gather_bus_ids(g);
     if (rc != 0) {
         const std::string m = g_err;
         group_teardown(g);
@@ -419,13 +595,9 @@ int iris_group_create_rank(int ordinal, uint32_t nranks, uint32_t rank, const ui
     if (rc == 0) {
         ncclUniqueId u;
         memcpy(&u, id, sizeof(u));
-        g->comms.assign(1, nullptr);
-        const ncclResult_t r = ncclCommInitRank(&g->comms[0], (int)nranks, u, (int)rank);
-        if (r != ncclSuccess) {
-            g->comms[0] = nullptr;
-            rc = fail(IRIS_E_HIP, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
-        }
+        rc = comm_init(g, u);
     }
+    if (rc == 0) rc = gather_bus_ids(g);
     if (rc != 0) {
         const std::string m = g_err;
         group_teardown(g);
@@ -447,6 +619,19 @@ int iris_group_info(const iris_group_t *g, uint32_t *local_devices, uint32_t *ra
     if (local_devices) *local_devices = (uint32_t)g->devs.size();
     if (ranks) *ranks = g->ranks;
     if (first_rank) *first_rank = g->rank0;
+    return 0;
+}
+
+int iris_group_rccl_info(const iris_group_t *g, uint32_t *comm_ranks, char *bus_ids, size_t len) {
+    ARG(g, "NULL argument");
+    if (comm_ranks) *comm_ranks = g->comm_count;
+    if (bus_ids) {
+        ARG(len >= (size_t)g->ranks * IRIS_GROUP_BUS_ID_BYTES, "bus_ids needs ranks * IRIS_GROUP_BUS_ID_BYTES bytes");
+        memset(bus_ids, 0, (size_t)g->ranks * IRIS_GROUP_BUS_ID_BYTES);
+        for (size_t r = 0; r < g->bus_ids.size() && r < g->ranks; ++r)
+            memcpy(bus_ids + r * IRIS_GROUP_BUS_ID_BYTES, g->bus_ids[r].c_str(),
+                   std::min(g->bus_ids[r].size(), (size_t)IRIS_GROUP_BUS_ID_BYTES - 1));
+    }
     return 0;
 }
 
@@ -708,10 +893,14 @@ int iris_group_template_search_async(iris_group_db_t *gdb, const iris_template_t
     // the exchange: every device's shard winners to every device (side streams, in order after the reduces)
     {
         ncclResult_t r = ncclGroupStart();
-        for (size_t i = 0; r == ncclSuccess && i < L; ++i)
+        for (size_t i = 0; r == ncclSuccess && i < L; ++i) {
             r = ncclAllGather((Partial *)gdb->send[i].p + (size_t)b * gdb->spd, gdb->recv[i].p,
                               (size_t)gdb->spd * sizeof(Partial), ncclUint8, g->comms[i], g->devs[i]->aux);
-        const ncclResult_t r2 = ncclGroupEnd();
+            if (r == ncclInProgress) r = ncclSuccess;
+        }
+        int lrc = 0;
+        const ncclResult_t r2 = group_end_launched(g, p->timeout_ms, &lrc);
+        if (lrc != 0) return abandon(lrc, true);
         if (r == ncclSuccess) r = r2;
         if (r != ncclSuccess) return abandon(fail(IRIS_E_HIP, std::string("ncclAllGather: ") + ncclGetErrorString(r)), true);
     }
@@ -851,12 +1040,14 @@ int iris_group_template_batch_search(iris_group_db_t *gdb, const iris_template_t
     if (rc == 0) {
         gather_started = true;
         ncclResult_t r = ncclGroupStart();
-        for (size_t i = 0; r == ncclSuccess && i < L; ++i)
+        for (size_t i = 0; r == ncclSuccess && i < L; ++i) {
             r = ncclAllGather(send[i].p, recv[i].p, (size_t)spd * stride * sizeof(Partial), ncclUint8, g->comms[i],
                               g->devs[i]->stream);
-        const ncclResult_t r2 = ncclGroupEnd();
+            if (r == ncclInProgress) r = ncclSuccess;
+        }
+        const ncclResult_t r2 = group_end_launched(g, group_timeout(g, gdb->max_count, nq), &rc);
         if (r == ncclSuccess) r = r2;
-        if (r != ncclSuccess) rc = fail(IRIS_E_HIP, std::string("ncclAllGather: ") + ncclGetErrorString(r));
+        if (rc == 0 && r != ncclSuccess) rc = fail(IRIS_E_HIP, std::string("ncclAllGather: ") + ncclGetErrorString(r));
     }
     for (size_t i = 0; i < L && rc == 0; ++i) {
         iris_device *d = g->devs[i];

@@ -151,6 +151,7 @@ def load_library(path=None):
             "iris_group_info": ([P, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32),
                                  ctypes.POINTER(ctypes.c_uint32)], ctypes.c_int),
             "iris_group_device": ([P, ctypes.c_uint32, PP], ctypes.c_int),
+            "iris_group_rccl_info": ([P, ctypes.POINTER(ctypes.c_uint32), ctypes.c_char_p, ctypes.c_size_t], ctypes.c_int),
             "iris_group_db_create": ([P, ctypes.c_int, u64, ctypes.c_int, ctypes.c_uint32, PP], ctypes.c_int),
             "iris_group_db_destroy": ([P], ctypes.c_int),
             "iris_group_db_info": ([P, ctypes.POINTER(u64), ctypes.POINTER(ctypes.c_uint32),
@@ -194,7 +195,7 @@ def exported_symbols():
         "iris_template_search_async", "iris_pending_wait",
         "iris_db_attach_host", "iris_db_detach_host",
         "iris_group_create", "iris_group_unique_id", "iris_group_create_rank", "iris_group_destroy", "iris_group_set_timeout", "iris_group_info",
-        "iris_group_device", "iris_group_db_create", "iris_group_db_destroy", "iris_group_db_info",
+        "iris_group_device", "iris_group_rccl_info", "iris_group_db_create", "iris_group_db_destroy", "iris_group_db_info",
         "iris_group_db_shard", "iris_group_db_generate", "iris_group_db_write", "iris_group_db_read",
         "iris_group_db_load_file", "iris_group_template_search", "iris_group_template_search_async",
         "iris_group_pending_wait", "iris_group_template_batch_search",
@@ -944,6 +945,12 @@ class Group:
         l, r, f = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
         _check(load_library().iris_group_info(self.handle, ctypes.byref(l), ctypes.byref(r), ctypes.byref(f)))
         self.local_devices, self.ranks, self.first_rank = l.value, r.value, f.value
+        # what RCCL reports: its communicators' rank count and every rank's device PCI bus id
+        cr = ctypes.c_uint32()
+        ids = ctypes.create_string_buffer(32 * self.ranks)
+        _check(load_library().iris_group_rccl_info(self.handle, ctypes.byref(cr), ids, len(ids)))
+        self.rccl_nranks = cr.value
+        self.rccl_devices = [ids.raw[32 * k:32 * (k + 1)].split(b"\0", 1)[0].decode() for k in range(self.ranks)]
         self.devices = []
         for i in range(self.local_devices):
             d = ctypes.c_void_p()

@@ -4,6 +4,7 @@ the default RCCL path on one rank (library communicator via ncclCommInitRank, gl
 rendezvous) and the single-process library device group (--single-process).  Each run plants a
 known answer (in a later rank's shard when there are several) that must be found."""
 import json
+import re
 import os
 import pathlib
 import socket
@@ -120,3 +121,6 @@ def test_bench_rccl_single_rank():
         d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
         assert d["n_gpus"] == 1 and d["check"]["ok"] and d["ranks_seen"] == 1
         assert "ncclCommInitRank" in d["backend"] and "RCCL" in d["config"]["exchange"]
+        # what the library's communicator saw: one rank, on this box's GPU (its PCI bus id)
+        assert d["rccl_nranks"] == 1 and len(d["rccl_devices"]) == 1
+        assert re.fullmatch(r"[0-9a-fA-F]{4}:[0-9a-fA-F]{2}:[0-9a-fA-F]{2}\.[0-9a-fA-F]", d["rccl_devices"][0])

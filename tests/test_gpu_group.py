@@ -233,8 +233,8 @@ def test_group_rejects_duplicate_device_and_bad_args():
 
 
 def test_group_single_rank_communicator():
-    """The multi-process form (ncclCommInitRank) with one rank: what each torchrun rank of
-    bench.py builds."""
+    """The multi-process form (non-blocking ncclCommInitRankConfig) with one rank: what each
+    torchrun rank of bench.py builds; RCCL itself reports one rank on this GPU."""
     uid = ih.Group.unique_id()
     assert len(uid) == 128
     n = 3000
@@ -243,10 +243,41 @@ def test_group_single_rank_communicator():
     query[5] ^= np.uint64(0xFF)
     with ih.Group.rank(0, 1, 0, uid) as g:
         assert (g.local_devices, g.ranks, g.first_rank) == (1, 1, 0)
+        assert g.rccl_nranks == 1 and len(g.rccl_devices) == 1 and ":" in g.rccl_devices[0]
         with ih.GroupDatabase(g, ih.KIND_TEMPLATES, n, shards_per_device=2) as gdb:
             gdb.generate(SEED)
             best, idx = oracle_best(query, ref)
             assert same(gdb.search(query), best, idx) and idx == 1234
+
+
+def test_group_missing_peer_fails_within_bound(monkeypatch, device):
+    """A 2-rank group whose second rank never comes: forming it must fail within the bound
+    (IRIS_GROUP_TIMEOUT_MS, read when the group's device opens) instead of hanging in RCCL's
+    init, and the GPU then opens, forms a 1-rank group and searches normally."""
+    import time
+
+    uid = ih.Group.unique_id()
+    bound_ms = 6000
+    with monkeypatch.context() as m:
+        m.setenv("IRIS_GROUP_TIMEOUT_MS", str(bound_ms))
+        t0 = time.monotonic()
+        with pytest.raises(ih.IrisError) as ex:
+            ih.Group.rank(0, 2, 0, uid)
+        dt = time.monotonic() - t0
+    assert dt < bound_ms / 1e3 + 20, dt
+    assert "did not complete" in str(ex.value) or "RCCL" in str(ex.value), ex.value
+    n = 2000
+    ref = oc.gen_templates(SEED + 3, 0, n)
+    query = ref[777].copy()
+    best, idx = oracle_best(query, ref)
+    with ih.Database(device, ih.KIND_TEMPLATES, n) as db:
+        db.append(ref)
+        with ih.TemplateEngine(device, query) as eng:
+            assert same(eng.search(db), best, idx)
+    with ih.Group.rank(0, 1, 0, ih.Group.unique_id()) as g:
+        with ih.GroupDatabase(g, ih.KIND_TEMPLATES, n) as gdb:
+            gdb.write(0, ref)
+            assert same(gdb.search(query), best, idx)
 
 
 @pytest.mark.parametrize("side", ["plain", "delayed"])
