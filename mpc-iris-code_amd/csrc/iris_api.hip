@@ -71,8 +71,8 @@ int iris_api::db_write_pinned(iris_db *db, uint64_t index, const void *records, 
     const size_t piece = std::min(kUploadSlot, std::max(kUploadPieceMin, (size_t)n * k.rec_bytes / 4));
     const uint64_t ch = std::max<uint64_t>(64, piece / k.rec_bytes / 64 * 64);
     const size_t slot = (size_t)ch * k.rec_bytes;
+    CHK(ensure_upin(d));  // host first: an IRIS_E_NOMEM with the slots in place is the device's
     CHK(ensure(d->staging, kUploadSlots * slot));
-    CHK(ensure_upin(d));
     int rc = 0;
     uint64_t c = 0;
     for (uint64_t done = 0; done < n && rc == 0; done += ch, ++c) {
@@ -131,7 +131,9 @@ int iris_api::db_store_locked(iris_db *db, uint64_t index, const void *records, 
         const int path = u.pick();
         const auto t0 = std::chrono::steady_clock::now();
         int rc = path == 0 ? db_write_pinned(db, index, records, n) : db_write_runtime(db, index, records, n);
-        if (rc == IRIS_E_NOMEM && path == 0) {  // no pinned host memory for the slots: the runtime's copy from now on
+        if (rc == IRIS_E_NOMEM && path == 0 && d->upin_cap < kUploadSlot) {
+            // no pinned host memory for the slots: the runtime's copy from now on (a device
+            // allocation failure is the caller's error and leaves the tuner as it was)
             u.no_pinned = true;
             return db_write_runtime(db, index, records, n);
         }

@@ -64,12 +64,18 @@ def test_capacity_checked(device, tmp_path):
         assert db.load_file(path, count=cap) == cap
 
 
-@pytest.fixture(params=["mmap", "pread"])
+@pytest.fixture(params=["slots", "windows", "pread"])
 def load_device(request, device, hooked_device):
-    """The loader's two paths: DMA from the registered page-cache mapping (default)
-    and pread into pinned buffers (the fallback: a device opened with the IRIS_LOAD_PREAD
-    test hook)."""
-    return hooked_device(IRIS_LOAD_PREAD="1") if request.param == "pread" else device
+    """The loader's three paths: reader threads pread into the two pinned upload slots (the
+    default for a load with no other in flight), DMA from registered page-cache windows of the
+    mapping (a concurrent per-device load in a group; forced by the IRIS_LOAD_WINDOWS test
+    hook), and pread into the loader's own pinned buffers (the fallback when the pages cannot
+    be registered; forced by IRIS_LOAD_PREAD)."""
+    if request.param == "pread":
+        return hooked_device(IRIS_LOAD_PREAD="1")
+    if request.param == "windows":
+        return hooked_device(IRIS_LOAD_WINDOWS="1")
+    return device
 
 
 def test_multi_chunk_unaligned_templates(load_device, tmp_path):
