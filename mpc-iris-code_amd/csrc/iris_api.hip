@@ -629,11 +629,19 @@ int iris_config(const iris_device_t *d, char *buf, size_t len, size_t *needed) {
         snprintf(r, sizeof(r), " upload_gbps=%.1f/%.1f", d->upload_tune.gbps[0] / 1e9, d->upload_tune.gbps[1] / 1e9);
         s += r;
         uint64_t rc = 0, rbytes = 0;
+        int via_fd = 0;
+        std::string skip;
         {
             std::lock_guard<std::recursive_mutex> g(const_cast<iris_device *>(d)->mu);
-            resident_stats(d, &rc, &rbytes);
+            resident_stats(d, &rc, &rbytes, &via_fd);
+            skip = d->resident_skip;
         }
-        s += " resident=" + std::to_string(rc) + "/" + std::to_string(rbytes);
+        s += " resident=" + std::to_string(rc) + "/" + std::to_string(rbytes) + " resident_via_fd=" + std::to_string(via_fd);
+        if (!skip.empty()) {  // one token: spaces and '=' replaced
+            for (char &c : skip)
+                if (c == ' ' || c == '=') c = '_';
+            s += " resident_skip=" + skip;
+        }
     }
     if (buf && len) {
         const size_t n = std::min(len - 1, s.size());

@@ -144,6 +144,7 @@ struct iris_device {
     std::vector<struct Resident *> resident;
     std::vector<std::pair<uintptr_t, uintptr_t>> not_resident;
     uint64_t resident_clock = 0;
+    std::string resident_skip;  // why the last mapping refused was not made resident (iris_config)
 };
 
 struct iris_db {
@@ -421,7 +422,9 @@ int db_store_locked(iris_db *db, uint64_t index, const void *records, uint64_t n
 int resident_slice(iris_device *d, int kind, const void *ptr, uint64_t n, iris_db **db, uint64_t *first,
                    uint64_t *end);
 void resident_drop_all(iris_device *d);  // frees every resident copy (waits for the device's streams)
-void resident_stats(const iris_device *d, uint64_t *count, uint64_t *bytes);
+// count and device bytes of the resident copies, and how many check their file through a held
+// descriptor (map_files unreadable)
+void resident_stats(const iris_device *d, uint64_t *count, uint64_t *bytes, int *via_fd);
 // Partial (indices offset by base) -> iris_match_t; +inf / UINT64_MAX when none
 void match_from(const iris::Partial &r, bool any, uint64_t base, iris_match_t *out);
 

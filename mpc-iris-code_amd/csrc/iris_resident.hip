@@ -15,19 +15,25 @@
 // the file behind exactly that mapping: a mapping that went away or was replaced fails or shows
 // another inode; ~2.5 us), plus a probe of three records of the slice against 64-byte snapshots
 // taken when their granule was uploaded (a write the timestamps miss: their granularity is the
-// kernel's tick).  A changed file drops its copy; the call then starts over.
+// kernel's tick).  A changed file drops its copy; the call then starts over.  Where map_files
+// cannot be read (it needs ptrace-read access to the process, which some sandboxes withhold) the
+// copy holds the mapped file open (checked to be the mapping's inode) and fstats that instead,
+// and re-reads the mapping's line of /proc/self/maps at most every 50 ms to notice a remap.
 //
 // Not made resident: anonymous or writable memory, private mappings, files larger than the
 // device's free memory (less a reserve; older copies are evicted first, least recently used),
 // IRIS_AUTO_RESIDENT=0.  Those slices keep the upload path.  A device allocation that fails
 // (iris_db_create) drops every resident copy and retries.
 #include <errno.h>
+#include <fcntl.h>
 #include <stdio.h>
+#include <sys/sysmacros.h>
 #include <string.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
 #include <string>
 #include <vector>
 
@@ -51,6 +57,10 @@ struct Resident {
     uintptr_t base = 0;        // address of record 0 (the first whole record of the slices seen)
     uint64_t nrec = 0;
     std::string link;          // /proc/self/map_files/<lo>-<hi>
+    int fd = -1;               // >= 0: map_files unreadable; the mapped file, held open
+    uint64_t inode = 0;        // of the mapping (/proc/self/maps)
+    std::string path;
+    std::chrono::steady_clock::time_point vma_checked;
     struct stat st {};
     iris_db *db = nullptr;
     size_t dev_bytes = 0;
@@ -74,6 +84,7 @@ void free_copy(iris_device *d, Resident *r) {
         if (r->db->data) (void)hipFree(r->db->data);
         delete r->db;
     }
+    if (r->fd >= 0) ::close(r->fd);
     delete r;
 }
 
@@ -83,9 +94,10 @@ void drop(iris_device *d, Resident *r) {
     free_copy(d, r);
 }
 
-void remember_not_resident(iris_device *d, uintptr_t lo, uintptr_t hi) {
+void remember_not_resident(iris_device *d, uintptr_t lo, uintptr_t hi, const std::string &why) {
     if (d->not_resident.size() >= kNotResidentMax) d->not_resident.clear();
     d->not_resident.emplace_back(lo, hi);
+    d->resident_skip = why;
 }
 
 // The mapping of /proc/self/maps that holds address p.
@@ -94,6 +106,7 @@ struct Vma {
     char perms[8] = {0};
     uint64_t off = 0;
     uint64_t inode = 0;
+    unsigned int maj = 0, mnr = 0;
     std::string path;
 };
 
@@ -114,6 +127,8 @@ bool find_vma(uintptr_t p, Vma *out) {
         memcpy(out->perms, perms, sizeof(perms));
         out->off = off;
         out->inode = ino;
+        out->maj = maj;
+        out->mnr = mnr;
         std::string path = line + pos;
         while (!path.empty() && (path.back() == '\n' || path.back() == ' ')) path.pop_back();
         out->path = path;
@@ -124,60 +139,110 @@ bool find_vma(uintptr_t p, Vma *out) {
     return found;
 }
 
+// The mapped file's stat: through map_files, or (where that is unreadable) the held descriptor.
+bool file_stat(const Resident *r, struct stat *st) {
+    return r->fd >= 0 ? fstat(r->fd, st) == 0 : stat(r->link.c_str(), st) == 0;
+}
+
+// Whether the mapping is still the one the copy was made of.  map_files answers that with every
+// stat; the descriptor form re-reads /proc/self/maps at most every 50 ms (now = always).
+bool vma_same(Resident *r, bool now) {
+    if (r->fd < 0) return true;
+    const auto t = std::chrono::steady_clock::now();
+    if (!now && t - r->vma_checked < std::chrono::milliseconds(50)) return true;
+    Vma v;
+    if (!find_vma(r->lo, &v) || v.lo != r->lo || v.hi != r->hi || v.inode != r->inode || v.path != r->path ||
+        v.perms[1] != '-')
+        return false;
+    r->vma_checked = t;
+    return true;
+}
+
 // A new resident copy of the file mapping that holds the slice [p, p + n records), or nullptr
 // (not eligible: remembered as such).  Errors are not reported: the caller uploads instead.
 Resident *make_resident(iris_device *d, int kind, uintptr_t p, uint64_t n) {
     const KindInfo k = kind_info(kind, IRIS_LAYOUT_TILES);
     const size_t rb = k.rec_bytes;
     Vma v;
-    if (!find_vma(p, &v)) return nullptr;
-    auto ineligible = [&]() -> Resident * {
-        remember_not_resident(d, v.lo, v.hi);
+    if (!find_vma(p, &v)) {
+        d->resident_skip = "no mapping holds the slice";
+        return nullptr;
+    }
+    auto ineligible = [&](const std::string &why) -> Resident * {
+        remember_not_resident(d, v.lo, v.hi, why);
         return nullptr;
     };
     // read-only (not writable), shared, backed by a named file
-    if (v.perms[0] != 'r' || v.perms[1] != '-' || v.perms[3] != 's' || v.inode == 0 || v.path.empty() ||
-        v.path[0] != '/' || v.path.find(" (deleted)") != std::string::npos)
-        return ineligible();
+    if (v.perms[0] != 'r' || v.perms[1] != '-' || v.perms[3] != 's')
+        return ineligible(std::string("mapping is not read-only shared (") + v.perms + ")");
+    if (v.inode == 0 || v.path.empty() || v.path[0] != '/' || v.path.find(" (deleted)") != std::string::npos)
+        return ineligible("mapping is not backed by a named file");
     char link[96];
     snprintf(link, sizeof(link), "/proc/self/map_files/%lx-%lx", (unsigned long)v.lo, (unsigned long)v.hi);
     struct stat st;
-    if (stat(link, &st) != 0 || !S_ISREG(st.st_mode) || (uint64_t)st.st_ino != v.inode) return ineligible();
-    if ((uint64_t)st.st_size <= v.off) return ineligible();
+    int fd = -1;
+    if (stat(link, &st) != 0) {
+        // map_files unreadable here: the mapped file by its path, if it is the mapping's inode
+        const int err = errno;
+        fd = ::open(v.path.c_str(), O_RDONLY | O_CLOEXEC);
+        if (fd < 0 || fstat(fd, &st) != 0 || (uint64_t)st.st_ino != v.inode ||
+            st.st_dev != makedev(v.maj, v.mnr)) {
+            if (fd >= 0) ::close(fd);
+            return ineligible(std::string("map_files: ") + strerror(err) + "; the path is not the mapped file");
+        }
+    }
+    if (!S_ISREG(st.st_mode) || (uint64_t)st.st_ino != v.inode) {
+        if (fd >= 0) ::close(fd);
+        return ineligible("mapping is not a regular file");
+    }
+    if ((uint64_t)st.st_size <= v.off) {
+        if (fd >= 0) ::close(fd);
+        return ineligible("mapping lies past the end of its file");
+    }
     const uintptr_t data_end = v.lo + std::min<uint64_t>(v.hi - v.lo, (uint64_t)st.st_size - v.off);
     const uintptr_t base = v.lo + (p - v.lo) % rb;
-    if (data_end < base + rb) return ineligible();
+    auto refuse = [&](const std::string &why) -> Resident * {
+        if (fd >= 0) ::close(fd);
+        return ineligible(why);
+    };
+    if (data_end < base + rb) return refuse("mapping holds no whole record");
     const uint64_t nrec = (data_end - base) / rb;
-    if ((p - base) / rb + n > nrec) return nullptr;  // the slice runs past the file's records
+    if ((p - base) / rb + n > nrec) {  // the slice runs past the file's records
+        if (fd >= 0) ::close(fd);
+        return nullptr;
+    }
     const uint64_t blocks = (nrec + k.block - 1) / k.block;
     const size_t dev_bytes = (size_t)blocks * block_bytes(k);
     // copies of mappings that are gone (unmapped, or their file replaced) free their memory first
     for (size_t i = d->resident.size(); i-- > 0;) {
         Resident *o = d->resident[i];
         struct stat ost;
-        if (stat(o->link.c_str(), &ost) != 0 || ost.st_ino != o->st.st_ino || ost.st_dev != o->st.st_dev) drop(d, o);
+        if (!file_stat(o, &ost) || ost.st_ino != o->st.st_ino || ost.st_dev != o->st.st_dev || !vma_same(o, true))
+            drop(d, o);
     }
     // room: the device's free memory less a reserve, after evicting older copies if need be
     size_t free_b = 0, total_b = 0;
-    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return ineligible();
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return refuse("hipMemGetInfo failed");
     const size_t reserve = std::max<size_t>(2ull << 30, total_b / 32);
     size_t evictable = 0;
     for (Resident *r : d->resident) evictable += r->dev_bytes;
-    if (dev_bytes + reserve > free_b + evictable) return ineligible();
+    if (dev_bytes + reserve > free_b + evictable)
+        return refuse("the file (" + std::to_string(dev_bytes >> 20) + " MB on the device) does not fit the free memory");
     while (dev_bytes + reserve > free_b && !d->resident.empty()) {
         auto lru = std::min_element(d->resident.begin(), d->resident.end(),
                                     [](const Resident *a, const Resident *b) { return a->last_use < b->last_use; });
         drop(d, *lru);
-        if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return nullptr;
+        if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return refuse("hipMemGetInfo failed");
     }
     Resident *r = new (std::nothrow) Resident();
-    if (!r) return nullptr;
+    if (!r) return refuse("out of host memory");
+    r->fd = fd;  // owned by r from here
     r->db = new (std::nothrow) iris_db();
     if (!r->db || hipMalloc(&r->db->data, dev_bytes) != hipSuccess) {
         (void)hipGetLastError();
         if (r->db) r->db->data = nullptr;
         free_copy(d, r);
-        return ineligible();
+        return ineligible("hipMalloc of the copy failed");
     }
     // zeroed: the last block's padding records are never candidates
     if (hipMemsetAsync(r->db->data, 0, dev_bytes, d->stream) != hipSuccess) {
@@ -195,6 +260,9 @@ Resident *make_resident(iris_device *d, int kind, uintptr_t p, uint64_t n) {
     r->base = base;
     r->nrec = nrec;
     r->link = link;
+    r->inode = v.inode;
+    r->path = v.path;
+    r->vma_checked = std::chrono::steady_clock::now();
     r->st = st;
     r->dev_bytes = dev_bytes;
     r->gran = std::max<uint64_t>(64, kGranuleBytes / rb / 64 * 64);
@@ -254,9 +322,9 @@ int iris_api::resident_slice(iris_device *d, int kind, const void *ptr, uint64_t
         // whole records of this copy's record grid, inside the file's records
         if (p < r->base || (p - r->base) % rb != 0 || (p - r->base) / rb + n > r->nrec) return 0;
         struct stat st;
-        if (stat(r->link.c_str(), &st) != 0 || st.st_dev != r->st.st_dev || st.st_ino != r->st.st_ino ||
+        if (!file_stat(r, &st) || st.st_dev != r->st.st_dev || st.st_ino != r->st.st_ino ||
             st.st_size != r->st.st_size || !same_time(st.st_mtim, r->st.st_mtim) ||
-            !same_time(st.st_ctim, r->st.st_ctim)) {
+            !same_time(st.st_ctim, r->st.st_ctim) || !vma_same(r, false)) {
             drop(d, r);  // the mapping went away or its file changed: start over
             continue;
         }
@@ -282,10 +350,14 @@ void iris_api::resident_drop_all(iris_device *d) {
     d->not_resident.clear();
 }
 
-void iris_api::resident_stats(const iris_device *d, uint64_t *count, uint64_t *bytes) {
+void iris_api::resident_stats(const iris_device *d, uint64_t *count, uint64_t *bytes, int *via_fd) {
     *count = d->resident.size();
     *bytes = 0;
-    for (const Resident *r : d->resident) *bytes += r->dev_bytes;
+    *via_fd = 0;
+    for (const Resident *r : d->resident) {
+        *bytes += r->dev_bytes;
+        *via_fd += r->fd >= 0;
+    }
 }
 
 extern "C" int iris_device_drop_resident(iris_device_t *d) {

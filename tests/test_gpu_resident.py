@@ -88,7 +88,7 @@ def test_mapped_file_walk_is_resident(device, tmp_path, kind):
             up1 = uploads(device)
             assert up1 >= 3  # at least one upload per granule
             count, nbytes = device.resident()
-            assert count == 1 and nbytes >= recs.nbytes
+            assert count == 1 and nbytes >= recs.nbytes, device.config()
             second = walk(eng, recs)
             third = walk(eng, recs, chunk=7_777)  # other slice sizes hit the same copy
             device.synchronize()

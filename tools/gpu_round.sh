@@ -38,6 +38,14 @@ for S in "$@"; do
         timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/tests.log 2>&1 ||
             { echo "tests rc=$?"; grep -E "FAILED|Error|error" $O/tests.log | tail -20; tail -5 $O/tests.log; exit 1; }
         tail -1 $O/tests.log ;;
+    tests:*)  # tests:file1,file2 -- those GPU test files only
+        F=$(echo ${S#tests:} | tr ',' ' ' | sed 's#\([^ ]*\)#tests/\1#g')
+        timeout -k 10 900 python -u -m pytest $F -m gpu -x -v --timeout 300 --timeout-method thread > $O/tests_part.log 2>&1 ||
+            { echo "tests rc=$?"; grep -E "FAILED|Error|error|assert" $O/tests_part.log | tail -20; tail -5 $O/tests_part.log; exit 1; }
+        tail -1 $O/tests_part.log ;;
+    diag)
+        timeout -k 10 300 python tools/resident_diag.py > $O/resident_diag.log 2>&1 || { echo "diag rc=$?"; tail -5 $O/resident_diag.log; exit 1; }
+        cat $O/resident_diag.log ;;
     smoke)
         timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo "smoke rc=$?"; tail -5 $O/smoke.log; exit 1; }
         tail -1 $O/smoke.log ;;
