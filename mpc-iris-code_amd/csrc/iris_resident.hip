@@ -17,8 +17,10 @@
 // taken when their granule was uploaded (a write the timestamps miss: their granularity is the
 // kernel's tick).  A changed file drops its copy; the call then starts over.  Where map_files
 // cannot be read (it needs ptrace-read access to the process, which some sandboxes withhold) the
-// copy holds the mapped file open (checked to be the mapping's inode) and fstats that instead,
-// and re-reads the mapping's line of /proc/self/maps at most every 50 ms to notice a remap.
+// copy holds the mapped file open (opened by the mapping's path and checked to be its inode) and
+// fstats that instead,
+// and re-reads the mapping's line of /proc/self/maps at the start of every walk (a slice at
+// record 0) and at least every 50 ms, to notice a remap.
 //
 // Not made resident: anonymous or writable memory, private mappings, files larger than the
 // device's free memory (less a reserve; older copies are evicted first, least recently used),
@@ -27,7 +29,6 @@
 #include <errno.h>
 #include <fcntl.h>
 #include <stdio.h>
-#include <sys/sysmacros.h>
 #include <string.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -145,7 +146,7 @@ bool file_stat(const Resident *r, struct stat *st) {
 }
 
 // Whether the mapping is still the one the copy was made of.  map_files answers that with every
-// stat; the descriptor form re-reads /proc/self/maps at most every 50 ms (now = always).
+// stat; the descriptor form re-reads /proc/self/maps when asked (now) and at least every 50 ms.
 bool vma_same(Resident *r, bool now) {
     if (r->fd < 0) return true;
     const auto t = std::chrono::steady_clock::now();
@@ -182,11 +183,12 @@ Resident *make_resident(iris_device *d, int kind, uintptr_t p, uint64_t n) {
     struct stat st;
     int fd = -1;
     if (stat(link, &st) != 0) {
-        // map_files unreadable here: the mapped file by its path, if it is the mapping's inode
+        // map_files unreadable here: the mapped file by its path, if it is the mapping's inode (the
+        // device number is not compared: on overlay file systems /proc/self/maps shows the lower
+        // layer's, which st_dev does not)
         const int err = errno;
         fd = ::open(v.path.c_str(), O_RDONLY | O_CLOEXEC);
-        if (fd < 0 || fstat(fd, &st) != 0 || (uint64_t)st.st_ino != v.inode ||
-            st.st_dev != makedev(v.maj, v.mnr)) {
+        if (fd < 0 || fstat(fd, &st) != 0 || (uint64_t)st.st_ino != v.inode) {
             if (fd >= 0) ::close(fd);
             return ineligible(std::string("map_files: ") + strerror(err) + "; the path is not the mapped file");
         }
@@ -324,7 +326,7 @@ int iris_api::resident_slice(iris_device *d, int kind, const void *ptr, uint64_t
         struct stat st;
         if (!file_stat(r, &st) || st.st_dev != r->st.st_dev || st.st_ino != r->st.st_ino ||
             st.st_size != r->st.st_size || !same_time(st.st_mtim, r->st.st_mtim) ||
-            !same_time(st.st_ctim, r->st.st_ctim) || !vma_same(r, false)) {
+            !same_time(st.st_ctim, r->st.st_ctim) || !vma_same(r, p == r->base)) {
             drop(d, r);  // the mapping went away or its file changed: start over
             continue;
         }
