@@ -19,8 +19,9 @@
 // cannot be read (it needs ptrace-read access to the process, which some sandboxes withhold) the
 // copy holds the mapped file open (opened by the mapping's path and checked to be its inode) and
 // fstats that instead,
-// and re-reads the mapping's line of /proc/self/maps at the start of every walk (a slice at
-// record 0) and at least every 50 ms, to notice a remap.
+// and re-reads the mapping's line of /proc/self/maps at least every 200 ms to notice a remap (a
+// read of /proc/self/maps costs ~0.4 ms in a process with ~500 mappings; the slice probe covers a
+// remap in between).
 //
 // Not made resident: anonymous or writable memory, private mappings, files larger than the
 // device's free memory (less a reserve; older copies are evicted first, least recently used),
@@ -146,11 +147,11 @@ bool file_stat(const Resident *r, struct stat *st) {
 }
 
 // Whether the mapping is still the one the copy was made of.  map_files answers that with every
-// stat; the descriptor form re-reads /proc/self/maps when asked (now) and at least every 50 ms.
+// stat; the descriptor form re-reads /proc/self/maps when asked (now) and at least every 200 ms.
 bool vma_same(Resident *r, bool now) {
     if (r->fd < 0) return true;
     const auto t = std::chrono::steady_clock::now();
-    if (!now && t - r->vma_checked < std::chrono::milliseconds(50)) return true;
+    if (!now && t - r->vma_checked < std::chrono::milliseconds(200)) return true;
     Vma v;
     if (!find_vma(r->lo, &v) || v.lo != r->lo || v.hi != r->hi || v.inode != r->inode || v.path != r->path ||
         v.perms[1] != '-')
@@ -326,7 +327,7 @@ int iris_api::resident_slice(iris_device *d, int kind, const void *ptr, uint64_t
         struct stat st;
         if (!file_stat(r, &st) || st.st_dev != r->st.st_dev || st.st_ino != r->st.st_ino ||
             st.st_size != r->st.st_size || !same_time(st.st_mtim, r->st.st_mtim) ||
-            !same_time(st.st_ctim, r->st.st_ctim) || !vma_same(r, p == r->base)) {
+            !same_time(st.st_ctim, r->st.st_ctim) || !vma_same(r, false)) {
             drop(d, r);  // the mapping went away or its file changed: start over
             continue;
         }
