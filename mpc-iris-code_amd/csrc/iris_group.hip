@@ -28,17 +28,21 @@
 // is polled meanwhile.  On expiry or error the group's communicators are
 // aborted (ncclCommAbort) and the call returns IRIS_E_HIP; the group then
 // refuses every further call except the destroys.  Forming the group is bounded
-// the same way: the communicators are created non-blocking
-// (ncclCommInitRankConfig, config.blocking = 0) and polled until ready, and a
-// rank whose peers never arrive aborts them and fails instead of hanging.  With
-// non-blocking communicators ncclGroupEnd may return ncclInProgress (RCCL
-// launches the group's work from a helper thread): the exchange then waits,
-// bounded, for the launch before it orders anything after the all-gather.
+// too: RCCL's init blocks until every rank has arrived (even non-blocking
+// communicators do, in RCCL 2.27.7), so it runs on a helper thread the caller
+// waits for with the group's bound; a rank whose peers never arrive fails
+// instead of hanging and abandons that thread's init.  An ncclGroupEnd that
+// returns ncclInProgress (non-blocking communicators, should a caller's RCCL
+// make them) is waited for, bounded, before anything is ordered after the
+// all-gather.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <string.h>
 
 #include <array>
+#include <condition_variable>
+#include <memory>
+#include <mutex>
 #include <chrono>
 #include <new>
 #include <thread>
@@ -386,39 +390,82 @@ uint32_t init_timeout(const iris_group *g) {
     return h ? h : 120000;
 }
 
-// Creates the communicators of the local devices as RCCL ranks rank0 + i of nranks, non-blocking,
-// and waits (bounded) until every one is ready; on failure aborts whatever was created.
-int comm_init(iris_group *g, const ncclUniqueId &u) {
-    const size_t L = g->devs.size();
-    g->comms.assign(L, nullptr);
-    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
-    cfg.blocking = 0;
+// A communicator init that may never finish (a peer that never starts): RCCL 2.27.7 blocks inside
+// ncclCommInitRankConfig / ncclGroupEnd even with config.blocking = 0
+// (profiles/r05_rccl_nonblocking_init.txt), so the init runs on a helper thread of its own and the
+// caller waits for it with a bound.  On expiry the caller leaves; the job is abandoned and owns
+// everything it uses -- should its init ever complete, it aborts the communicators itself.
+struct InitJob {
+    std::mutex mu;
+    std::condition_variable cv;
+    bool done = false, abandoned = false;
+    ncclResult_t r = ncclSuccess;
+    std::string err;
+    std::vector<int> ordinals;
+    std::vector<ncclComm_t> comms;
+    ncclUniqueId u;
+    int nranks = 0, rank0 = 0;
+};
+
+void init_job_run(std::shared_ptr<InitJob> job) {
     ncclResult_t r = ncclGroupStart();
-    for (size_t i = 0; r == ncclSuccess && i < L; ++i) {
-        if (hipSetDevice(g->devs[i]->ordinal) != hipSuccess) {
+    for (size_t i = 0; r == ncclSuccess && i < job->ordinals.size(); ++i) {
+        if (hipSetDevice(job->ordinals[i]) != hipSuccess) {
             r = ncclInvalidArgument;
             break;
         }
-        r = ncclCommInitRankConfig(&g->comms[i], (int)g->ranks, u, (int)(g->rank0 + i), &cfg);
-        if (r == ncclInProgress) r = ncclSuccess;
+        r = ncclCommInitRank(&job->comms[i], job->nranks, job->u, job->rank0 + (int)i);
     }
-    ncclResult_t r2 = ncclGroupEnd();
-    if (r2 == ncclInProgress) r2 = ncclSuccess;
-    int rc = 0;
-    if (r != ncclSuccess || r2 != ncclSuccess)
-        rc = fail(IRIS_E_HIP, std::string("ncclCommInitRankConfig: ") + ncclGetErrorString(r != ncclSuccess ? r : r2));
-    else
-        rc = comms_ready(g, init_timeout(g), "RCCL communicator init (" + std::to_string(g->ranks) + " ranks)");
-    if (rc != 0) {
-        const std::string m = g_err;
-        for (size_t i = 0; i < L; ++i)
-            if (g->comms[i]) {
-                (void)hipSetDevice(g->devs[i]->ordinal);
-                (void)ncclCommAbort(g->comms[i]);
+    const ncclResult_t r2 = ncclGroupEnd();
+    if (r == ncclSuccess) r = r2;
+    std::lock_guard<std::mutex> l(job->mu);
+    job->r = r;
+    if (r != ncclSuccess) job->err = ncclGetErrorString(r);
+    job->done = true;
+    if (job->abandoned) {  // nobody waits any more: release what was created
+        for (size_t i = 0; i < job->comms.size(); ++i)
+            if (job->comms[i]) {
+                (void)hipSetDevice(job->ordinals[i]);
+                (void)ncclCommAbort(job->comms[i]);
             }
-        g->comms.assign(L, nullptr);
-        return fail(rc, m);
+        return;
     }
+    job->cv.notify_all();
+}
+
+// Creates the communicators of the local devices as RCCL ranks rank0 + i of nranks (one RCCL
+// group, ncclCommInitAll's form for several local devices) and waits at most the group's bound.
+int comm_init(iris_group *g, const ncclUniqueId &u) {
+    const size_t L = g->devs.size();
+    g->comms.assign(L, nullptr);
+    auto job = std::make_shared<InitJob>();
+    for (iris_device *d : g->devs) job->ordinals.push_back(d->ordinal);
+    job->comms.assign(L, nullptr);
+    job->u = u;
+    job->nranks = (int)g->ranks;
+    job->rank0 = (int)g->rank0;
+    try {
+        std::thread(init_job_run, job).detach();
+    } catch (...) {
+        return fail(IRIS_E_NOMEM, "cannot start the RCCL init thread");
+    }
+    const uint32_t ms = init_timeout(g);
+    std::unique_lock<std::mutex> l(job->mu);
+    if (!job->cv.wait_for(l, std::chrono::milliseconds(ms), [&] { return job->done; })) {
+        job->abandoned = true;
+        return fail(IRIS_E_HIP, "RCCL communicator init (" + std::to_string(g->ranks) + " ranks) did not complete within " +
+                                    std::to_string(ms) + " ms (a peer rank failed, never started, or is unreachable); "
+                                    "the pending init is abandoned");
+    }
+    if (job->r != ncclSuccess) {
+        for (size_t i = 0; i < L; ++i)
+            if (job->comms[i]) {
+                (void)hipSetDevice(job->ordinals[i]);
+                (void)ncclCommAbort(job->comms[i]);
+            }
+        return fail(IRIS_E_HIP, "ncclCommInitRank: " + job->err);
+    }
+    g->comms = job->comms;
     return 0;
 }
 

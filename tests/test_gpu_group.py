@@ -250,6 +250,174 @@ def test_group_single_rank_communicator():
             assert same(gdb.search(query), best, idx) and idx == 1234
 
 
+MISSING_PEER_CHILD = r"""
+import json, os, sys, time
+import numpy as np
+import iris_hip as ih
+from oracle import oracle_c as oc
+
+t0 = time.monotonic()
+err = None
+try:
+    ih.Group.rank(0, 2, 0, ih.Group.unique_id())  # rank 1 never comes
+except ih.IrisError as e:
+    err = str(e)
+dt = time.monotonic() - t0
+n = 2000
+ref = oc.gen_templates(80, 0, n)
+query = ref[777].copy()
+best, idx = oc.argmin(oc.template_distances(query, ref))
+dev = ih.Device(0)
+with ih.Database(dev, ih.KIND_TEMPLATES, n) as db:
+    db.append(ref)
+    with ih.TemplateEngine(dev, query) as eng:
+        m1 = eng.search(db)
+with ih.Group.rank(0, 1, 0, ih.Group.unique_id()) as g:
+    with ih.GroupDatabase(g, ih.KIND_TEMPLATES, n) as gdb:
+        gdb.write(0, ref)
+        m2 = gdb.search(query)
+dev.close()
+print(json.dumps({"err": err, "dt": dt, "want": [int(idx), float(best)],
+                  "single": [int(m1.index), m1.distance], "group": [int(m2.index), m2.distance]}))
+sys.stdout.flush()
+"""
+
+
+def test_group_missing_peer_fails_within_bound(tmp_path):
+    """A 2-rank group whose second rank never comes: forming it must fail within the bound
+    (IRIS_GROUP_TIMEOUT_MS, read when the group's device opens) instead of hanging in RCCL's
+    init; the same process's GPU then searches and forms a 1-rank group normally, and the
+    process exits although the abandoned init never finished.  Run in a child process so that
+    its exit is part of what is tested."""
+    import json
+    import os
+    import subprocess
+    import sys
+    import time
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, IRIS_GROUP_TIMEOUT_MS="6000",
+               PYTHONPATH=os.pathsep.join([os.path.join(root, "mpc-iris-code_amd"), root]))
+    script = tmp_path / "child.py"
+    script.write_text(MISSING_PEER_CHILD)
+    t0 = time.monotonic()
+    r = subprocess.run([sys.executable, str(script)], cwd=root, env=env, capture_output=True, text=True,
+                       timeout=150)
+    wall = time.monotonic() - t0
+    assert r.returncode == 0, (r.returncode, r.stderr[-3000:])
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert d["err"] and "did not complete within 6000 ms" in d["err"], d
+    assert d["dt"] < 6 + 10, d  # the bound, plus opening the device
+    want_idx, want_d = d["want"]
+    assert d["single"][0] == want_idx and d["group"][0] == want_idx == 777
+    assert np.float64(d["single"][1]).view(np.uint64) == np.float64(want_d).view(np.uint64)
+    assert np.float64(d["group"][1]).view(np.uint64) == np.float64(want_d).view(np.uint64)
+    assert wall < 120, wall  # the child exited with the abandoned init still pending
+
+
+@pytest.mark.parametrize("side", ["plain", "delayed"])
+def test_group_async_out_of_order(group, hooked_group, side):
+    """Pipelined searches, waited out of order; "delayed": every all-gather is held back by the
+    IRIS_GROUP_DELAY_US hook, so searches k + 4, k + 8 (the send-slot ring) run their kernels
+    before search k's winners are sent -- each must still get its own answer."""
+    g = group if side == "plain" else hooked_group(IRIS_GROUP_DELAY_US=DELAY_US)
+    got, want = async_out_of_order(g)
+    for k, (best, idx) in enumerate(want):
+        assert same(got[k], best, idx) and idx == 1000 + 4100 * k, (k, got[k], idx)
+
+
+def test_group_delay_hook_reaches_the_race_window(hooked_group):
+    """The same run with the exchange-buffer ordering dropped (IRIS_GROUP_UNORDERED, test-only):
+    later searches overwrite the winners of earlier ones before they are sent, so some answers
+    are wrong -- the delayed test above exercises the write-after-read hazard it guards."""
+    g = hooked_group(IRIS_GROUP_DELAY_US=DELAY_US, IRIS_GROUP_UNORDERED=1)
+    got, want = async_out_of_order(g)
+    wrong = [k for k, (best, idx) in enumerate(want) if not same(got[k], best, idx)]
+    assert wrong, "the delayed all-gathers never met a reused send slot"
+
+
+@pytest.mark.parametrize("layout", [ih.LAYOUT_LANES])
+def test_group_other_layouts(group, layout):
+    n = 3001
+    ref = oc.gen_templates(SEED, 0, n)
+    query = oc.gen_templates(SEED + 4, 0, 1)[0]
+    with ih.GroupDatabase(group, ih.KIND_TEMPLATES, n, layout, shards_per_device=3) as gdb:
+        gdb.generate(SEED)
+        gdb.write(2999, planted(query, 15, 0x11)[None, :])
+        ref[2999] = planted(query, 15, 0x11)
+        best, idx = oracle_best(query, ref)
+        m = gdb.search(query)
+        assert same(m, best, idx) and idx == 2999 and m.rotation == 15
+
+
+@pytest.mark.parametrize("nq", [2, 3, 9])
+def test_group_batch_search(group, device, nq):
+    n, spd = 6000, 3
+    ref = oc.gen_templates(SEED, 0, n)
+    qs = oc.gen_templates(SEED + 20, 0, nq)
+    with ih.GroupDatabase(group, ih.KIND_TEMPLATES, n, shards_per_device=spd) as gdb:
+        gdb.generate(SEED)
+        sites = [gdb.shard(k % spd)[0] + 17 * k + 3 for k in range(nq)]
+        for k, s in enumerate(sites):
+            if k % 2 == 0:  # every other query gets a planted answer
+                rec = planted(qs[k], (k % 31) - 15, 0x5)
+                gdb.write(s, rec[None, :])
+                ref[s] = rec
+        got = gdb.batch_search(qs)
+        for k, q in enumerate(qs):
+            best, idx = oracle_best(q, ref)
+            assert same(got[k], best, idx), (k, got[k], best, idx)
+
+
+def test_group_write_read_across_shards_and_load_file(group, tmp_path):
+    n, spd = 2500, 4
+    rng = np.random.default_rng(5)
+    recs = rng.integers(0, 2**64, (n, 400), dtype=np.uint64)
+    path = tmp_path / "t.templates"
+    recs.tofile(path)
+    with ih.GroupDatabase(group, ih.KIND_TEMPLATES, n - 100, shards_per_device=spd) as gdb:
+        gdb.load_file(path, first=100)
+        assert (gdb.read(0, n - 100) == recs[100:]).all()
+        a, b = gdb.shard(2)[0] - 3, gdb.shard(2)[0] + 4  # a range across a shard boundary
+        gdb.write(a, recs[:b - a])
+        assert (gdb.read(a, b - a) == recs[:b - a]).all()
+        query = recs[7]
+        best, idx = oracle_best(query, gdb.read(0, n - 100))
+        assert same(gdb.search(query), best, idx)
+    with ih.GroupDatabase(group, ih.KIND_TEMPLATES, n, shards_per_device=spd) as gdb:
+        with pytest.raises(ih.IrisError):
+            gdb.load_file(path, first=1)  # the file holds fewer than first + total records
+
+
+def test_group_rejects_duplicate_device_and_bad_args():
+    with pytest.raises(ih.IrisError):
+        ih.Group([0, 0])
+    with ih.Group([0]) as g:
+        with pytest.raises(ih.IrisError):
+            ih.GroupDatabase(g, ih.KIND_TEMPLATES, 10, shards_per_device=0)
+        with ih.GroupDatabase(g, ih.KIND_MASKS, 10) as gdb:
+            with pytest.raises(ih.IrisError):
+                gdb.search(oc.gen_templates(1, 0, 1)[0])
+
+
+def test_group_single_rank_communicator():
+    """The multi-process form (non-blocking ncclCommInitRankConfig) with one rank: what each
+    torchrun rank of bench.py builds; RCCL itself reports one rank on this GPU."""
+    uid = ih.Group.unique_id()
+    assert len(uid) == 128
+    n = 3000
+    ref = oc.gen_templates(SEED, 0, n)
+    query = ref[1234].copy()
+    query[5] ^= np.uint64(0xFF)
+    with ih.Group.rank(0, 1, 0, uid) as g:
+        assert (g.local_devices, g.ranks, g.first_rank) == (1, 1, 0)
+        assert g.rccl_nranks == 1 and len(g.rccl_devices) == 1 and ":" in g.rccl_devices[0]
+        with ih.GroupDatabase(g, ih.KIND_TEMPLATES, n, shards_per_device=2) as gdb:
+            gdb.generate(SEED)
+            best, idx = oracle_best(query, ref)
+            assert same(gdb.search(query), best, idx) and idx == 1234
+
+
 def test_group_missing_peer_fails_within_bound(monkeypatch, device):
     """A 2-rank group whose second rank never comes: forming it must fail within the bound
     (IRIS_GROUP_TIMEOUT_MS, read when the group's device opens) instead of hanging in RCCL's

@@ -172,12 +172,15 @@ def test_other_arrays_upload_per_call(device, hooked_device, tmp_path, monkeypat
             dev.reset_stats()
             dev.set_profiling(True)
             try:
+                calls = -(-n // CHUNK)
                 a = walk(eng, recs)
                 dev.synchronize()
                 u1 = uploads(dev)
                 b = walk(eng, recs)
                 dev.synchronize()
-                assert uploads(dev) >= 2 * u1 > 0
+                # every call of both walks uploads (at least one pack launch each; the tuned upload
+                # path may split a call's records into several)
+                assert u1 >= calls and uploads(dev) - u1 >= calls, (u1, uploads(dev))
             finally:
                 dev.set_profiling(False)
             assert dev.resident() == (0, 0)
