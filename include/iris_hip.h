@@ -380,11 +380,12 @@ int iris_match_merge(const iris_match_t *records, uint64_t count, iris_match_t *
  *    rank (any side channel); each rank then calls iris_group_create_rank with
  *    the same id.  Every rank makes the same group calls (SPMD); each holds
  *    and fills only its own shards.
- * Forming a group is bounded: the communicators are created non-blocking
- * (ncclCommInitRankConfig, blocking = 0) and polled until ready, then every
- * rank's PCI bus id is all-gathered over them; if a peer never arrives the call
- * aborts its communicators and fails (IRIS_E_HIP) within IRIS_GROUP_TIMEOUT_MS
- * (default 120 s) instead of hanging, and the device stays usable.
+ * Forming a group is bounded: RCCL's init (which blocks until every rank has
+ * arrived) runs on a helper thread waited for at most IRIS_GROUP_TIMEOUT_MS
+ * (default 120 s); if a peer never arrives the call fails (IRIS_E_HIP) instead
+ * of hanging, the pending init is abandoned (it aborts its communicators should
+ * it ever complete) and the device stays usable.  A formed group all-gathers
+ * every rank's PCI bus id over its communicators (iris_group_rccl_info).
  * Group calls are blocking and serialised per group, like the device calls.
  *
  * Failure: waiting for an exchange is bounded.  The clock starts when every
