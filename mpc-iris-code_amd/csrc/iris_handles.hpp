@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <functional>
 #include <map>
 #include <mutex>
@@ -142,7 +143,11 @@ struct iris_device {
     // read-only file mappings kept resident for host-slice calls (iris_resident.hip), the address
     // ranges found ineligible, and the use counter of their LRU eviction
     std::vector<struct Resident *> resident;
-    std::vector<std::pair<uintptr_t, uintptr_t>> not_resident;
+    struct NotResident {
+        uintptr_t lo, hi;
+        std::chrono::steady_clock::time_point until;  // re-examined after this (memory frees, addresses get reused)
+    };
+    std::vector<NotResident> not_resident;
     uint64_t resident_clock = 0;
     std::string resident_skip;  // why the last mapping refused was not made resident (iris_config)
 };

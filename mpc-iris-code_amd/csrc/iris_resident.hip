@@ -50,6 +50,7 @@ constexpr size_t kGranuleBytes = 256ull << 20;  // upload unit of a resident cop
 constexpr size_t kSnapBytes = 64;              // probe snapshot of every 64th record
 constexpr uint64_t kSnapStride = 64;
 constexpr size_t kNotResidentMax = 4096;       // remembered ineligible address ranges
+constexpr int kNotResidentSeconds = 5;         // how long a refusal stands before the range is re-examined
 
 }  // namespace
 
@@ -98,7 +99,7 @@ void drop(iris_device *d, Resident *r) {
 
 void remember_not_resident(iris_device *d, uintptr_t lo, uintptr_t hi, const std::string &why) {
     if (d->not_resident.size() >= kNotResidentMax) d->not_resident.clear();
-    d->not_resident.emplace_back(lo, hi);
+    d->not_resident.push_back({lo, hi, std::chrono::steady_clock::now() + std::chrono::seconds(kNotResidentSeconds)});
     d->resident_skip = why;
 }
 
@@ -317,8 +318,19 @@ int iris_api::resident_slice(iris_device *d, int kind, const void *ptr, uint64_t
                 break;
             }
         if (!r) {
-            for (const auto &x : d->not_resident)
-                if (p >= x.first && p < x.second) return 0;
+            const auto t = std::chrono::steady_clock::now();
+            bool refused = false;
+            for (size_t i = 0; i < d->not_resident.size();) {
+                const auto &x = d->not_resident[i];
+                if (t >= x.until) {  // expired: dropped, the range is examined afresh
+                    d->not_resident[i] = d->not_resident.back();
+                    d->not_resident.pop_back();
+                    continue;
+                }
+                refused |= p >= x.lo && p < x.hi;
+                ++i;
+            }
+            if (refused) return 0;
             r = make_resident(d, kind, p, n);
             if (!r) return 0;
         }
