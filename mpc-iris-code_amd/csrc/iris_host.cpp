@@ -220,6 +220,7 @@ void build_query_tile(const iris_template_t *q, uint32_t *tile) {
 #include <thread>
 #include <vector>
 
+#include <errno.h>
 #include <unistd.h>
 
 namespace iris {
@@ -240,11 +241,16 @@ class CopyPool {
     pid_t pid() const { return pid_; }
     int parts() const { return (int)threads_.size() + 1; }
 
-    void run(char *dst, const char *src, size_t bytes) {
+    // src != nullptr: memcpy; else pread from fd at file offset off.  Returns false if a read failed
+    // (an I/O error, or the file ended before `bytes`).
+    bool run(char *dst, const char *src, size_t bytes, int fd = -1, off_t off = 0) {
         std::lock_guard<std::mutex> one(run_mu_);  // one copy at a time (devices may call concurrently)
         dst_ = dst;
         src_ = src;
         bytes_ = bytes;
+        fd_ = fd;
+        off_ = off;
+        ok_.store(true, std::memory_order_relaxed);
         remaining_.store(parts() - 1, std::memory_order_relaxed);
         {
             std::lock_guard<std::mutex> l(mu_);
@@ -253,13 +259,27 @@ class CopyPool {
         cv_.notify_all();
         part(0);
         while (remaining_.load(std::memory_order_acquire) != 0) __builtin_ia32_pause();
+        return ok_.load(std::memory_order_acquire);
     }
 
    private:
     void part(int id) {
         const size_t per = ((bytes_ + parts() - 1) / parts() + 63) & ~(size_t)63;
         const size_t a = std::min(bytes_, (size_t)id * per), b = std::min(bytes_, a + per);
-        if (a < b) memcpy(dst_ + a, src_ + a, b - a);
+        if (a >= b) return;
+        if (src_) {
+            memcpy(dst_ + a, src_ + a, b - a);
+            return;
+        }
+        for (size_t done = a; done < b;) {
+            const ssize_t r = ::pread(fd_, dst_ + done, b - done, off_ + (off_t)done);
+            if (r < 0 && errno == EINTR) continue;
+            if (r <= 0) {
+                ok_.store(false, std::memory_order_relaxed);
+                return;
+            }
+            done += (size_t)r;
+        }
     }
     void worker(int id) {
         uint64_t seen = 0;
@@ -288,6 +308,9 @@ class CopyPool {
     char *dst_ = nullptr;
     const char *src_ = nullptr;
     size_t bytes_ = 0;
+    int fd_ = -1;
+    off_t off_ = 0;
+    std::atomic<bool> ok_{true};
 };
 
 constexpr int kCopyHelpers = 3;
@@ -381,24 +404,32 @@ size_t format_hooks(const Hooks &h, char *buf, size_t len) {
     return s.size();
 }
 
-void parallel_copy(void *dst, const void *src, size_t bytes, int lane) {
-    // one pool per device (lane = ordinal): devices driven from their own threads (a device group's
-    // loads, concurrent host-slice calls) copy in parallel instead of queueing on one pool
+namespace {
+
+// one pool per device (lane = ordinal): devices driven from their own threads (a device group's
+// loads, concurrent host-slice calls) copy in parallel instead of queueing on one pool
+CopyPool *pool_of(int lane) {
     constexpr int kLanes = 16;
     static std::mutex create_mu;
     static CopyPool *pools[kLanes] = {};  // leaked on purpose (detached helpers)
+    const int l = ((lane % kLanes) + kLanes) % kLanes;
+    std::lock_guard<std::mutex> g(create_mu);
+    if (!pools[l] || pools[l]->pid() != getpid()) pools[l] = new CopyPool(copy_helpers());  // a forked child gets its own
+    return pools[l];
+}
+
+}  // namespace
+
+void parallel_copy(void *dst, const void *src, size_t bytes, int lane) {
     if (bytes < kParallelCopyMin) {
         memcpy(dst, src, bytes);
         return;
     }
-    const int l = ((lane % kLanes) + kLanes) % kLanes;
-    CopyPool *p;
-    {
-        std::lock_guard<std::mutex> g(create_mu);
-        if (!pools[l] || pools[l]->pid() != getpid()) pools[l] = new CopyPool(copy_helpers());  // a forked child gets its own
-        p = pools[l];
-    }
-    p->run((char *)dst, (const char *)src, bytes);
+    (void)pool_of(lane)->run((char *)dst, (const char *)src, bytes);
+}
+
+bool parallel_pread(int fd, void *dst, size_t bytes, off_t off, int lane) {
+    return pool_of(lane)->run((char *)dst, nullptr, bytes, fd, off);
 }
 
 }  // namespace iris

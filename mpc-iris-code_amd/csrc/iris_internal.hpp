@@ -310,5 +310,8 @@ void build_shares_rotations(const uint16_t *query, uint32_t *tab);
 bool partial_better(const Partial &a, const Partial &b);
 // memcpy split over a few persistent helper threads (copies of at least 256 KB)
 void parallel_copy(void *dst, const void *src, size_t bytes, int lane = 0);  // lane: the device ordinal
+// pread of [off, off + bytes) of fd into dst, split over the same helper threads; false if a read
+// failed or the file ended early
+bool parallel_pread(int fd, void *dst, size_t bytes, long off, int lane = 0);
 
 }  // namespace iris

@@ -172,7 +172,7 @@ int iris_db_load_file(iris_db_t *db, const char *path, uint64_t first, uint64_t 
             // an IRIS_E_IO return, not a SIGBUS
             const off_t off0 = (off_t)first * (off_t)k.rec_bytes;
             const SlotFill fill = [&](void *dst, size_t off, size_t bytes) {
-                return parallel_io(f.fd, (char *)dst, bytes, off0 + (off_t)off, false);
+                return parallel_pread(f.fd, dst, bytes, off0 + (off_t)off, d->ordinal);
             };
             const int rc = db_write_pinned(db, base, nullptr, n, &fill);
             if (rc != IRIS_E_NOMEM) {  // no pinned memory for the slots: the registered windows below
