@@ -240,6 +240,21 @@ int run_u16_engine(iris_engine *e, const iris_db *db, uint64_t first, uint64_t n
 
 // calls of at most this many records (62 MB of rows per buffer) go through the read-ahead
 constexpr uint64_t kReadaheadMax = 1ull << 20;
+// A walk's read-ahead windows: up to kWindowMax consecutive chunks computed by one launch, enough to
+// read ~kWindowBytes of records (a 20 000-share chunk reads 512 MB in ~99 us, ~25 us of it the
+// launch's ramp and drain), with at most kWindowRowsMax of rows per buffer.
+constexpr uint64_t kWindowMax = 8;
+constexpr size_t kWindowBytes = 2ull << 30;
+constexpr size_t kWindowRowsMax = 64ull << 20;
+
+// Records a walk's window starting at a chunk of n records computes (at most `avail`).
+uint64_t window_records(const iris_db *db, uint64_t n, uint64_t avail) {
+    const size_t chunk_bytes = (size_t)n * db->k.rec_bytes;
+    uint64_t w = std::max<uint64_t>(1, (kWindowBytes + chunk_bytes - 1) / chunk_bytes);
+    w = std::min<uint64_t>(w, kWindowMax);
+    w = std::min<uint64_t>(w, std::max<uint64_t>(1, kWindowRowsMax / ((size_t)n * kRot * 2)));
+    return std::min<uint64_t>(w * n, avail);
+}
 
 // TILES databases only: their kernels store the rows as 16-B runs (store_tile_rows), which the
 // host link takes well; the LANES kernels' 2-byte stores would each be a host-link write.
@@ -248,13 +263,12 @@ bool readahead_ok(const iris_db *db, uint64_t n) {
     return db->dev->hooks.readahead && n <= kReadaheadMax && db->k.layout == IRIS_LAYOUT_TILES;
 }
 
-// Drops the engine's read-ahead: its kernels (side stream) have finished when this returns, so
-// the row buffers may be reused or freed.
+// Waits for the engine's read-ahead kernels (side stream): the row buffers may be reused or freed
+// when this returns.  The windows' rows stay valid (a change of the database changes its version).
 int ra_wait(iris_engine *e) {
     Readahead &ra = e->ra;
     if (!ra.computed[0]) return 0;
     iris_device *d = e->dev;
-    ra.pending = false;
     if (d->aux) HIPCHK(hipStreamSynchronize(d->aux));
     if (d->profiling) fold_done(d);
     return 0;
@@ -346,19 +360,25 @@ void ra_release(iris_engine *e) {
 }
 
 // Enqueues the engine kernel over [first, first+n) of db on the device's side stream; it stores
-// the rows straight into the pinned buffer rows[b] (over the host link, no copy-engine DMA);
-// records computed[b].  rows[b] is not being read: the host copies out synchronously.
-int ra_launch(iris_engine *e, const iris_db *a, uint64_t first, uint64_t n, int b) {
+// the rows straight into the pinned buffer rows[b] (over the host link, no copy-engine DMA) and
+// records computed[b]; win[b] describes them from now on.  rows[b] is not being read: the host
+// copies out synchronously.  grow = false: if the buffers are too small, launch nothing
+// (*launched = false) rather than reallocate them under the other window's rows.
+int ra_launch(iris_engine *e, const iris_db *a, uint64_t first, uint64_t n, int b, bool grow = true,
+              bool *launched = nullptr) {
     Readahead &ra = e->ra;
     iris_device *d = e->dev;
+    if (launched) *launched = false;
     CHK(ensure_aux(d));
     if (!ra.computed[0])
         for (int i = 0; i < 2; ++i) HIPCHK(hipEventCreateWithFlags(&ra.computed[i], hipEventDisableTiming));
     const size_t bytes = (size_t)n * kRot * 2;
     if (bytes > ra.cap) {
+        if (!grow) return 0;
         CHK(ra_wait(e));  // no kernel in flight writes either buffer
         for (int i = 0; i < 2; ++i) rows_give(d, ra.rows[i], ra.cap);
         ra.rows[0] = ra.rows[1] = nullptr;
+        ra.win[0].live = ra.win[1].live = false;
         ra.cap = 0;
         const size_t want = std::max(bytes, (size_t)4096);
         size_t got[2] = {0, 0};
@@ -376,40 +396,50 @@ int ra_launch(iris_engine *e, const iris_db *a, uint64_t first, uint64_t n, int 
         HIPCHK(hipEventRecord(d->ra_order, d->stream));
         HIPCHK(hipStreamWaitEvent(d->aux, d->ra_order, 0));
     }
+    ra.win[b].live = false;
     CHK(enqueue_u16_engine(e, a, first, n, (uint16_t *)ra.rows[b], d->aux));
     HIPCHK(hipEventRecord(ra.computed[b], d->aux));
-    ra.db = a;
-    ra.version = a->version;
-    ra.first = first;
-    ra.n = n;
-    ra.cur = b;
-    ra.pending = true;
+    ra.win[b] = Readahead::Window{a, a->version, first, n, true};
+    if (launched) *launched = true;
     return 0;
 }
 
 // A host-output call on records [first, first+n) of db (records [0, end) exist).  Its rows come
-// from the read-ahead buffer when that holds exactly this range of this version of db, else they
-// are computed into the other buffer now; the next range of the same size is launched into the
-// other buffer before this call's rows are copied out, so the kernel overlaps the copy.  The copy
-// is the CPU's, split over helper threads: the copy engines' D2H of these 1.24 MB took 31 us on
-// one box and 150-275 us (8 GB/s) on others, and queued behind the side stream's event it fell
-// into the slow form on boxes that had the fast one (profiles/r03_host_rows.txt, r03_readahead.txt).
+// from a read-ahead window that holds them (same version of the same database), else they are
+// computed now -- a whole window of consecutive chunks when the call continues a walk.  While a
+// window's rows are copied out, the window after it is already computed into the other buffer
+// (one launch of up to kWindowMax chunks, so a chunk pays a fraction of a launch's ramp), and a
+// random-access caller never pays for rows it does not ask for.  The copy is the CPU's, split
+// over helper threads: the copy engines' D2H of these 1.24 MB took 31 us on one box and
+// 150-275 us (8 GB/s) on others, and queued behind the side stream's event it fell into the slow
+// form on boxes that had the fast one (profiles/r03_host_rows.txt, r03_readahead.txt).
 int readahead_u16_call(iris_engine *e, const iris_db *a, uint64_t first, uint64_t n, uint64_t end, uint16_t *out) {
     Readahead &ra = e->ra;
     iris_device *d = e->dev;
-    const bool hit = ra.pending && ra.db == a && ra.version == a->version && ra.first == first && ra.n == n;
-    // speculate only inside a walk: this call read ahead for, or continuing where the last call ended
-    const bool walk = hit || (ra.last_db == a && ra.last_version == a->version && ra.last_end == first);
-    if (!hit) CHK(ra_launch(e, a, first, n, ra.pending ? ra.cur ^ 1 : 0));
-    const int b = ra.cur;
-    ra.pending = false;
+    auto holds = [&](int b) {
+        const Readahead::Window &w = ra.win[b];
+        return w.live && w.db == a && w.version == a->version && w.first <= first && first + n <= w.first + w.n;
+    };
+    int b = holds(0) ? 0 : holds(1) ? 1 : -1;
+    // a walk: this call continues where the last one ended (or was read ahead for)
+    const bool walk = b >= 0 || (ra.last_db == a && ra.last_version == a->version && ra.last_end == first);
+    if (b < 0) {  // a miss: into the buffer whose window starts earlier (the one a walk has left)
+        b = !ra.win[0].live ? 0 : !ra.win[1].live ? 1 : ra.win[0].first <= ra.win[1].first ? 0 : 1;
+        CHK(ra_launch(e, a, first, walk ? window_records(a, n, end - first) : n, b));
+    }
+    const Readahead::Window w = ra.win[b];
     ra.last_db = a;
     ra.last_version = a->version;
     ra.last_end = first + n;
-    const uint64_t next = first + n;
-    if (walk && next < end) CHK(ra_launch(e, a, next, std::min<uint64_t>(n, end - next), b ^ 1));
+    // the walk's next window, into the other buffer (whose window the walk has left behind)
+    const uint64_t next = w.first + w.n;
+    if (walk && next < end) {
+        const Readahead::Window &o = ra.win[b ^ 1];
+        if (!(o.live && o.db == a && o.version == a->version && o.first == next))
+            CHK(ra_launch(e, a, next, window_records(a, n, end - next), b ^ 1, false));
+    }
     HIPCHK(hipEventSynchronize(ra.computed[b]));
-    parallel_copy(out, ra.rows[b], (size_t)n * kRot * 2, d->ordinal);
+    parallel_copy(out, (const char *)ra.rows[b] + (size_t)(first - w.first) * kRot * 2, (size_t)n * kRot * 2, d->ordinal);
     if (d->profiling) fold_done(d);
     return 0;
 }

@@ -170,24 +170,26 @@ inline uint64_t next_db_version() {
     return ++v;
 }
 
-// Read-ahead of a masks / distance engine's host-output calls (host slices of an attached
-// array, iris_engine_batch_process_host, or ranges of a resident database,
+// Read-ahead of a masks / distance engine's host-output calls (host slices of an attached or
+// resident file array, iris_engine_batch_process_host, or ranges of a resident database,
 // iris_engine_batch_process): the reference's participant and resolver walk their file in
-// consecutive 20 000-record chunks (src/main.rs:427-431, 511-516), so while the rows of chunk
-// [first, first + n) are copied to the caller, the engine already computes [first + n, first + 2n)
-// on the device's side stream, its kernel storing the rows straight into the other of two pinned
-// host buffers; the next call, if it asks for exactly that range of the same version of the same
-// database, only copies those rows out.  Speculation starts with the second consecutive call.
+// consecutive 20 000-record chunks (src/main.rs:427-431, 511-516), so while the rows of one window
+// of chunks are copied to the caller, the engine already computes the next window on the device's
+// side stream, its kernel storing the rows straight into the other of two pinned host buffers; a
+// call whose range lies in a window of the same version of the same database only copies its rows
+// out.  Speculation starts with the second consecutive call.
 struct Readahead {
-    const struct iris_db *db = nullptr;
-    uint64_t version = 0, first = 0, n = 0;  // the range in flight into rows[cur]
+    struct Window {
+        const struct iris_db *db = nullptr;
+        uint64_t version = 0, first = 0, n = 0;  // the records whose rows rows[b] holds (once computed[b])
+        bool live = false;
+    };
+    Window win[2];
     void *rows[2] = {nullptr, nullptr};      // pinned host [n][31] u16 rows
     size_t cap = 0;                          // bytes of each
     hipEvent_t computed[2] = {nullptr, nullptr};  // side stream, after the kernel into rows[b]
-    int cur = 0;
-    bool pending = false;
     // the previous call's range end: a call that starts there (or was read ahead) is part of a
-    // walk, and only then is the next range computed speculatively (a random-access caller
+    // walk, and only then is the next window computed speculatively (a random-access caller
     // never pays for rows it does not ask for)
     const struct iris_db *last_db = nullptr;
     uint64_t last_version = 0, last_end = 0;
