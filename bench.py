@@ -625,12 +625,19 @@ def run_aux(args, dev):
         shares_wl = args.workload == "host-shares"
         n = min(args.n_per_gpu, 200_000 if shares_wl else 2_000_000)  # 5.1 GB / 3.2 GB of host records
         qt = gen_records(dev, ih.KIND_TEMPLATES, 1, SEED + 1)[0]
+        # one engine per walk, as the participant and the resolver build one per request
+        # (src/main.rs:427, 512): no walk is served from rows an earlier walk computed
         if shares_wl:
             host = rng.integers(0, 65536, (n, 12800), dtype=np.uint16)
-            eng = ih.DistanceEngine(dev, ih.encode(ih.Template.from_array(qt)))
+            qenc = ih.encode(ih.Template.from_array(qt))
+
+            def new_engine():
+                return ih.DistanceEngine(dev, qenc)
         else:
             host = gen_records(dev, ih.KIND_MASKS, n, SEED)
-            eng = ih.MasksEngine(dev, qt[200:])
+
+            def new_engine():
+                return ih.MasksEngine(dev, qt[200:])
         hout = np.empty((n, ROT), np.uint16)
         chunk = args.chunk or (20_000 if (args.attached or args.mmap) else n)
         kind = ih.KIND_SHARES if shares_wl else ih.KIND_MASKS
@@ -644,8 +651,9 @@ def run_aux(args, dev):
             del arr
             # the first walk makes the file resident (granule uploads): timed apart from the steps
             t_first = time.perf_counter()
-            for a in range(0, n, chunk):
-                eng.batch_process(hout[a:a + chunk], host[a:a + chunk])
+            with new_engine() as eng:
+                for a in range(0, n, chunk):
+                    eng.batch_process(hout[a:a + chunk], host[a:a + chunk])
             extra["first_walk_s"] = time.perf_counter() - t_first
             extra["resident"] = dict(zip(("count", "bytes"), dev.resident()))
         extra["host_pages_numa"] = {"pages_by_node": pages_nodes(host), "gpu_node": dev.config().get("numa_node")}
@@ -656,14 +664,16 @@ def run_aux(args, dev):
             extra["attach_s"] = time.perf_counter() - t_att
 
         def step():
-            for a in range(0, n, chunk):
-                eng.batch_process(hout[a:a + chunk], host[a:a + chunk])
+            with new_engine() as eng:
+                for a in range(0, n, chunk):
+                    eng.batch_process(hout[a:a + chunk], host[a:a + chunk])
 
         kname, unit = ("shares" if shares_wl else "masks"), "records/s"
         rec_bytes = host.shape[1] * host.itemsize
         workload = (f"{'DistanceEngine' if shares_wl else 'MasksEngine'}::batch_process(out, db: &[T]) over host "
                     f"slices of {chunk} records (src/lib.rs:42-52, 69-79; the participant / resolver loop of "
                     "src/main.rs:426-431, 511-516): "
+                    + "one engine per walk (per request, src/main.rs:427, 512); "
                     + ("the host array is attached to its resident copy (iris_db_attach_host): no upload"
                        if args.attached else
                        ("slices of a read-only file mapping, no attach call: "
@@ -761,21 +771,21 @@ def run_aux(args, dev):
         if args.attached:  # the same chunks through the resident calls, for comparison
             hdev = dev.alloc(chunk * ROT * 2)
             res = {}
-            for form in ("host_out", "device_out"):
-                for _ in range(2):
+            def walk_db(form):
+                with new_engine() as eng:
                     for a in range(0, n, chunk):
                         if form == "host_out":
                             eng.batch_process(hout[a:a + chunk], adb, first=a, n=min(chunk, n - a))
                         else:
                             eng.batch_process_device(adb, hdev, first=a, n=min(chunk, n - a))
+
+            for form in ("host_out", "device_out"):
+                for _ in range(2):
+                    walk_db(form)
                 dev.synchronize()
                 tr = time.perf_counter()
                 for _ in range(args.steps):
-                    for a in range(0, n, chunk):
-                        if form == "host_out":
-                            eng.batch_process(hout[a:a + chunk], adb, first=a, n=min(chunk, n - a))
-                        else:
-                            eng.batch_process_device(adb, hdev, first=a, n=min(chunk, n - a))
+                    walk_db(form)
                 dev.synchronize()
                 res[form + "_records_per_s"] = n * args.steps / (time.perf_counter() - tr)
             dev.free(hdev)
