@@ -252,6 +252,7 @@ uint64_t window_records(const iris_db *db, uint64_t n, uint64_t avail) {
     const size_t chunk_bytes = (size_t)n * db->k.rec_bytes;
     uint64_t w = std::max<uint64_t>(1, (kWindowBytes + chunk_bytes - 1) / chunk_bytes);
     w = std::min<uint64_t>(w, kWindowMax);
+    if (db->dev->hooks.ra_window) w = db->dev->hooks.ra_window;  // test hook: a fixed window
     w = std::min<uint64_t>(w, std::max<uint64_t>(1, kWindowRowsMax / ((size_t)n * kRot * 2)));
     return std::min<uint64_t>(w * n, avail);
 }

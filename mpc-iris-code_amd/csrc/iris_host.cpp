@@ -333,7 +333,7 @@ namespace {
 constexpr const char *kHookNames[] = {"IRIS_TILES_PER_WAVE",  "IRIS_FUSED_REDUCE", "IRIS_BATCH_KERNEL",
                                       "IRIS_SCHEDULE",        "IRIS_LOAD_PREAD",   "IRIS_GROUP_DELAY_US",
                                       "IRIS_GROUP_STALL",     "IRIS_GROUP_UNORDERED", "IRIS_UPLOAD",
-                                      "IRIS_LOAD_WINDOWS"};
+                                      "IRIS_LOAD_WINDOWS",    "IRIS_READAHEAD_WINDOW"};
 constexpr int kNumHooks = (int)(sizeof(kHookNames) / sizeof(kHookNames[0]));
 
 const char *env(const char *name) {
@@ -373,6 +373,7 @@ void read_hooks(Hooks *h) {
         case 7: h->group_unordered = v[0] != '0'; break;
         case 8: h->upload = !strcmp(v, "pinned") ? 1 : !strcmp(v, "runtime") ? 2 : 0; break;
         case 9: h->load_windows = v[0] != '0'; break;
+        case 10: h->ra_window = env_u32(v, 8); break;
         }
     }
 }
@@ -389,7 +390,8 @@ size_t format_hooks(const Hooks &h, char *buf, size_t len) {
              " fused_reduce=" + std::to_string(h.fused_reduce) + " batch_kernel=" + std::to_string(h.batch_kernel) +
              " schedule=" + sched[h.schedule & 3] +
              " load_pread=" + std::to_string(h.load_pread) +
-             " load_windows=" + std::to_string(h.load_windows) + " group_delay_us=" + std::to_string(h.group_delay_us) +
+             " load_windows=" + std::to_string(h.load_windows) + " readahead_window=" + std::to_string(h.ra_window) +
+             " group_delay_us=" + std::to_string(h.group_delay_us) +
              " group_stall=" + std::to_string(h.group_stall) + " group_unordered=" + std::to_string(h.group_unordered) +
              " upload=" + upload_names[h.upload & 3];
     std::string ign;
