@@ -294,10 +294,16 @@ int rows_take(iris_device *d, size_t bytes, void **p, size_t *got) {
     return 0;
 }
 
+// Back to the pool; a full pool frees its oldest buffer, so the sizes callers use now stay
+// pooled (a pool full of another walk's sizes cost every later walk two hipHostMalloc and two
+// hipHostFree of ~0.8 ms each, profiles/r05_rows_pool_trace.txt).
 void rows_give(iris_device *d, void *p, size_t bytes) {
     if (!p) return;
-    if (d->rows_pool.size() < kRowsPoolMax) d->rows_pool.emplace_back(bytes, p);
-    else (void)hipHostFree(p);
+    if (d->rows_pool.size() >= kRowsPoolMax) {
+        (void)hipHostFree(d->rows_pool.front().second);
+        d->rows_pool.erase(d->rows_pool.begin());
+    }
+    d->rows_pool.emplace_back(bytes, p);
 }
 
 // records per kernel of the pinned-rows form (62 MB of rows per buffer)
@@ -364,9 +370,11 @@ void ra_release(iris_engine *e) {
 // the rows straight into the pinned buffer rows[b] (over the host link, no copy-engine DMA) and
 // records computed[b]; win[b] describes them from now on.  rows[b] is not being read: the host
 // copies out synchronously.  grow = false: if the buffers are too small, launch nothing
-// (*launched = false) rather than reallocate them under the other window's rows.
+// (*launched = false) rather than reallocate them under the other window's rows.  New buffers
+// hold at least `reserve` records' rows: a new engine's first call (one chunk) sizes them for the
+// windows a walk from there goes on to, so they are not reallocated at its second call.
 int ra_launch(iris_engine *e, const iris_db *a, uint64_t first, uint64_t n, int b, bool grow = true,
-              bool *launched = nullptr) {
+              bool *launched = nullptr, uint64_t reserve = 0) {
     Readahead &ra = e->ra;
     iris_device *d = e->dev;
     if (launched) *launched = false;
@@ -381,7 +389,7 @@ int ra_launch(iris_engine *e, const iris_db *a, uint64_t first, uint64_t n, int 
         ra.rows[0] = ra.rows[1] = nullptr;
         ra.win[0].live = ra.win[1].live = false;
         ra.cap = 0;
-        const size_t want = std::max(bytes, (size_t)4096);
+        const size_t want = std::max({bytes, (size_t)reserve * kRot * 2, (size_t)4096});
         size_t got[2] = {0, 0};
         for (int i = 0; i < 2; ++i) CHK(rows_take(d, want, &ra.rows[i], &got[i]));
         ra.cap = std::min(got[0], got[1]);
@@ -426,7 +434,8 @@ int readahead_u16_call(iris_engine *e, const iris_db *a, uint64_t first, uint64_
     const bool walk = b >= 0 || (ra.last_db == a && ra.last_version == a->version && ra.last_end == first);
     if (b < 0) {  // a miss: into the buffer whose window starts earlier (the one a walk has left)
         b = !ra.win[0].live ? 0 : !ra.win[1].live ? 1 : ra.win[0].first <= ra.win[1].first ? 0 : 1;
-        CHK(ra_launch(e, a, first, walk ? window_records(a, n, end - first) : n, b));
+        const uint64_t wn = window_records(a, n, end - first);
+        CHK(ra_launch(e, a, first, walk ? wn : n, b, true, nullptr, std::max(wn, window_records(a, n, end))));
     }
     const Readahead::Window w = ra.win[b];
     ra.last_db = a;

@@ -3,6 +3,7 @@
 #   tests   the whole -m gpu suite          smoke   __graft_entry__.smoke()
 #   prof    rocprofv3 kernel stats of the default bench line
 #   pmc     HBM counters of the default bench line (tools/pmc_traffic.sh's passes, into gpurun_out/pmc)
+#   walks:KIND  tools/walk_calls.py KIND (per-call times of chunk walks, mapped file and attached)
 #   any other STEP is a bench line named in the table below
 # Output under gpurun_out/TAG; every GPU step has its own time limit and the script stops at
 # the first failure (no retries).
@@ -46,6 +47,10 @@ for S in "$@"; do
     diag)
         timeout -k 10 300 python tools/resident_diag.py > $O/resident_diag.log 2>&1 || { echo "diag rc=$?"; tail -5 $O/resident_diag.log; exit 1; }
         cat $O/resident_diag.log ;;
+    walks:*)  # walks:shares / walks:masks -- per-call times of chunk walks (tools/walk_calls.py)
+        timeout -k 10 300 python tools/walk_calls.py ${S#walks:} 8 > $O/walks_${S#walks:}.log 2>&1 ||
+            { echo "walks rc=$?"; tail -5 $O/walks_${S#walks:}.log; exit 1; }
+        grep -E "walk 7:" $O/walks_${S#walks:}.log ;;
     smoke)
         timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo "smoke rc=$?"; tail -5 $O/smoke.log; exit 1; }
         tail -1 $O/smoke.log ;;
