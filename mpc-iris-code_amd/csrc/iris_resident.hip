@@ -8,7 +8,10 @@
 // the bytes is what helps: a slice that lies inside a read-only, shared, file-backed mapping of a
 // regular file is served from a device copy of the whole mapping, made granule by granule (256 MB)
 // the first time a call touches it, so the first walk costs what the upload path costs and every
-// later walk reads HBM only.
+// later walk reads HBM only.  Granules are read from the file (pread by the helper threads into the
+// pinned upload slots), not through the caller's mapping: a file that shrinks or fails to read
+// under the fill is a short read -- the copy is dropped and the call uploads its own slice, as it
+// would without this path -- rather than a SIGBUS on a page past the new end of the file.
 //
 // Staleness: the copy stands for (st_dev, st_ino, st_size, st_mtim, st_ctim) of the mapped file,
 // re-checked on every call with one stat of /proc/self/map_files/<lo>-<hi> (the kernel's link to
@@ -58,6 +61,7 @@ struct Resident {
     int kind = 0;
     uintptr_t lo = 0, hi = 0;  // the mapping (one VMA)
     uintptr_t base = 0;        // address of record 0 (the first whole record of the slices seen)
+    uint64_t file_off = 0;     // its offset in the file
     uint64_t nrec = 0;
     std::string link;          // /proc/self/map_files/<lo>-<hi>
     int fd = -1;               // >= 0: map_files unreadable; the mapped file, held open
@@ -262,6 +266,7 @@ Resident *make_resident(iris_device *d, int kind, uintptr_t p, uint64_t n) {
     r->lo = v.lo;
     r->hi = v.hi;
     r->base = base;
+    r->file_off = v.off + (base - v.lo);
     r->nrec = nrec;
     r->link = link;
     r->inode = v.inode;
@@ -276,19 +281,61 @@ Resident *make_resident(iris_device *d, int kind, uintptr_t p, uint64_t n) {
     return r;
 }
 
-// Uploads the granules of [first, first + n) that are not resident yet.
-int fill(Resident *r, uint64_t first, uint64_t n) {
-    const size_t rb = r->db->k.rec_bytes;
-    for (uint64_t g = first / r->gran; g * r->gran < first + n; ++g) {
-        if (r->have[g]) continue;
-        const uint64_t a = g * r->gran, m = std::min<uint64_t>(r->gran, r->nrec - a);
-        const char *src = (const char *)r->base + a * rb;
-        CHK(db_store_locked(r->db, a, src, m));
-        for (uint64_t i = (a + kSnapStride - 1) / kSnapStride * kSnapStride; i < a + m; i += kSnapStride)
-            memcpy(&r->snap[i / kSnapStride * kSnapBytes], (const char *)r->base + i * rb, std::min(kSnapBytes, rb));
-        r->have[g] = 1;
+// The mapped file opened for reading (the held descriptor, else by the mapping's path if that is
+// still the mapping's inode), or -1.
+int open_mapped(const Resident *r, bool *owned) {
+    *owned = false;
+    if (r->fd >= 0) return r->fd;
+    const int fd = ::open(r->path.c_str(), O_RDONLY | O_CLOEXEC);
+    struct stat st;
+    if (fd >= 0 && fstat(fd, &st) == 0 && S_ISREG(st.st_mode) && (uint64_t)st.st_ino == r->inode) {
+        *owned = true;
+        return fd;
     }
-    return 0;
+    if (fd >= 0) ::close(fd);
+    return -1;
+}
+
+// Snapshots of the records [a, a + m) held at `recs` (record a first).
+void take_snapshots(Resident *r, uint64_t a, uint64_t m, const char *recs) {
+    const size_t rb = r->db->k.rec_bytes;
+    for (uint64_t i = (a + kSnapStride - 1) / kSnapStride * kSnapStride; i < a + m; i += kSnapStride)
+        memcpy(&r->snap[i / kSnapStride * kSnapBytes], recs + (i - a) * rb, std::min(kSnapBytes, rb));
+}
+
+// Uploads the granules of [first, first + n) that are not resident yet, read from the file by the
+// helper threads into the pinned upload slots (snapshots taken from the slots).  Where the file
+// cannot be opened or no pinned slots can be had, from the caller's mapping through the tuned upload.
+int fill(iris_device *d, Resident *r, uint64_t first, uint64_t n) {
+    const size_t rb = r->db->k.rec_bytes;
+    int fd = -1;
+    bool owned = false, tried = false;
+    int rc = 0;
+    for (uint64_t g = first / r->gran; g * r->gran < first + n && rc == 0; ++g) {
+        if (r->have[g]) continue;
+        if (!tried) {
+            fd = open_mapped(r, &owned);
+            tried = true;
+        }
+        const uint64_t a = g * r->gran, m = std::min<uint64_t>(r->gran, r->nrec - a);
+        rc = IRIS_E_NOMEM;
+        if (fd >= 0) {
+            const SlotFill read = [&](void *dst, size_t off, size_t bytes) {
+                if (!parallel_pread(fd, dst, bytes, (long)(r->file_off + a * rb + off), d->ordinal)) return false;
+                take_snapshots(r, a + off / rb, bytes / rb, (const char *)dst);
+                return true;
+            };
+            rc = db_write_pinned(r->db, a, nullptr, m, &read);
+        }
+        if (rc == IRIS_E_NOMEM) {  // no descriptor, or no pinned slots: the mapping itself
+            const char *src = (const char *)r->base + a * rb;
+            rc = db_store_locked(r->db, a, src, m);
+            if (rc == 0) take_snapshots(r, a, m, src);
+        }
+        if (rc == 0) r->have[g] = 1;
+    }
+    if (owned) ::close(fd);
+    return rc;
 }
 
 // The slice's probe: up to three snapshotted records inside [first, first + n) still equal the mapping.
@@ -344,7 +391,12 @@ int iris_api::resident_slice(iris_device *d, int kind, const void *ptr, uint64_t
             continue;
         }
         const uint64_t f = (p - r->base) / rb;
-        CHK(fill(r, f, n));
+        if (fill(d, r, f, n) != 0) {  // a short read (the file shrank) or an I/O error: this call uploads
+            const uintptr_t lo = r->lo, hi = r->hi;
+            drop(d, r);
+            remember_not_resident(d, lo, hi, "filling the copy failed: " + g_err);
+            return 0;
+        }
         if (!probe_ok(r, f, n)) {  // written without a timestamp change: start over
             drop(d, r);
             continue;

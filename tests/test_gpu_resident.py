@@ -222,3 +222,28 @@ def test_drop_resident_and_unaligned_slices(device, tmp_path):
         assert (out == want_fn(np.ascontiguousarray(shifted))).all()
         del raw, shifted
     del recs
+
+
+def test_file_with_header_and_truncated_file(device, tmp_path):
+    """Records after a 5000-byte header (the mapping starts at a page-aligned file offset, the
+    records 904 bytes into it: the granules are read from the file at that offset); then the file
+    is cut to fewer records under the live mapping: calls on the records still in the file serve
+    them (the size change drops the copy, a new one of the shorter file is made)."""
+    kind, n, hdr = ih.KIND_MASKS, 30_000, 5000
+    path = tmp_path / "h.masks"
+    host = gen(kind, SEED + 11, n)
+    with open(path, "wb") as f:
+        f.write(np.random.default_rng(1).integers(0, 256, hdr, dtype=np.uint8).tobytes())
+        f.write(host.tobytes())
+    recs = np.memmap(path, dtype=np.uint64, mode="r", offset=hdr, shape=(n, 200))
+    eng, want_fn = engine_and_oracle(device, kind, SEED + 12)
+    want = want_fn(host)
+    with eng:
+        assert (walk(eng, recs) == want).all()
+        assert device.resident()[0] == 1, device.config()
+        keep = 12_345
+        os.truncate(path, hdr + keep * 1600)
+        out = walk(eng, recs[:keep], chunk=5_000)
+        assert (out == want[:keep]).all()
+        assert device.resident()[0] == 1, device.config()
+    del recs
