@@ -49,7 +49,8 @@ using namespace iris_api;
 
 namespace {
 
-constexpr size_t kGranuleBytes = 256ull << 20;  // upload unit of a resident copy
+constexpr size_t kGranuleBytes = 256ull << 20;  // residency unit of a copy
+constexpr size_t kFillRunBytes = 4ull << 30;    // a fill reads ahead up to this much in one pipelined write
 constexpr size_t kSnapBytes = 64;              // probe snapshot of every 64th record
 constexpr uint64_t kSnapStride = 64;
 constexpr size_t kNotResidentMax = 4096;       // remembered ineligible address ranges
@@ -306,18 +307,28 @@ void take_snapshots(Resident *r, uint64_t a, uint64_t m, const char *recs) {
 // Uploads the granules of [first, first + n) that are not resident yet, read from the file by the
 // helper threads into the pinned upload slots (snapshots taken from the slots).  Where the file
 // cannot be opened or no pinned slots can be had, from the caller's mapping through the tuned upload.
+// A run of missing granules goes as one write, extended ahead of the slice up to kFillRunBytes: the
+// slot pipeline's fill and drain then come once per run, not once per granule (a first walk over
+// 3.2 GB took 0.135 s granule by granule, against ~75 ms for the pipelined load of the same file).
 int fill(iris_device *d, Resident *r, uint64_t first, uint64_t n) {
     const size_t rb = r->db->k.rec_bytes;
     int fd = -1;
     bool owned = false, tried = false;
     int rc = 0;
-    for (uint64_t g = first / r->gran; g * r->gran < first + n && rc == 0; ++g) {
-        if (r->have[g]) continue;
+    for (uint64_t g = first / r->gran; g * r->gran < first + n && rc == 0;) {
+        if (r->have[g]) {
+            ++g;
+            continue;
+        }
         if (!tried) {
             fd = open_mapped(r, &owned);
             tried = true;
         }
-        const uint64_t a = g * r->gran, m = std::min<uint64_t>(r->gran, r->nrec - a);
+        uint64_t ge = g + 1;  // the run [g, ge): the slice's missing granules, then read-ahead
+        while (ge < r->have.size() && !r->have[ge] &&
+               (ge * r->gran < first + n || (ge + 1 - g) * r->gran * rb <= kFillRunBytes))
+            ++ge;
+        const uint64_t a = g * r->gran, m = std::min<uint64_t>(ge * r->gran, r->nrec) - a;
         rc = IRIS_E_NOMEM;
         if (fd >= 0) {
             const SlotFill read = [&](void *dst, size_t off, size_t bytes) {
@@ -332,7 +343,8 @@ int fill(iris_device *d, Resident *r, uint64_t first, uint64_t n) {
             rc = db_store_locked(r->db, a, src, m);
             if (rc == 0) take_snapshots(r, a, m, src);
         }
-        if (rc == 0) r->have[g] = 1;
+        if (rc == 0) std::fill(r->have.begin() + g, r->have.begin() + ge, (uint8_t)1);
+        g = ge;
     }
     if (owned) ::close(fd);
     return rc;
