@@ -247,3 +247,39 @@ def test_file_with_header_and_truncated_file(device, tmp_path):
         assert (out == want[:keep]).all()
         assert device.resident()[0] == 1, device.config()
     del recs
+
+
+def test_concurrent_walks_share_one_copy(device, tmp_path):
+    """Two request threads (each its own engine and query, as concurrent participant requests)
+    walk the same mapped file at once, three walks each: one resident copy serves both, and every
+    walk's rows are its own query's (the engines' read-ahead windows never serve each other)."""
+    import threading
+    kind, n = ih.KIND_MASKS, 90_001
+    path = tmp_path / "c.masks"
+    host = gen(kind, SEED + 13, n)
+    host.tofile(path)
+    recs = mapped(path, kind, n)
+    results, errors = {}, []
+
+    def request(i):
+        try:
+            want = None
+            for w in range(3):  # a new engine per walk, as per request
+                eng, want_fn = engine_and_oracle(device, kind, SEED + 20 + i)
+                with eng:
+                    out = walk(eng, recs, chunk=CHUNK if i == 0 else 13_000)
+                if want is None:
+                    want = want_fn(host)
+                results[(i, w)] = (out == want).all()
+        except Exception as exc:  # reported by the main thread
+            errors.append(repr(exc))
+
+    threads = [threading.Thread(target=request, args=(i,)) for i in range(2)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=100)
+    assert not errors, errors
+    assert len(results) == 6 and all(results.values()), results
+    assert device.resident()[0] == 1
+    del recs
