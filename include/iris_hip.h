@@ -253,7 +253,9 @@ int iris_engine_batch_process_device(iris_engine_t *engine, const iris_db_t *db,
  * A slice inside a read-only shared mapping of a regular file -- what the
  * participant and resolver walk (src/main.rs:386-391, 426-431; 455-460,
  * 511-516) -- runs on the device's copy of that file's records, made on first
- * use (256-MB granules as calls reach them) and kept; every call re-checks the
+ * use (read from the file in 256-MB granules, a call's missing ones and up to
+ * 4 GB after them at once; a read that comes up short -- the file shrank --
+ * drops the copy and the call uploads its slice) and kept; every call re-checks the
  * file behind the mapping (device, inode, size, mtime, ctime) and probes three
  * records of the slice, and a changed file is copied afresh.  Files that do not
  * fit the device's free memory (less a reserve) and IRIS_AUTO_RESIDENT=0 keep
