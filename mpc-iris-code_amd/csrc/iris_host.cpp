@@ -333,7 +333,7 @@ namespace {
 constexpr const char *kHookNames[] = {"IRIS_TILES_PER_WAVE",  "IRIS_FUSED_REDUCE", "IRIS_BATCH_KERNEL",
                                       "IRIS_SCHEDULE",        "IRIS_LOAD_PREAD",   "IRIS_GROUP_DELAY_US",
                                       "IRIS_GROUP_STALL",     "IRIS_GROUP_UNORDERED", "IRIS_UPLOAD",
-                                      "IRIS_LOAD_WINDOWS",    "IRIS_READAHEAD_WINDOW"};
+                                      "IRIS_LOAD_WINDOWS",    "IRIS_READAHEAD_WINDOW", "IRIS_RESIDENT_BUDGET_MB"};
 constexpr int kNumHooks = (int)(sizeof(kHookNames) / sizeof(kHookNames[0]));
 
 const char *env(const char *name) {
@@ -374,6 +374,7 @@ void read_hooks(Hooks *h) {
         case 8: h->upload = !strcmp(v, "pinned") ? 1 : !strcmp(v, "runtime") ? 2 : 0; break;
         case 9: h->load_windows = v[0] != '0'; break;
         case 10: h->ra_window = env_u32(v, 8); break;
+        case 11: h->resident_budget_mb = env_u32(v, 1u << 30); break;
         }
     }
 }
@@ -391,6 +392,7 @@ size_t format_hooks(const Hooks &h, char *buf, size_t len) {
              " schedule=" + sched[h.schedule & 3] +
              " load_pread=" + std::to_string(h.load_pread) +
              " load_windows=" + std::to_string(h.load_windows) + " readahead_window=" + std::to_string(h.ra_window) +
+             " resident_budget_mb=" + std::to_string(h.resident_budget_mb) +
              " group_delay_us=" + std::to_string(h.group_delay_us) +
              " group_stall=" + std::to_string(h.group_stall) + " group_unordered=" + std::to_string(h.group_unordered) +
              " upload=" + upload_names[h.upload & 3];

@@ -187,6 +187,7 @@ struct Hooks {
     bool group_unordered = false;    // IRIS_GROUP_UNORDERED=1: drop the exchange-buffer ordering (shows the race)
     int upload = 0;                  // IRIS_UPLOAD=pinned|runtime (1|2): the path of writes >= 8 MB (0: the faster lately)
     uint32_t ra_window = 0;          // IRIS_READAHEAD_WINDOW=1..8: chunks per read-ahead window (0: by size)
+    uint32_t resident_budget_mb = 0; // IRIS_RESIDENT_BUDGET_MB: resident copies hold at most this (0: free memory)
     uint32_t ignored = 0;            // bit i: test hook kHookNames[i] was set without IRIS_TEST_HOOKS=1
 };
 // Reads the environment (the Hooks a device opened now gets).

@@ -235,14 +235,22 @@ Resident *make_resident(iris_device *d, int kind, uintptr_t p, uint64_t n) {
     const size_t reserve = std::max<size_t>(2ull << 30, total_b / 32);
     size_t evictable = 0;
     for (Resident *r : d->resident) evictable += r->dev_bytes;
-    if (dev_bytes + reserve > free_b + evictable)
+    // test hook: the copies together may hold at most this much (the eviction and refusal paths
+    // without filling a 288-GB device)
+    const size_t budget = (size_t)d->hooks.resident_budget_mb << 20;
+    if (dev_bytes + reserve > free_b + evictable || (budget && dev_bytes > budget))
         return refuse("the file (" + std::to_string(dev_bytes >> 20) + " MB on the device) does not fit the free memory");
-    while (dev_bytes + reserve > free_b && !d->resident.empty()) {
+    auto lru_drop = [&] {
         auto lru = std::min_element(d->resident.begin(), d->resident.end(),
                                     [](const Resident *a, const Resident *b) { return a->last_use < b->last_use; });
+        evictable -= (*lru)->dev_bytes;
         drop(d, *lru);
+    };
+    while (dev_bytes + reserve > free_b && !d->resident.empty()) {
+        lru_drop();
         if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return refuse("hipMemGetInfo failed");
     }
+    while (budget && evictable + dev_bytes > budget && !d->resident.empty()) lru_drop();
     Resident *r = new (std::nothrow) Resident();
     if (!r) return refuse("out of host memory");
     r->fd = fd;  // owned by r from here

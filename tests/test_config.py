@@ -9,7 +9,7 @@ import iris_hip as ih
 
 TEST_HOOKS = ["IRIS_TILES_PER_WAVE", "IRIS_FUSED_REDUCE", "IRIS_BATCH_KERNEL", "IRIS_SCHEDULE",
               "IRIS_LOAD_PREAD", "IRIS_GROUP_DELAY_US", "IRIS_GROUP_STALL", "IRIS_GROUP_UNORDERED", "IRIS_UPLOAD",
-              "IRIS_LOAD_WINDOWS", "IRIS_READAHEAD_WINDOW"]
+              "IRIS_LOAD_WINDOWS", "IRIS_READAHEAD_WINDOW", "IRIS_RESIDENT_BUDGET_MB"]
 
 
 @pytest.fixture(autouse=True)
@@ -49,6 +49,8 @@ def test_test_hooks_with_opt_in(monkeypatch):
         ("1", "1", "2", "spin", "1500")
     assert (c["fused_reduce"], c["group_stall"], c["load_pread"], c["upload"]) == ("1", "0", "0", "pinned")
     assert c["load_windows"] == "0"
+    monkeypatch.setenv("IRIS_RESIDENT_BUDGET_MB", "700")
+    assert ih.config()["resident_budget_mb"] == "700"
 
 
 def test_production_knobs_need_no_opt_in(monkeypatch):

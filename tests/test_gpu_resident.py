@@ -283,3 +283,42 @@ def test_concurrent_walks_share_one_copy(device, tmp_path):
     assert len(results) == 6 and all(results.values()), results
     assert device.resident()[0] == 1
     del recs
+
+
+def test_budget_evicts_least_recently_used_and_refuses_too_large(hooked_device, tmp_path):
+    """IRIS_RESIDENT_BUDGET_MB (test hook) caps what the copies may hold, standing in for a full
+    device: with room for one of two 160-MB files, walking the second evicts the first (least
+    recently used) and walking the first again evicts the second; a 288-MB file is refused (it
+    uploads every walk and iris_config says why) and the copy in place stays.  Rows equal the
+    oracle's throughout."""
+    kind, n, nbig = ih.KIND_MASKS, 100_000, 180_000
+    dev = hooked_device(IRIS_RESIDENT_BUDGET_MB=250)
+    files = []
+    for i, cnt in enumerate((n, n, nbig)):
+        p = tmp_path / f"f{i}.masks"
+        h = gen(kind, SEED + 30 + i, cnt)
+        h.tofile(p)
+        files.append((h, mapped(p, kind, cnt)))
+    eng, want_fn = engine_and_oracle(dev, kind, SEED + 33)
+    wants = [want_fn(h) for h, _ in files]
+    dev.set_profiling(True)
+    try:
+        with eng:
+            def walk_uploads(i):
+                dev.reset_stats()
+                assert (walk(eng, files[i][1]) == wants[i]).all()
+                dev.synchronize()
+                return uploads(dev)
+
+            assert walk_uploads(0) > 0 and dev.resident()[0] == 1
+            assert walk_uploads(0) == 0
+            assert walk_uploads(1) > 0 and dev.resident()[0] == 1  # file 0's copy evicted
+            assert walk_uploads(1) == 0
+            assert walk_uploads(0) > 0 and dev.resident()[0] == 1  # and back
+            calls = -(-nbig // CHUNK)
+            assert walk_uploads(2) >= calls and walk_uploads(2) >= calls  # refused: uploads per call
+            assert "does not fit" in dev.config()["resident_skip"], dev.config()
+            assert dev.resident()[0] == 1 and walk_uploads(0) == 0  # file 0's copy stayed
+    finally:
+        dev.set_profiling(False)
+    del files
