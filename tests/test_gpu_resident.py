@@ -317,7 +317,7 @@ def test_budget_evicts_least_recently_used_and_refuses_too_large(hooked_device, 
             assert walk_uploads(0) > 0 and dev.resident()[0] == 1  # and back
             calls = -(-nbig // CHUNK)
             assert walk_uploads(2) >= calls and walk_uploads(2) >= calls  # refused: uploads per call
-            assert "does not fit" in dev.config()["resident_skip"], dev.config()
+            assert "does_not_fit" in dev.config()["resident_skip"], dev.config()  # spaces show as _
             assert dev.resident()[0] == 1 and walk_uploads(0) == 0  # file 0's copy stayed
     finally:
         dev.set_profiling(False)
