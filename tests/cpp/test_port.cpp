@@ -2,6 +2,10 @@
 // (include/iris_hip.hpp) so they run against libiris_hip.so unchanged in
 // meaning.  Each case cites the Rust test it ports; the GPU cases run the
 // engines / arch kernels on an MI355X.  Usage: test_port cpu|gpu|all
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <unistd.h>
+
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -275,6 +279,44 @@ std::vector<Case> cases() {
                  for (std::size_t i = a; i < b; i += 13)
                      for (int k = 0; k < 31; ++k) CHECK(out[i - a][k] == q.mask.rotated(k - 15).dot(masks[i]));
              }
+         }},
+        // the participant / resolver loop exactly as the reference has it (src/main.rs:386-391,
+        // 426-431): the record file mapped read-only and shared (memmap2's Mmap::map), chunks of the
+        // mapping handed to batch_process, no attach call -- served from the device's copy of the file
+        {"main::mapped_file_chunks", true, [] {
+             const Template q = gen_template();
+             std::vector<Bits> masks;
+             for (int i = 0; i < 1000; ++i) masks.push_back(gen_bits());
+             char path[] = "/tmp/iris_port_XXXXXX";
+             const int fd = mkstemp(path);
+             CHECK(fd >= 0);
+             if (fd < 0) return;
+             const size_t bytes = masks.size() * sizeof(Bits);
+             CHECK(write(fd, masks.data(), bytes) == (ssize_t)bytes);
+             void *map = mmap(nullptr, bytes, PROT_READ, MAP_SHARED, fd, 0);
+             close(fd);
+             CHECK(map != MAP_FAILED);
+             if (map != MAP_FAILED) {
+                 const Bits *recs = static_cast<const Bits *>(map);
+                 Device &dev = Device::default_device();
+                 check(iris_device_drop_resident(dev.handle()));
+                 for (int walk = 0; walk < 2; ++walk) {
+                     MasksEngine eng(q.mask, dev);  // one engine per request
+                     for (std::size_t a = 0; a < masks.size(); a += 200) {
+                         const std::size_t b = std::min(masks.size(), a + 200);
+                         std::vector<Rotations> out(b - a);
+                         check(iris_engine_batch_process_host(eng.handle(), recs + a, b - a, out[0].data()));
+                         for (std::size_t i = a; i < b; i += 17)
+                             for (int k = 0; k < 31; ++k) CHECK(out[i - a][k] == q.mask.rotated(k - 15).dot(masks[i]));
+                     }
+                 }
+                 char cfg[1024];
+                 check(iris_config(dev.handle(), cfg, sizeof cfg, nullptr));
+                 CHECK(std::string(cfg).find("resident=1/") != std::string::npos);
+                 check(iris_device_drop_resident(dev.handle()));
+                 munmap(map, bytes);
+             }
+             unlink(path);
          }},
         // the resolver's cross-participant minimum (src/main.rs:616-621) over 5 logical shards
         {"main::sharded_search", true, [] {
