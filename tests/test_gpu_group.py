@@ -315,137 +315,78 @@ def test_group_missing_peer_fails_within_bound(tmp_path):
     assert wall < 120, wall  # the child exited with the abandoned init still pending
 
 
-@pytest.mark.parametrize("side", ["plain", "delayed"])
-def test_group_async_out_of_order(group, hooked_group, side):
-    """Pipelined searches, waited out of order; "delayed": every all-gather is held back by the
-    IRIS_GROUP_DELAY_US hook, so searches k + 4, k + 8 (the send-slot ring) run their kernels
-    before search k's winners are sent -- each must still get its own answer."""
-    g = group if side == "plain" else hooked_group(IRIS_GROUP_DELAY_US=DELAY_US)
-    got, want = async_out_of_order(g)
-    for k, (best, idx) in enumerate(want):
-        assert same(got[k], best, idx) and idx == 1000 + 4100 * k, (k, got[k], idx)
+TWO_RANK_CHILD = r"""
+import json, os, sys, time
+import iris_hip as ih
 
-
-def test_group_delay_hook_reaches_the_race_window(hooked_group):
-    """The same run with the exchange-buffer ordering dropped (IRIS_GROUP_UNORDERED, test-only):
-    later searches overwrite the winners of earlier ones before they are sent, so some answers
-    are wrong -- the delayed test above exercises the write-after-read hazard it guards."""
-    g = hooked_group(IRIS_GROUP_DELAY_US=DELAY_US, IRIS_GROUP_UNORDERED=1)
-    got, want = async_out_of_order(g)
-    wrong = [k for k, (best, idx) in enumerate(want) if not same(got[k], best, idx)]
-    assert wrong, "the delayed all-gathers never met a reused send slot"
-
-
-@pytest.mark.parametrize("layout", [ih.LAYOUT_LANES])
-def test_group_other_layouts(group, layout):
-    n = 3001
-    ref = oc.gen_templates(SEED, 0, n)
-    query = oc.gen_templates(SEED + 4, 0, 1)[0]
-    with ih.GroupDatabase(group, ih.KIND_TEMPLATES, n, layout, shards_per_device=3) as gdb:
-        gdb.generate(SEED)
-        gdb.write(2999, planted(query, 15, 0x11)[None, :])
-        ref[2999] = planted(query, 15, 0x11)
-        best, idx = oracle_best(query, ref)
-        m = gdb.search(query)
-        assert same(m, best, idx) and idx == 2999 and m.rotation == 15
-
-
-@pytest.mark.parametrize("nq", [2, 3, 9])
-def test_group_batch_search(group, device, nq):
-    n, spd = 6000, 3
-    ref = oc.gen_templates(SEED, 0, n)
-    qs = oc.gen_templates(SEED + 20, 0, nq)
-    with ih.GroupDatabase(group, ih.KIND_TEMPLATES, n, shards_per_device=spd) as gdb:
-        gdb.generate(SEED)
-        sites = [gdb.shard(k % spd)[0] + 17 * k + 3 for k in range(nq)]
-        for k, s in enumerate(sites):
-            if k % 2 == 0:  # every other query gets a planted answer
-                rec = planted(qs[k], (k % 31) - 15, 0x5)
-                gdb.write(s, rec[None, :])
-                ref[s] = rec
-        got = gdb.batch_search(qs)
-        for k, q in enumerate(qs):
-            best, idx = oracle_best(q, ref)
-            assert same(got[k], best, idx), (k, got[k], best, idx)
-
-
-def test_group_write_read_across_shards_and_load_file(group, tmp_path):
-    n, spd = 2500, 4
-    rng = np.random.default_rng(5)
-    recs = rng.integers(0, 2**64, (n, 400), dtype=np.uint64)
-    path = tmp_path / "t.templates"
-    recs.tofile(path)
-    with ih.GroupDatabase(group, ih.KIND_TEMPLATES, n - 100, shards_per_device=spd) as gdb:
-        gdb.load_file(path, first=100)
-        assert (gdb.read(0, n - 100) == recs[100:]).all()
-        a, b = gdb.shard(2)[0] - 3, gdb.shard(2)[0] + 4  # a range across a shard boundary
-        gdb.write(a, recs[:b - a])
-        assert (gdb.read(a, b - a) == recs[:b - a]).all()
-        query = recs[7]
-        best, idx = oracle_best(query, gdb.read(0, n - 100))
-        assert same(gdb.search(query), best, idx)
-    with ih.GroupDatabase(group, ih.KIND_TEMPLATES, n, shards_per_device=spd) as gdb:
-        with pytest.raises(ih.IrisError):
-            gdb.load_file(path, first=1)  # the file holds fewer than first + total records
-
-
-def test_group_rejects_duplicate_device_and_bad_args():
-    with pytest.raises(ih.IrisError):
-        ih.Group([0, 0])
-    with ih.Group([0]) as g:
-        with pytest.raises(ih.IrisError):
-            ih.GroupDatabase(g, ih.KIND_TEMPLATES, 10, shards_per_device=0)
-        with ih.GroupDatabase(g, ih.KIND_MASKS, 10) as gdb:
-            with pytest.raises(ih.IrisError):
-                gdb.search(oc.gen_templates(1, 0, 1)[0])
-
-
-def test_group_single_rank_communicator():
-    """The multi-process form (non-blocking ncclCommInitRankConfig) with one rank: what each
-    torchrun rank of bench.py builds; RCCL itself reports one rank on this GPU."""
+rank, idfile = int(sys.argv[1]), sys.argv[2]
+if rank == 0:
     uid = ih.Group.unique_id()
-    assert len(uid) == 128
-    n = 3000
-    ref = oc.gen_templates(SEED, 0, n)
-    query = ref[1234].copy()
-    query[5] ^= np.uint64(0xFF)
-    with ih.Group.rank(0, 1, 0, uid) as g:
-        assert (g.local_devices, g.ranks, g.first_rank) == (1, 1, 0)
-        assert g.rccl_nranks == 1 and len(g.rccl_devices) == 1 and ":" in g.rccl_devices[0]
-        with ih.GroupDatabase(g, ih.KIND_TEMPLATES, n, shards_per_device=2) as gdb:
-            gdb.generate(SEED)
-            best, idx = oracle_best(query, ref)
-            assert same(gdb.search(query), best, idx) and idx == 1234
+    with open(idfile + ".tmp", "wb") as f:
+        f.write(uid)
+    os.rename(idfile + ".tmp", idfile)
+else:
+    t = time.monotonic()
+    while not os.path.exists(idfile) and time.monotonic() - t < 60:
+        time.sleep(0.01)
+    with open(idfile, "rb") as f:
+        uid = f.read()
+t0 = time.monotonic()
+err = None
+try:
+    ih.Group.rank(0, 2, rank, uid)  # both ranks on device 0
+except ih.IrisError as e:
+    err = str(e)
+dt = time.monotonic() - t0
+with ih.Group.rank(0, 1, 0, ih.Group.unique_id()) as g:  # the device still forms a group and searches
+    with ih.GroupDatabase(g, ih.KIND_TEMPLATES, 3000) as gdb:
+        gdb.generate(7)
+        m = gdb.search(gdb.read(1234, 1)[0])
+print(json.dumps({"err": err, "dt": dt, "found": [int(m.index), m.distance]}))
+sys.stdout.flush()
+"""
 
 
-def test_group_missing_peer_fails_within_bound(monkeypatch, device):
-    """A 2-rank group whose second rank never comes: forming it must fail within the bound
-    (IRIS_GROUP_TIMEOUT_MS, read when the group's device opens) instead of hanging in RCCL's
-    init, and the GPU then opens, forms a 1-rank group and searches normally."""
+def test_group_two_ranks_bootstrap_then_refuse_one_device(tmp_path):
+    """Two processes form one 2-rank group on the box's single GPU: RCCL's bootstrap must connect
+    the ranks (each then finds the other's device in the exchanged peer table -- "Duplicate GPU
+    detected: rank 0 and rank 1", which only a completed bootstrap can report) and refuses two
+    ranks on one device; each create_rank fails with RCCL's error well inside the bound, not a
+    hang, and each process's GPU then forms a 1-rank group and searches normally.  The one
+    multi-process RCCL exchange a one-GPU box can run."""
+    import json
+    import os
+    import subprocess
+    import sys
     import time
 
-    uid = ih.Group.unique_id()
-    bound_ms = 6000
-    with monkeypatch.context() as m:
-        m.setenv("IRIS_GROUP_TIMEOUT_MS", str(bound_ms))
-        t0 = time.monotonic()
-        with pytest.raises(ih.IrisError) as ex:
-            ih.Group.rank(0, 2, 0, uid)
-        dt = time.monotonic() - t0
-    assert dt < bound_ms / 1e3 + 20, dt
-    assert "did not complete" in str(ex.value) or "RCCL" in str(ex.value), ex.value
-    n = 2000
-    ref = oc.gen_templates(SEED + 3, 0, n)
-    query = ref[777].copy()
-    best, idx = oracle_best(query, ref)
-    with ih.Database(device, ih.KIND_TEMPLATES, n) as db:
-        db.append(ref)
-        with ih.TemplateEngine(device, query) as eng:
-            assert same(eng.search(db), best, idx)
-    with ih.Group.rank(0, 1, 0, ih.Group.unique_id()) as g:
-        with ih.GroupDatabase(g, ih.KIND_TEMPLATES, n) as gdb:
-            gdb.write(0, ref)
-            assert same(gdb.search(query), best, idx)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, IRIS_GROUP_TIMEOUT_MS="30000", NCCL_DEBUG="WARN",
+               PYTHONPATH=os.pathsep.join([os.path.join(root, "mpc-iris-code_amd"), root]))
+    script = tmp_path / "rank.py"
+    script.write_text(TWO_RANK_CHILD)
+    idfile = str(tmp_path / "uid")
+    t0 = time.monotonic()
+    procs = [subprocess.Popen([sys.executable, str(script), str(r), idfile], cwd=root, env=env,
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(2)]
+    outs = []
+    try:
+        for p in procs:
+            outs.append(p.communicate(timeout=150))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    assert time.monotonic() - t0 < 150
+    logs = "".join(o + e for o, e in outs)  # RCCL's NCCL_DEBUG lines go to stdout
+    for p, (out, err) in zip(procs, outs):
+        assert p.returncode == 0, (p.returncode, err[-3000:])
+        d = json.loads([ln for ln in out.splitlines() if ln.startswith("{")][-1])
+        assert d["err"] and "ncclCommInitRank" in d["err"] and "did not complete" not in d["err"], d
+        assert d["dt"] < 30, d
+        assert d["found"] == [1234, 0.0], d
+    assert "Duplicate GPU detected" in logs, logs[-3000:]
 
 
 @pytest.mark.parametrize("side", ["plain", "delayed"])
