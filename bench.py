@@ -282,7 +282,9 @@ def cpu_baseline(args, reserve=0):
         passes, t = _time_passes(run, secs)
         value, unit = ROT * n * nq * passes / t, "template comparisons/s"
         sample = (f"{passes} passes of {nq} quer{'y' if nq == 1 else 'ies'} x 31 rotations x {n} templates "
-                  "(Template::distance per pair + argmin, src/template.rs:43-64, src/main.rs:616-621)")
+                  "(the fractional Hamming of src/template.rs:49-64 per pair and rotation + argmin, src/main.rs:616-621; "
+                  "the 31 rotated queries are built once per query, engine-style, rather than per pair as "
+                  "Template::distance does, src/template.rs:43-47 -- a stronger-than-reference CPU baseline)")
     elif wl in ("masks", "host-masks"):
         n = 2_000_000  # 3.2 GB of masks
         db = oc.gen_masks(SEED, 0, n)
@@ -315,23 +317,25 @@ def cpu_baseline(args, reserve=0):
         d, i = np.zeros(1, np.float64), np.zeros(1, np.uint64)
 
         def run():
-            oc_lib.orc_resolver_combine(oc._p(shares), args.parties, oc._p(denoms), n, oc._p(out))
+            # the share sum + decode split over the threads (rayon into_par_iter, src/main.rs:597-612);
+            # the argmin stays sequential (src/main.rs:616-621)
+            oc_lib.orc_resolver_combine(oc._p(shares), args.parties, oc._p(denoms), n, oc._p(out), threads)
             oc_lib.orc_argmin(oc._p(out), n, oc._p(d), oc._p(i))
 
         passes, t = _time_passes(run, secs)
-        threads = 1  # the combine loop is the reference's sequential scan
         value, unit = n * passes / t, "records/s"
-        sample = f"{passes} passes of the share sum + decode + argmin (src/main.rs:597-621) over {n} entries"
+        sample = (f"{passes} passes of the share sum + decode (parallel over entries, as the reference's rayon "
+                  f"into_par_iter, src/main.rs:597-612) + sequential argmin (src/main.rs:616-621) over {n} entries")
         if wl == "resolve-masks":
             sample += " (the masks engine's denominators are not included)"
     elif wl == "prepare":
-        n = 2000
+        n = 2000 * threads
         tmpl = oc.gen_templates(SEED, 0, n)
         passes, t = _time_passes(lambda: oc.prepare_shares(tmpl, bytes(range(32)), parties=args.parties,
-                                                           rounds=args.rounds), secs)
-        threads = 1
+                                                           rounds=args.rounds, threads=threads), secs)
         value, unit = n * passes / t, "templates/s"
-        sample = f"{passes} passes of encode + EncodedBits::share({args.parties}) (ChaCha{args.rounds}) over {n} templates"
+        sample = (f"{passes} passes of encode + EncodedBits::share({args.parties}) (ChaCha{args.rounds}) over {n} "
+                  "templates, parallel over templates as the reference's rayon par_iter (src/main.rs:337-344)")
     elif wl == "criterion":
         threads = 1  # criterion runs the loop on one thread (src/arch/mod.rs:34-41)
         shapes = {}
@@ -452,11 +456,12 @@ class Ranks:
         self.group = None
         self.backend = None
         self.ordinal = 0
+        self.group_form_s = None
         if args.single_process:
             if "WORLD_SIZE" in os.environ and self.world > 1:
                 raise SystemExit("error: --single-process drives every GPU from one process; do not launch ranks")
             self.world, self.rank = 1, 0
-            self.backend = "rccl (library group, one process: non-blocking ncclCommInitRankConfig per device)"
+            self.backend = "rccl (library group, one process: helper-thread ncclCommInitRank (bounded) per device)"
             return
         if self.world != args.gpus:
             raise SystemExit(f"error: --gpus {args.gpus} but the launcher started WORLD_SIZE={self.world} ranks")
@@ -486,7 +491,7 @@ class Ranks:
             raise SystemExit(f"error: process group has {dist.get_world_size()} ranks, --gpus {args.gpus}")
         self.dist = dist
         self.backend = ("gloo" if backend == "gloo" else
-                        "rccl (library group, non-blocking ncclCommInitRankConfig; gloo control)")
+                        "rccl (library group, helper-thread ncclCommInitRank (bounded); gloo control)")
         self.rccl = backend == "nccl"
 
     def join_group(self, args):
@@ -494,12 +499,15 @@ class Ranks:
         # one node (the bench contract): RCCL's bootstrap sockets over loopback; the data path is
         # xGMI peer-to-peer either way (a caller's own setting wins)
         os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+        t0 = time.perf_counter()
         if args.single_process:
             self.group = ih.Group(list(range(args.gpus)))
         elif self.dist is not None and self.rccl:
             box = [ih.Group.unique_id() if self.rank == 0 else None]
             self.dist.broadcast_object_list(box, src=0)
             self.group = ih.Group.rank(self.ordinal, self.world, self.rank, box[0])
+        # wall time of forming the group (RCCL init + the bus-id all-gather), max over ranks below
+        self.group_form_s = time.perf_counter() - t0 if self.group is not None else None
         return self.group
 
     def barrier(self):
@@ -623,32 +631,55 @@ def run_aux(args, dev):
         workload = "raw template file (page cache) -> DMA from registered page-cache windows -> TILES transpose (src/main.rs:386-400)"
     elif args.workload in ("host-shares", "host-masks"):
         shares_wl = args.workload == "host-shares"
-        n = min(args.n_per_gpu, 200_000 if shares_wl else 2_000_000)  # 5.1 GB / 3.2 GB of host records
+        kind = ih.KIND_SHARES if shares_wl else ih.KIND_MASKS
+        rec_size = 25600 if shares_wl else 1600
+        file_walk = args.mmap and not args.attached
+        if file_walk:
+            # the participant / resolver walk their whole file per request (src/main.rs:426-431,
+            # 511-516; "3 million entries", specification.ipynb:173): 1M shares (25.6 GB) / 3M masks
+            # (4.8 GB) by default, fewer only if the temp directory's file system has no room for them
+            n = args.n_per_gpu if args.n_explicit else (1_000_000 if shares_wl else 3_000_000)
+            import shutil
+            room = shutil.disk_usage(tempfile.gettempdir()).free - (4 << 30)
+            if n * rec_size > room:
+                n = max(20_000, room // rec_size // 20_000 * 20_000)
+                extra["file_records_reduced_to_fit"] = {"free_bytes": room + (4 << 30), "records": n}
+        else:
+            n = min(args.n_per_gpu, 200_000 if shares_wl else 2_000_000)  # 5.1 GB / 3.2 GB of host records
         qt = gen_records(dev, ih.KIND_TEMPLATES, 1, SEED + 1)[0]
         # one engine per walk, as the participant and the resolver build one per request
         # (src/main.rs:427, 512): no walk is served from rows an earlier walk computed
+        dt, width = (np.uint16, 12800) if shares_wl else (np.uint64, 200)
         if shares_wl:
-            host = rng.integers(0, 65536, (n, 12800), dtype=np.uint16)
             qenc = ih.encode(ih.Template.from_array(qt))
 
             def new_engine():
                 return ih.DistanceEngine(dev, qenc)
         else:
-            host = gen_records(dev, ih.KIND_MASKS, n, SEED)
-
             def new_engine():
                 return ih.MasksEngine(dev, qt[200:])
-        hout = np.empty((n, ROT), np.uint16)
-        chunk = args.chunk or (20_000 if (args.attached or args.mmap) else n)
-        kind = ih.KIND_SHARES if shares_wl else ih.KIND_MASKS
-        adb = None
         mpath = None
         if args.mmap:  # the record file the participant / resolver maps (page-cached after the write)
+            # written from the on-device generator 1 GB at a time (uniform u16 shares / mask bits)
             mpath = pathlib.Path(tempfile.gettempdir()) / f"iris_bench_{os.getpid()}.records"
-            host.tofile(mpath)
-            arr = host
-            host = np.memmap(mpath, dtype=arr.dtype, mode="r", shape=arr.shape)
-            del arr
+            t_gen = time.perf_counter()
+            per = max(1, (1 << 30) // rec_size)
+            with ih.Database(dev, kind, min(n, per)) as g, open(mpath, "wb") as f:
+                for a in range(0, n, per):
+                    m = min(per, n - a)
+                    g.truncate(0)
+                    g.generate(m, SEED, global_index0=a)
+                    g.read(0, m).tofile(f)
+            extra["file"] = {"records": n, "bytes": n * rec_size, "write_s": time.perf_counter() - t_gen}
+            host = np.memmap(mpath, dtype=dt, mode="r", shape=(n, width))
+        elif shares_wl:
+            host = rng.integers(0, 65536, (n, 12800), dtype=np.uint16)
+        else:
+            host = gen_records(dev, ih.KIND_MASKS, n, SEED)
+        hout = np.empty((n, ROT), np.uint16)
+        chunk = args.chunk or (20_000 if (args.attached or args.mmap) else n)
+        adb = None
+        if args.mmap:
             # the first walk makes the file resident (granule uploads): timed apart from the steps
             t_first = time.perf_counter()
             with new_engine() as eng:
@@ -663,9 +694,14 @@ def run_aux(args, dev):
             adb.attach_host(host)
             extra["attach_s"] = time.perf_counter() - t_att
 
+        first_calls = []  # engine creation + the walk's first call (a request's first rows)
+
         def step():
+            t1 = time.perf_counter()
             with new_engine() as eng:
-                for a in range(0, n, chunk):
+                eng.batch_process(hout[0:chunk], host[0:chunk])
+                first_calls.append(time.perf_counter() - t1)
+                for a in range(chunk, n, chunk):
                     eng.batch_process(hout[a:a + chunk], host[a:a + chunk])
 
         kname, unit = ("shares" if shares_wl else "masks"), "records/s"
@@ -743,17 +779,34 @@ def run_aux(args, dev):
     dev.reset_stats()
     dev.set_profiling(not separate)
     dev.synchronize()
+    if separate:
+        first_calls.clear()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         m = step()
     dev.synchronize()
     elapsed = time.perf_counter() - t0
     if separate:
+        fc = sorted(first_calls)
+        extra["first_call_ms"] = {"median": fc[len(fc) // 2] * 1e3, "max": fc[-1] * 1e3,
+                                  "is": "engine creation + the walk's first batch_process call, timed steps"}
+        dev.reset_stats()
         dev.set_profiling(True)
         for _ in range(args.steps):
             step()
         dev.synchronize()
         extra["kernel_times_from"] = "a separate profiled pass of the same steps (the timed steps run unprofiled)"
+        ra = [int(x) for x in dev.config().get("readahead_windows", "0/0/0").split("/")]
+        big_items, big_ms = dev.kernel_stats_largest("shares" if shares_wl else "masks")
+        extra["readahead"] = {
+            "launches_per_walk": ra[0] / args.steps, "records_computed_per_walk": ra[1] / args.steps,
+            "largest_window_records": ra[2],
+            "largest_launch": {"records": big_items, "kernel_ms": big_ms,
+                               "hbm_frac": (big_items * rec_bytes / (big_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
+                                            if big_ms else None)},
+            "windows": "1, 2, 4, ... chunks up to 64 MB of rows, at most half of what is left of the walk",
+            "rows_over_host_link": ("packed: 32 B per record (base + 31 byte offsets, full-row escape)"
+                                    if not shares_wl else "[u16;31]: 62 B per record")}
     dev.set_profiling(False)
     launches, kms, items = dev.kernel_stats(kname)
     achieved = rec_bytes * items / (kms * 1e-3) / 1e9
@@ -883,6 +936,7 @@ def main():
         return dry_run(args, ranks)
     world_gpus = args.gpus  # GPUs in the run (ranks x 1, or one process x --gpus)
     rank = ranks.rank
+    args.n_explicit = args.n_per_gpu is not None
     if args.n_per_gpu is None:  # configs[1] at N=1; configs[4] (100M over 8 GPUs) at N=8
         args.n_per_gpu = 12_500_000 if (args.workload == "search" and world_gpus > 1) else 10_000_000
     n = args.n_per_gpu
@@ -902,6 +956,7 @@ def main():
 
     # the library device group: the search / batch exchange of every multi-GPU run (RCCL)
     group = ranks.join_group(args) if args.workload in ("search", "batch") else None
+    group_form_s = ranks.max_over_ranks(ranks.group_form_s) if ranks.group_form_s is not None else None
     if group is not None:
         devs = group.devices
     else:
@@ -1144,6 +1199,8 @@ def main():
             # device PCI bus id gathered over that communicator), not torch's view
             "rccl_nranks": group.rccl_nranks if group is not None else None,
             "rccl_devices": group.rccl_devices if group is not None else None,
+            "group_form_s": group_form_s,
+            "rccl_init_timeout_ms": (int(dev.config()["group_init_timeout_ms"]) if group is not None else None),
             "processes": ranks.world,
             "backend": ranks.backend,
             "launcher": launcher_name() if not args.single_process else "none (one process, library device group)",

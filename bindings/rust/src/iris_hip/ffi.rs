@@ -115,10 +115,17 @@ extern "C" {
         total_ms: *mut f64,
         items: *mut u64,
     ) -> c_int;
+    pub fn iris_device_kernel_stats_largest(
+        dev: *mut IrisDevice,
+        kernel: *const c_char,
+        items: *mut u64,
+        ms: *mut f64,
+    ) -> c_int;
     pub fn iris_device_reset_stats(dev: *mut IrisDevice) -> c_int;
     pub fn iris_device_alloc(dev: *mut IrisDevice, bytes: usize, ptr: *mut *mut c_void) -> c_int;
     pub fn iris_device_free(dev: *mut IrisDevice, ptr: *mut c_void) -> c_int;
     pub fn iris_device_drop_resident(dev: *mut IrisDevice) -> c_int;
+    pub fn iris_device_drop_resident_range(dev: *mut IrisDevice, ptr: *const c_void) -> c_int;
     pub fn iris_memcpy_d2h(dev: *mut IrisDevice, host: *mut c_void, device: *const c_void, bytes: usize) -> c_int;
     pub fn iris_memcpy_h2d(dev: *mut IrisDevice, device: *mut c_void, host: *const c_void, bytes: usize) -> c_int;
 

@@ -97,13 +97,20 @@ const char *iris_version(void);
  * IRIS_GROUP_TIMEOUT_MS, IRIS_COPY_HELPERS (process-wide).  Test-only hooks
  * (IRIS_TILES_PER_WAVE, IRIS_FUSED_REDUCE, IRIS_BATCH_KERNEL, IRIS_SCHEDULE,
  * IRIS_LOAD_PREAD, IRIS_LOAD_WINDOWS, IRIS_GROUP_DELAY_US, IRIS_GROUP_STALL,
- * IRIS_GROUP_UNORDERED, IRIS_UPLOAD, IRIS_READAHEAD_WINDOW, IRIS_RESIDENT_BUDGET_MB)
- * take effect only with IRIS_TEST_HOOKS=1;
+ * IRIS_GROUP_UNORDERED, IRIS_UPLOAD, IRIS_READAHEAD_WINDOW, IRIS_RESIDENT_BUDGET_MB,
+ * IRIS_READAHEAD_PACKED) take effect only with IRIS_TEST_HOOKS=1;
  * otherwise they are ignored and listed as "ignored=...".  With dev != NULL the
  * device's own facts follow: numa_node= (host NUMA node of its PCI function, -1
  * unknown), upload_gbps=P/R (recent rates of large writes through the pinned
- * slots / the runtime's copy, GB/s; 0 = not measured yet) and resident= (the
- * record files it keeps resident for host-slice calls: count and bytes). */
+ * slots / the runtime's copy, GB/s; 0 = not measured yet), resident= (the
+ * record files it keeps resident for host-slice calls: count and bytes) and
+ * readahead_windows=L/R/M (read-ahead launches of host-output engine calls since
+ * the last iris_device_reset_stats, the records they computed, the largest
+ * window in records) and abandoned_inits=P/T (RCCL communicator inits of this
+ * device that a group formation gave up on at its bound: still pending inside
+ * RCCL / all in this process; while one is pending the device forms no further
+ * multi-rank group in this process).  group_init_timeout_ms= is the bound of
+ * forming a group (IRIS_GROUP_TIMEOUT_MS, else 120000). */
 int iris_config(const iris_device_t *dev, char *buf, size_t len, size_t *needed);
 
 /* --------------------------------------------------------------- devices */
@@ -124,6 +131,10 @@ int iris_device_memory(iris_device_t *dev, size_t *free_bytes, size_t *total_byt
 int iris_device_set_profiling(iris_device_t *dev, int enabled);
 int iris_device_kernel_stats(iris_device_t *dev, const char *kernel, uint64_t *launches,
                              double *total_ms, uint64_t *items);
+/* The largest launch of the named kernel family since the last reset: its items
+ * (records) and its duration (ms; the latest of equal-sized ones); 0 / 0 if none.
+ * A walk's biggest read-ahead window, for its HBM fraction. */
+int iris_device_kernel_stats_largest(iris_device_t *dev, const char *kernel, uint64_t *items, double *ms);
 int iris_device_reset_stats(iris_device_t *dev);
 /* Raw device memory for outputs that stay on the GPU (e.g. per-template distances). */
 int iris_device_alloc(iris_device_t *dev, size_t bytes, void **ptr);
@@ -265,6 +276,12 @@ int iris_engine_batch_process_host(iris_engine_t *engine, const void *db, uint64
 /* Frees the device's resident file copies (a failing iris_db_create does so too
  * before it retries); iris_config reports them as resident=count/bytes. */
 int iris_device_drop_resident(iris_device_t *dev);
+/* Frees the resident copy of the file mapping that holds host address ptr (of any
+ * record kind), and forgets a refusal of that mapping: the next call on its slices
+ * copies the file afresh.  For a caller that changed the file in a way the per-call
+ * check does not see (stores through a writable shared mapping into pages already
+ * dirty, see iris_engine_batch_process_host).  No copy there: nothing to do (0). */
+int iris_device_drop_resident_range(iris_device_t *dev, const void *ptr);
 
 /* Template engine, per template and rotation k: num = popcount((qp^ep)&qm&em),
  * den = popcount(qm&em) with q rotated by k-15 (src/template.rs:49-64).
@@ -387,7 +404,11 @@ int iris_match_merge(const iris_match_t *records, uint64_t count, iris_match_t *
  * arrived) runs on a helper thread waited for at most IRIS_GROUP_TIMEOUT_MS
  * (default 120 s); if a peer never arrives the call fails (IRIS_E_HIP) instead
  * of hanging, the pending init is abandoned (it aborts its communicators should
- * it ever complete) and the device stays usable.  A formed group all-gathers
+ * it ever complete) and the device stays usable.  While such an init is still
+ * pending, a multi-rank group on that device is refused at once (IRIS_E_HIP:
+ * start a fresh process; iris_config's abandoned_inits counts them), so failed
+ * formations cannot pile up in a long-lived process; 1-rank groups still form.
+ * A formed group all-gathers
  * every rank's PCI bus id over its communicators (iris_group_rccl_info).
  * Group calls are blocking and serialised per group, like the device calls.
  *

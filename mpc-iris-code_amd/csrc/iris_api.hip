@@ -199,7 +199,7 @@ constexpr uint64_t kU16Chunk = 4ull << 20;  // records per engine launch of the 
 // o, on `stream` (default: the device stream); nothing waits.  sig (TILES only): the kernel's
 // completion word, if the kernel chosen signals one (sig->armed).
 int enqueue_u16_engine(iris_engine *e, const iris_db *db, uint64_t first, uint64_t n, uint16_t *o,
-                       hipStream_t stream = nullptr, DoneSignal *sig = nullptr) {
+                       hipStream_t stream = nullptr, DoneSignal *sig = nullptr, bool packed = false) {
     iris_device *d = e->dev;
     if (!stream) stream = d->stream;
     LaunchRange r{first, n};
@@ -207,7 +207,7 @@ int enqueue_u16_engine(iris_engine *e, const iris_db *db, uint64_t first, uint64
     if (sig) sig->armed = false;
     if (e->kind == IRIS_KIND_MASKS)
         return timed(d, "masks", n, [&] {
-            return tiles ? launch_masks_mfma(d->hooks, stream, db->data, e->qfrag, r, o, sig)
+            return tiles ? launch_masks_mfma(d->hooks, stream, db->data, e->qfrag, r, o, sig, packed)
                          : launch_masks(stream, db->data, e->qtab, r, o);
         }, stream);
     return timed(d, "shares", n, [&] {
@@ -240,20 +240,34 @@ int run_u16_engine(iris_engine *e, const iris_db *db, uint64_t first, uint64_t n
 
 // calls of at most this many records (62 MB of rows per buffer) go through the read-ahead
 constexpr uint64_t kReadaheadMax = 1ull << 20;
-// A walk's read-ahead windows: up to kWindowMax consecutive chunks computed by one launch, enough to
-// read ~kWindowBytes of records (a 20 000-share chunk reads 512 MB in ~99 us, ~25 us of it the
-// launch's ramp and drain), with at most kWindowRowsMax of rows per buffer.
-constexpr uint64_t kWindowMax = 8;
-constexpr size_t kWindowBytes = 2ull << 30;
+// A walk's read-ahead windows grow geometrically: the walk's first window is one chunk, each later
+// one twice the chunks of the window before it, up to kWindowRowsMax of rows per buffer (~1M
+// records), and never more than half of what is left of the resident run (at least one chunk).  A
+// launch costs a ramp and a drain (~74 us of a 100k-share window's 446 us, profiles/
+// r05u_shares_window_kernels.txt), so a long walk's big windows run at the full-launch rate; the
+// first calls keep the latency of small ones, and the walk's tail windows shrink so that the rows
+// of its last window (copied out after the device is done) are few.
 constexpr size_t kWindowRowsMax = 64ull << 20;
 
-// Records a walk's window starting at a chunk of n records computes (at most `avail`).
-uint64_t window_records(const iris_db *db, uint64_t n, uint64_t avail) {
-    const size_t chunk_bytes = (size_t)n * db->k.rec_bytes;
-    uint64_t w = std::max<uint64_t>(1, (kWindowBytes + chunk_bytes - 1) / chunk_bytes);
-    w = std::min<uint64_t>(w, kWindowMax);
+// A MasksEngine window's rows cross the host link packed (store_tile_packed, iris_device.hpp): 32 B
+// per record, then an escape row of 31 u16 per record that only rows spanning more than a byte
+// use; the copy-out expands them into the caller's [u16; 31] (parallel_expand).  The resolver's
+// 20 000-mask walk is bound by its rows crossing the host link (~44 GB/s, 23 us of a 28-us call).
+constexpr size_t kPackedRecBytes = 32;
+bool ra_packed(const iris_engine *e) { return e->kind == IRIS_KIND_MASKS && e->dev->hooks.ra_packed; }
+// bytes of a read-ahead buffer per record
+size_t ra_rec_bytes(const iris_engine *e) { return ra_packed(e) ? kPackedRecBytes + kRot * 2 : kRot * 2; }
+
+uint64_t window_chunks_max(uint64_t n) { return std::max<uint64_t>(1, kWindowRowsMax / ((size_t)n * kRot * 2)); }
+
+// Records of a walk's window of chunks of n records that follows a window of `prev` records (0: the
+// walk's first window), with `avail` records left in the run.
+uint64_t window_records(const iris_db *db, uint64_t n, uint64_t prev, uint64_t avail) {
+    uint64_t w = prev ? 2 * ((prev + n - 1) / n) : 1;
+    const uint64_t left = (avail + n - 1) / n;
+    w = std::min(w, std::max<uint64_t>(1, (left + 1) / 2));
     if (db->dev->hooks.ra_window) w = db->dev->hooks.ra_window;  // test hook: a fixed window
-    w = std::min<uint64_t>(w, std::max<uint64_t>(1, kWindowRowsMax / ((size_t)n * kRot * 2)));
+    w = std::min(w, window_chunks_max(n));
     return std::min<uint64_t>(w * n, avail);
 }
 
@@ -381,7 +395,8 @@ int ra_launch(iris_engine *e, const iris_db *a, uint64_t first, uint64_t n, int 
     CHK(ensure_aux(d));
     if (!ra.computed[0])
         for (int i = 0; i < 2; ++i) HIPCHK(hipEventCreateWithFlags(&ra.computed[i], hipEventDisableTiming));
-    const size_t bytes = (size_t)n * kRot * 2;
+    const size_t rec = ra_rec_bytes(e);
+    const size_t bytes = (size_t)n * rec;
     if (bytes > ra.cap) {
         if (!grow) return 0;
         CHK(ra_wait(e));  // no kernel in flight writes either buffer
@@ -389,7 +404,7 @@ int ra_launch(iris_engine *e, const iris_db *a, uint64_t first, uint64_t n, int 
         ra.rows[0] = ra.rows[1] = nullptr;
         ra.win[0].live = ra.win[1].live = false;
         ra.cap = 0;
-        const size_t want = std::max({bytes, (size_t)reserve * kRot * 2, (size_t)4096});
+        const size_t want = std::max({bytes, (size_t)reserve * rec, (size_t)4096});
         size_t got[2] = {0, 0};
         for (int i = 0; i < 2; ++i) CHK(rows_take(d, want, &ra.rows[i], &got[i]));
         ra.cap = std::min(got[0], got[1]);
@@ -406,9 +421,12 @@ int ra_launch(iris_engine *e, const iris_db *a, uint64_t first, uint64_t n, int 
         HIPCHK(hipStreamWaitEvent(d->aux, d->ra_order, 0));
     }
     ra.win[b].live = false;
-    CHK(enqueue_u16_engine(e, a, first, n, (uint16_t *)ra.rows[b], d->aux));
+    CHK(enqueue_u16_engine(e, a, first, n, (uint16_t *)ra.rows[b], d->aux, nullptr, ra_packed(e)));
     HIPCHK(hipEventRecord(ra.computed[b], d->aux));
     ra.win[b] = Readahead::Window{a, a->version, first, n, true};
+    d->ra_launches += 1;
+    d->ra_records += n;
+    d->ra_window_max = std::max(d->ra_window_max, n);
     if (launched) *launched = true;
     return 0;
 }
@@ -434,8 +452,12 @@ int readahead_u16_call(iris_engine *e, const iris_db *a, uint64_t first, uint64_
     const bool walk = b >= 0 || (ra.last_db == a && ra.last_version == a->version && ra.last_end == first);
     if (b < 0) {  // a miss: into the buffer whose window starts earlier (the one a walk has left)
         b = !ra.win[0].live ? 0 : !ra.win[1].live ? 1 : ra.win[0].first <= ra.win[1].first ? 0 : 1;
-        const uint64_t wn = window_records(a, n, end - first);
-        CHK(ra_launch(e, a, first, walk ? wn : n, b, true, nullptr, std::max(wn, window_records(a, n, end))));
+        // a walk's window follows the one the walk was in; a random-access call computes its range
+        const uint64_t wn = walk ? window_records(a, n, ra.grow ? ra.grow : n, end - first) : n;
+        // new buffers take the walk's largest window (not reallocated under it as the windows grow)
+        const uint64_t reserve = std::min<uint64_t>(window_chunks_max(n) * n, end - first);
+        CHK(ra_launch(e, a, first, std::max(wn, n), b, true, nullptr, reserve));
+        ra.grow = std::max(wn, n);
     }
     const Readahead::Window w = ra.win[b];
     ra.last_db = a;
@@ -445,11 +467,22 @@ int readahead_u16_call(iris_engine *e, const iris_db *a, uint64_t first, uint64_
     const uint64_t next = w.first + w.n;
     if (walk && next < end) {
         const Readahead::Window &o = ra.win[b ^ 1];
-        if (!(o.live && o.db == a && o.version == a->version && o.first == next))
-            CHK(ra_launch(e, a, next, window_records(a, n, end - next), b ^ 1, false));
+        if (!(o.live && o.db == a && o.version == a->version && o.first == next)) {
+            const uint64_t nn = window_records(a, n, w.n, end - next);
+            bool launched = false;
+            CHK(ra_launch(e, a, next, nn, b ^ 1, false, &launched));
+            if (launched) ra.grow = nn;
+        }
     }
     HIPCHK(hipEventSynchronize(ra.computed[b]));
-    parallel_copy(out, (const char *)ra.rows[b] + (size_t)(first - w.first) * kRot * 2, (size_t)n * kRot * 2, d->ordinal);
+    const uint64_t at = first - w.first;
+    if (ra_packed(e)) {
+        const uint8_t *pk = (const uint8_t *)ra.rows[b];
+        parallel_expand(out, pk + at * kPackedRecBytes, (const uint16_t *)(pk + w.n * kPackedRecBytes) + at * kRot, n,
+                        d->ordinal);
+    } else {
+        parallel_copy(out, (const char *)ra.rows[b] + (size_t)at * kRot * 2, (size_t)n * kRot * 2, d->ordinal);
+    }
     if (d->profiling) fold_done(d);
     return 0;
 }
@@ -675,8 +708,15 @@ int iris_config(const iris_device_t *d, char *buf, size_t len, size_t *needed) {
             std::lock_guard<std::recursive_mutex> g(const_cast<iris_device *>(d)->mu);
             resident_stats(d, &rc, &rbytes, &via_fd);
             skip = d->resident_skip;
+            // read-ahead windows since the last iris_device_reset_stats: launches, records computed,
+            // the largest window (records)
+            s += " readahead_windows=" + std::to_string(d->ra_launches) + "/" + std::to_string(d->ra_records) + "/" +
+                 std::to_string(d->ra_window_max);
         }
         s += " resident=" + std::to_string(rc) + "/" + std::to_string(rbytes) + " resident_via_fd=" + std::to_string(via_fd);
+        uint64_t ab_pending = 0, ab_total = 0;  // RCCL inits abandoned on a formation timeout: pending/total
+        abandoned_inits(d->ordinal, &ab_pending, &ab_total);
+        s += " abandoned_inits=" + std::to_string(ab_pending) + "/" + std::to_string(ab_total);
         if (!skip.empty()) {  // one token: spaces and '=' replaced
             for (char &c : skip)
                 if (c == ' ' || c == '=') c = '_';
@@ -794,11 +834,24 @@ int iris_device_kernel_stats(iris_device_t *d, const char *kernel, uint64_t *lau
     return 0;
 }
 
+int iris_device_kernel_stats_largest(iris_device_t *d, const char *kernel, uint64_t *items, double *ms) {
+    IRIS_KEEP_DEVICE();
+    ARG(d && kernel, "NULL argument");
+    std::lock_guard<std::recursive_mutex> g(d->mu);
+    fold_done(d);
+    auto it = d->stats.find(kernel);
+    KStat s = it == d->stats.end() ? KStat{} : it->second;
+    if (items) *items = s.max_items;
+    if (ms) *ms = s.max_ms;
+    return 0;
+}
+
 int iris_device_reset_stats(iris_device_t *d) {
     IRIS_KEEP_DEVICE();
     ARG(d, "device is NULL");
     std::lock_guard<std::recursive_mutex> g(d->mu);
     d->stats.clear();
+    d->ra_launches = d->ra_records = d->ra_window_max = 0;
     return 0;
 }
 

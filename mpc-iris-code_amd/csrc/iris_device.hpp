@@ -83,6 +83,56 @@ __device__ __forceinline__ void store_tile_rows(uint16_t *__restrict__ out, uint
     }
 }
 
+// Writes one 32-record tile's MasksEngine rows in the packed form the read-ahead windows carry over
+// the host link (32 B per record instead of 62, iris_api.hip kPackedRecBytes): record i of the
+// range [first, end) at pk + 32 i holds bytes 0..30 = row[k] - 64 B and byte 31 = B, where
+// B = min_k row[k] >> 6 (den <= 12800, so B <= 200), whenever every row[k] - 64 B fits a byte;
+// otherwise byte 31 is 0xFF and the row is stored in full at esc + 31 i.  Random masks never
+// escape (the 31 rotations' counts span ~115-220); structured ones (a block of masked columns) do.
+// In the 32x32 MFMA C layout lane l holds rows k = (r & 3) + 8 (r >> 2) + 4 h, h = l >> 5, of record
+// l & 31, so its registers 4j..4j+3 are the record's bytes 8j + 4h .. +3 (record dword 2j + h); after
+// swapping two dwords with its partner lane l ^ 32, half 0 holds the record's bytes 0..15 and half 1
+// bytes 16..31, and a wave's 64 16-B stores cover a tile's 1024 B contiguously.
+template <class F>
+__device__ __forceinline__ void store_tile_packed(uint8_t *__restrict__ pk, uint16_t *__restrict__ esc, uint64_t tile_t0,
+                                                  uint64_t first, uint64_t end, bool tile_valid, int lane, F val) {
+    const int h = lane >> 5;
+    uint32_t v[16];
+    uint32_t lo = 0xFFFFu, hi = 0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int k = (r & 3) + 8 * (r >> 2) + 4 * h;
+        v[r] = val(r);
+        if (k < kRot) {
+            lo = v[r] < lo ? v[r] : lo;
+            hi = v[r] > hi ? v[r] : hi;
+        }
+    }
+    const uint32_t plo = __shfl_xor(lo, 32), phi = __shfl_xor(hi, 32);
+    lo = plo < lo ? plo : lo;
+    hi = phi > hi ? phi : hi;
+    const uint32_t b = lo >> 6, base = b << 6;
+    const bool escape = hi - base > 255u;
+    uint32_t dw[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        dw[j] = ((v[4 * j] - base) & 0xFFu) | ((v[4 * j + 1] - base) & 0xFFu) << 8 | ((v[4 * j + 2] - base) & 0xFFu) << 16 |
+                ((v[4 * j + 3] - base) & 0xFFu) << 24;
+    if (h) dw[3] = (dw[3] & 0x00FFFFFFu) | (escape ? 0xFFu : b) << 24;  // byte 31: row k = 31 is the zero row
+    const uint32_t sa = __shfl_xor(h ? dw[0] : dw[2], 32), sb = __shfl_xor(h ? dw[1] : dw[3], 32);
+    const u32x4_nt w = h ? u32x4_nt{sa, dw[2], sb, dw[3]} : u32x4_nt{dw[0], sa, dw[1], sb};
+    const uint64_t tg = tile_t0 + (lane & 31);
+    if (!tile_valid || tg < first || tg >= end) return;
+    __builtin_nontemporal_store(w, (u32x4_nt *)(pk + (tg - first) * 32 + 16 * h));
+    if (escape) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int k = (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (k < kRot) esc[(tg - first) * kRot + k] = (uint16_t)v[r];
+        }
+    }
+}
+
 // Shares TILES planes: 16 u16 elements (8 dwords) -> the low-byte and
 // high-byte planes, each byte XOR 0x80 (the byte - 128 as i8), 16 B each.
 __device__ __forceinline__ void split_bytes(const uint32_t *src8, uint4 &lo, uint4 &hi) {

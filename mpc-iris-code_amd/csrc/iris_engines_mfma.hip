@@ -36,7 +36,7 @@ constexpr int kTile = 32;
 constexpr int kMasksTiles = 7;
 constexpr int kResolveTiles = 4;
 template <int MODE>
-constexpr int masks_tiles() { return MODE == 0 ? kMasksTiles : kResolveTiles; }
+constexpr int masks_tiles() { return MODE != 1 ? kMasksTiles : kResolveTiles; }
 constexpr int kMasksBlocksPerCu = 2;  // persistent grid: workgroups per CU
 // MasksEngine stages the compact query (51 KB) in LDS per workgroup (two workgroups per CU); the
 // fused resolver (4 tiles per wave, 168 VGPRs) runs three workgroups per CU with the query read
@@ -45,7 +45,7 @@ constexpr int kMasksBlocksPerCu = 2;  // persistent grid: workgroups per CU
 // (2.90-3.01 vs 2.93-3.00 ms).
 constexpr int kResolveBlocksPerCu = 3;
 template <int MODE>
-constexpr int masks_blocks_per_cu() { return MODE == 0 ? kMasksBlocksPerCu : kResolveBlocksPerCu; }
+constexpr int masks_blocks_per_cu() { return MODE != 1 ? kMasksBlocksPerCu : kResolveBlocksPerCu; }
 constexpr int kSharesTiles = 2;
 
 __device__ __forceinline__ uint4 nt_load(const uint4 *p) {
@@ -96,7 +96,8 @@ struct MaskResolve {
     Partial *partials;
 };
 
-enum { MASKS_OUT = 0, MASKS_RESOLVE = 1 };
+// MASKS_PACKED: the [u16;31] rows in the read-ahead's packed form (store_tile_packed, iris_device.hpp)
+enum { MASKS_OUT = 0, MASKS_RESOLVE = 1, MASKS_PACKED = 2 };
 
 // Persistent: each wave walks the tile groups wave, wave + nwaves, ... as one
 // flat stream of (group, step) K-steps, so the loads of the next group are in
@@ -116,7 +117,7 @@ __global__ void __launch_bounds__(256, masks_blocks_per_cu<MODE>())
                       uint64_t first, uint64_t end, uint16_t *__restrict__ out, MaskResolve rs) {
     constexpr uint32_t kSteps = kMaskChunks / 4;  // 50 steps of 4 chunks
     const uint4 *sq = qfrag;  // the query's compact fragments: in LDS, or read from L2
-    if constexpr (MODE == MASKS_OUT) {
+    if constexpr (MODE != MASKS_RESOLVE) {
         __shared__ uint4 sq_lds[kMaskFragUint4];
         for (int i = threadIdx.x; i < (int)kMaskFragUint4; i += blockDim.x) sq_lds[i] = qfrag[i];
         __syncthreads();
@@ -128,7 +129,7 @@ __global__ void __launch_bounds__(256, masks_blocks_per_cu<MODE>())
     const uint64_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * kWaveSlots + (threadIdx.x >> 6));
     const uint64_t nwaves = (uint64_t)gridDim.x * kWaveSlots;
     const uint64_t ngroups = (ntiles + T - 1) / T;
-    if (MODE == MASKS_OUT && wave >= ngroups) return;
+    if (MODE != MASKS_RESOLVE && wave >= ngroups) return;
     const uint32_t total = wave < ngroups ? (uint32_t)((ngroups - wave + nwaves - 1) / nwaves) * kSteps : 0;
     uint16_t *lds = sh_out[threadIdx.x >> 6];
     Partial best = partial_none();
@@ -221,6 +222,9 @@ __global__ void __launch_bounds__(256, masks_blocks_per_cu<MODE>())
                     if constexpr (MODE == MASKS_OUT)
                         store_tile_rows(out, lds, (tile0 + tw + t) * kTile, first, end, tw + t < ntiles, lane,
                                         [&](int r) { return (uint16_t)(uint32_t)acc[t][r]; });
+                    else if constexpr (MODE == MASKS_PACKED)
+                        store_tile_packed((uint8_t *)out, out + (end - first) * 16, (tile0 + tw + t) * kTile, first, end,
+                                          tw + t < ntiles, lane, [&](int r) { return (uint32_t)acc[t][r]; });
                     else
                         resolve_tile((tile0 + tw + t) * kTile, tw + t < ntiles, acc[t]);
                 }
@@ -268,7 +272,7 @@ __global__ void __launch_bounds__(256, masks_blocks_per_cu<MODE>())
 constexpr int kMasksSplitKS = 10;
 constexpr uint64_t kMasksSplitTiles = 1024;
 
-template <int KS>
+template <int KS, bool PACKED = false>
 __global__ void __launch_bounds__(64 * KS)
     masks_split_kernel(const uint4 *__restrict__ db, const uint4 *__restrict__ qfrag, uint64_t tile0,
                        uint64_t first, uint64_t end, uint16_t *__restrict__ out, DoneSignal sig) {
@@ -307,6 +311,11 @@ __global__ void __launch_bounds__(64 * KS)
     for (int k = 0; k < KS - 1; ++k)
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[i] += red[k][i][lane];
+    if constexpr (PACKED) {
+        store_tile_packed((uint8_t *)out, out + (end - first) * 16, tile * kTile, first, end, true, lane,
+                          [&](int r) { return (uint32_t)acc[r]; });
+        return;
+    }
     store_tile_rows(out, sh_out, tile * kTile, first, end, true, lane,
                     [&](int r) { return (uint16_t)(uint32_t)acc[r]; }, sig.done != nullptr);
     if (sig.done) {  // wave 0 stored the workgroup's rows: once they are performed, take the ticket
@@ -325,26 +334,27 @@ static int tiles_per_wave(const Hooks &h, uint64_t ntiles, int big) {
 }
 
 int launch_masks_mfma(const Hooks &h, void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *out,
-                      DoneSignal *sig) {
+                      DoneSignal *sig, bool packed) {
     if (sig) sig->armed = false;
     if (r.n == 0) return 0;
     const uint64_t ntiles = tiles_of(r, 1).ntiles;
     // the K-split form for small ranges (IRIS_TILES_PER_WAVE pins the persistent kernel for tests)
     if (ntiles <= kMasksSplitTiles && !h.tiles_per_wave) {
         DoneSignal s{};
-        if (sig) {
+        if (sig && !packed) {
             s = *sig;
             sig->armed = true;
         }
-        hipLaunchKernelGGL(masks_split_kernel<kMasksSplitKS>, dim3((uint32_t)ntiles), dim3(64 * kMasksSplitKS), 0,
-                           (hipStream_t)stream, (const uint4 *)db, (const uint4 *)qfrag, tiles_of(r, 1).tile0,
-                           r.first, r.first + r.n, out, s);
+        auto kern = packed ? masks_split_kernel<kMasksSplitKS, true> : masks_split_kernel<kMasksSplitKS>;
+        hipLaunchKernelGGL(kern, dim3((uint32_t)ntiles), dim3(64 * kMasksSplitKS), 0, (hipStream_t)stream,
+                           (const uint4 *)db, (const uint4 *)qfrag, tiles_of(r, 1).tile0, r.first, r.first + r.n, out, s);
         return hipGetLastError() == hipSuccess ? 0 : -1;
     }
     const int tpw = tiles_per_wave(h, ntiles, kMasksTiles);
     const Tiles t = tiles_of(r, tpw);
     const uint64_t grid = std::min<uint64_t>(t.grid, resident_blocks(kMasksBlocksPerCu));
-    auto kern = tpw == 1 ? masks_mfma_kernel<MASKS_OUT, 1> : masks_mfma_kernel<MASKS_OUT>;
+    auto kern = packed ? (tpw == 1 ? masks_mfma_kernel<MASKS_PACKED, 1> : masks_mfma_kernel<MASKS_PACKED>)
+                       : (tpw == 1 ? masks_mfma_kernel<MASKS_OUT, 1> : masks_mfma_kernel<MASKS_OUT>);
     hipLaunchKernelGGL(kern, dim3((uint32_t)grid), dim3(256), 0, (hipStream_t)stream,
                        (const uint4 *)db, (const uint4 *)qfrag, t.tile0, t.ntiles, r.first, r.first + r.n, out,
                        MaskResolve{});

@@ -40,6 +40,7 @@
 #include <string.h>
 
 #include <array>
+#include <map>
 #include <condition_variable>
 #include <memory>
 #include <mutex>
@@ -387,7 +388,19 @@ int comms_ready(iris_group *g, uint32_t ms, const std::string &what) {
 // (eight ranks' bootstrap and topology discovery take seconds).
 uint32_t init_timeout(const iris_group *g) {
     const uint32_t h = g->devs.empty() ? 0 : g->devs[0]->hooks.group_timeout_ms;
-    return h ? h : 120000;
+    return h ? h : kGroupInitTimeoutMs;
+}
+
+// Abandoned inits per device ordinal, process-wide: `pending` are still blocked inside RCCL (each
+// holds a helper thread, its bootstrap sockets and a partial communicator until its peers come, if
+// ever), `total` counts every one since the process started (iris_config "abandoned_inits").
+struct Abandoned {
+    std::mutex mu;
+    std::map<int, std::pair<uint64_t, uint64_t>> by_ordinal;  // ordinal -> (pending, total)
+};
+Abandoned &abandoned() {
+    static Abandoned *a = new Abandoned();  // never destroyed: abandoned helper threads may outlive main
+    return *a;
 }
 
 // A communicator init that may never finish (a peer that never starts): RCCL 2.27.7 blocks inside
@@ -428,6 +441,8 @@ void init_job_run(std::shared_ptr<InitJob> job) {
                 (void)hipSetDevice(job->ordinals[i]);
                 (void)ncclCommAbort(job->comms[i]);
             }
+        std::lock_guard<std::mutex> a(abandoned().mu);
+        for (int o : job->ordinals) abandoned().by_ordinal[o].first -= 1;
         return;
     }
     job->cv.notify_all();
@@ -438,6 +453,17 @@ void init_job_run(std::shared_ptr<InitJob> job) {
 int comm_init(iris_group *g, const ncclUniqueId &u) {
     const size_t L = g->devs.size();
     g->comms.assign(L, nullptr);
+    if (g->ranks > 1) {  // a multi-rank init beside a pending abandoned one would pile another on top
+        std::lock_guard<std::mutex> a(abandoned().mu);
+        for (iris_device *d : g->devs) {
+            auto it = abandoned().by_ordinal.find(d->ordinal);
+            if (it != abandoned().by_ordinal.end() && it->second.first > 0)
+                return fail(IRIS_E_HIP, "an abandoned RCCL communicator init on device " + std::to_string(d->ordinal) +
+                                            " is still pending (a peer rank never arrived): this process forms no "
+                                            "further multi-rank group on it -- start a fresh process (1-rank groups "
+                                            "still form)");
+        }
+    }
     auto job = std::make_shared<InitJob>();
     for (iris_device *d : g->devs) job->ordinals.push_back(d->ordinal);
     job->comms.assign(L, nullptr);
@@ -453,6 +479,13 @@ int comm_init(iris_group *g, const ncclUniqueId &u) {
     std::unique_lock<std::mutex> l(job->mu);
     if (!job->cv.wait_for(l, std::chrono::milliseconds(ms), [&] { return job->done; })) {
         job->abandoned = true;
+        {
+            std::lock_guard<std::mutex> a(abandoned().mu);
+            for (int o : job->ordinals) {
+                abandoned().by_ordinal[o].first += 1;
+                abandoned().by_ordinal[o].second += 1;
+            }
+        }
         return fail(IRIS_E_HIP, "RCCL communicator init (" + std::to_string(g->ranks) + " ranks) did not complete within " +
                                     std::to_string(ms) + " ms (a peer rank failed, never started, or is unreachable); "
                                     "the pending init is abandoned");
@@ -1128,3 +1161,10 @@ int iris_group_template_batch_search(iris_group_db_t *gdb, const iris_template_t
 }
 
 }  // extern "C"
+
+void iris_api::abandoned_inits(int ordinal, uint64_t *pending, uint64_t *total) {
+    std::lock_guard<std::mutex> a(abandoned().mu);
+    auto it = abandoned().by_ordinal.find(ordinal);
+    *pending = it == abandoned().by_ordinal.end() ? 0 : it->second.first;
+    *total = it == abandoned().by_ordinal.end() ? 0 : it->second.second;
+}

@@ -47,6 +47,8 @@ inline int fail(int code, const std::string &msg) {
 struct KStat {
     uint64_t launches = 0, items = 0;
     double ms = 0;
+    uint64_t max_items = 0;  // the largest launch (the latest of equal ones) and its duration
+    double max_ms = 0;
 };
 
 struct Pending {
@@ -150,6 +152,9 @@ struct iris_device {
     std::vector<NotResident> not_resident;
     uint64_t resident_clock = 0;
     std::string resident_skip;  // why the last mapping refused was not made resident (iris_config)
+    // read-ahead launches, the records they computed and the largest window, since the last
+    // iris_device_reset_stats (iris_config "readahead_windows")
+    uint64_t ra_launches = 0, ra_records = 0, ra_window_max = 0;
 };
 
 struct iris_db {
@@ -193,6 +198,7 @@ struct Readahead {
     // never pays for rows it does not ask for)
     const struct iris_db *last_db = nullptr;
     uint64_t last_version = 0, last_end = 0;
+    uint64_t grow = 0;  // records of the walk's latest window (the next one is twice its chunks)
 };
 
 struct iris_engine {
@@ -348,6 +354,10 @@ inline void fold_done(iris_device *d) {
             s.launches += 1;
             s.ms += ms;
             s.items += p.items;
+            if (p.items >= s.max_items) {
+                s.max_items = p.items;
+                s.max_ms = ms;
+            }
             d->event_pool.push_back(p.a);
             d->event_pool.push_back(p.b);
         } else {
@@ -429,9 +439,14 @@ int db_store_locked(iris_db *db, uint64_t index, const void *records, uint64_t n
 int resident_slice(iris_device *d, int kind, const void *ptr, uint64_t n, iris_db **db, uint64_t *first,
                    uint64_t *end);
 void resident_drop_all(iris_device *d);  // frees every resident copy (waits for the device's streams)
+// frees the copy of the mapping holding p and forgets refusals of addresses there; true if one was freed
+bool resident_drop_at(iris_device *d, uintptr_t p);
 // count and device bytes of the resident copies, and how many check their file through a held
 // descriptor (map_files unreadable)
 void resident_stats(const iris_device *d, uint64_t *count, uint64_t *bytes, int *via_fd);
+// Abandoned RCCL communicator inits of device `ordinal` in this process (iris_group.hip): still
+// pending inside RCCL, and all since the process started
+void abandoned_inits(int ordinal, uint64_t *pending, uint64_t *total);
 // Partial (indices offset by base) -> iris_match_t; +inf / UINT64_MAX when none
 void match_from(const iris::Partial &r, bool any, uint64_t base, iris_match_t *out);
 

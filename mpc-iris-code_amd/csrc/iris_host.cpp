@@ -221,11 +221,50 @@ void build_query_tile(const iris_template_t *q, uint32_t *tile) {
 #include <vector>
 
 #include <errno.h>
+#include <immintrin.h>
 #include <unistd.h>
 
 namespace iris {
 
 namespace {
+
+// Packed MasksEngine rows (store_tile_packed): bytes 0..30 of a record are row[k] - 64 B, byte 31
+// is B, or 0xFF for a row stored in full in the escape rows.  Records go in increasing order, and
+// each is written as one 64-B store whose last 2 bytes the next record's store overwrites; the
+// last record of a range is written exactly (its successor may belong to another thread).
+__attribute__((target("avx512bw,avx512vl"))) void expand_avx512(uint16_t *out, const uint8_t *pk, const uint16_t *esc,
+                                                                  size_t n) {
+    for (size_t i = 0; i < n; ++i) {
+        const uint8_t *p = pk + 32 * i;
+        const uint32_t b = p[31];
+        uint16_t *o = out + kRot * i;
+        if (b == 0xFFu) {
+            memcpy(o, esc + kRot * i, kRot * 2);
+            continue;
+        }
+        const __m512i w = _mm512_add_epi16(_mm512_cvtepu8_epi16(_mm256_loadu_si256((const __m256i *)p)),
+                                           _mm512_set1_epi16((short)(b << 6)));
+        if (i + 1 < n)
+            _mm512_storeu_si512((void *)o, w);
+        else
+            _mm512_mask_storeu_epi16(o, 0x7FFFFFFFu, w);
+    }
+}
+
+void expand_scalar(uint16_t *out, const uint8_t *pk, const uint16_t *esc, size_t n) {
+    for (size_t i = 0; i < n; ++i) {
+        const uint8_t *p = pk + 32 * i;
+        uint16_t *o = out + kRot * i;
+        if (p[31] == 0xFFu) {
+            memcpy(o, esc + kRot * i, kRot * 2);
+            continue;
+        }
+        const uint16_t base = (uint16_t)(p[31] << 6);
+        for (int k = 0; k < kRot; ++k) o[k] = (uint16_t)(base + p[k]);
+    }
+}
+
+const bool kHaveAvx512 = __builtin_cpu_supports("avx512bw") && __builtin_cpu_supports("avx512vl");
 
 // Helper threads (one pool per device) for copying an engine call's rows out of pinned memory
 // into the caller's buffer (read-ahead, iris_api.hip) and a large write's records into the pinned
@@ -242,11 +281,13 @@ class CopyPool {
     int parts() const { return (int)threads_.size() + 1; }
 
     // src != nullptr: memcpy; else pread from fd at file offset off.  Returns false if a read failed
-    // (an I/O error, or the file ended before `bytes`).
-    bool run(char *dst, const char *src, size_t bytes, int fd = -1, off_t off = 0) {
+    // (an I/O error, or the file ended before `bytes`).  esc != nullptr: expand `bytes` packed
+    // MasksEngine records at src (escape rows at esc) into dst instead.
+    bool run(char *dst, const char *src, size_t bytes, int fd = -1, off_t off = 0, const uint16_t *esc = nullptr) {
         std::lock_guard<std::mutex> one(run_mu_);  // one copy at a time (devices may call concurrently)
         dst_ = dst;
         src_ = src;
+        esc_ = esc;
         bytes_ = bytes;
         fd_ = fd;
         off_ = off;
@@ -264,6 +305,12 @@ class CopyPool {
 
    private:
     void part(int id) {
+        if (esc_) {  // bytes_ records, split on record boundaries
+            const size_t per = (bytes_ + parts() - 1) / parts();
+            const size_t a = std::min(bytes_, (size_t)id * per), b = std::min(bytes_, a + per);
+            if (a < b) expand_packed_rows((uint16_t *)dst_ + kRot * a, (const uint8_t *)src_ + 32 * a, esc_ + kRot * a, b - a);
+            return;
+        }
         const size_t per = ((bytes_ + parts() - 1) / parts() + 63) & ~(size_t)63;
         const size_t a = std::min(bytes_, (size_t)id * per), b = std::min(bytes_, a + per);
         if (a >= b) return;
@@ -307,6 +354,7 @@ class CopyPool {
     std::atomic<int> remaining_{0};
     char *dst_ = nullptr;
     const char *src_ = nullptr;
+    const uint16_t *esc_ = nullptr;
     size_t bytes_ = 0;
     int fd_ = -1;
     off_t off_ = 0;
@@ -333,7 +381,8 @@ namespace {
 constexpr const char *kHookNames[] = {"IRIS_TILES_PER_WAVE",  "IRIS_FUSED_REDUCE", "IRIS_BATCH_KERNEL",
                                       "IRIS_SCHEDULE",        "IRIS_LOAD_PREAD",   "IRIS_GROUP_DELAY_US",
                                       "IRIS_GROUP_STALL",     "IRIS_GROUP_UNORDERED", "IRIS_UPLOAD",
-                                      "IRIS_LOAD_WINDOWS",    "IRIS_READAHEAD_WINDOW", "IRIS_RESIDENT_BUDGET_MB"};
+                                      "IRIS_LOAD_WINDOWS",    "IRIS_READAHEAD_WINDOW", "IRIS_RESIDENT_BUDGET_MB",
+                                      "IRIS_READAHEAD_PACKED"};
 constexpr int kNumHooks = (int)(sizeof(kHookNames) / sizeof(kHookNames[0]));
 
 const char *env(const char *name) {
@@ -373,8 +422,9 @@ void read_hooks(Hooks *h) {
         case 7: h->group_unordered = v[0] != '0'; break;
         case 8: h->upload = !strcmp(v, "pinned") ? 1 : !strcmp(v, "runtime") ? 2 : 0; break;
         case 9: h->load_windows = v[0] != '0'; break;
-        case 10: h->ra_window = env_u32(v, 8); break;
+        case 10: h->ra_window = env_u32(v, 64); break;
         case 11: h->resident_budget_mb = env_u32(v, 1u << 30); break;
+        case 12: h->ra_packed = v[0] != '0'; break;
         }
     }
 }
@@ -385,6 +435,8 @@ size_t format_hooks(const Hooks &h, char *buf, size_t len) {
     std::string s = "readahead=" + std::to_string(h.readahead) + " auto_resident=" + std::to_string(h.auto_resident) +
                     " group_timeout_ms=" +
                     (h.group_timeout_ms ? std::to_string(h.group_timeout_ms) : std::string("auto")) +
+                    " group_init_timeout_ms=" +
+                    std::to_string(h.group_timeout_ms ? h.group_timeout_ms : kGroupInitTimeoutMs) +
                     " copy_helpers=" + std::to_string(copy_helpers()) + " test_hooks=" + std::to_string(h.test);
     if (h.test)
         s += " tiles_per_wave=" + (h.tiles_per_wave ? std::to_string(h.tiles_per_wave) : std::string("auto")) +
@@ -393,6 +445,7 @@ size_t format_hooks(const Hooks &h, char *buf, size_t len) {
              " load_pread=" + std::to_string(h.load_pread) +
              " load_windows=" + std::to_string(h.load_windows) + " readahead_window=" + std::to_string(h.ra_window) +
              " resident_budget_mb=" + std::to_string(h.resident_budget_mb) +
+             " readahead_packed=" + std::to_string(h.ra_packed) +
              " group_delay_us=" + std::to_string(h.group_delay_us) +
              " group_stall=" + std::to_string(h.group_stall) + " group_unordered=" + std::to_string(h.group_unordered) +
              " upload=" + upload_names[h.upload & 3];
@@ -434,6 +487,21 @@ void parallel_copy(void *dst, const void *src, size_t bytes, int lane) {
 
 bool parallel_pread(int fd, void *dst, size_t bytes, off_t off, int lane) {
     return pool_of(lane)->run((char *)dst, nullptr, bytes, fd, off);
+}
+
+void expand_packed_rows(uint16_t *out, const uint8_t *pk, const uint16_t *esc, size_t n) {
+    if (kHaveAvx512)
+        expand_avx512(out, pk, esc, n);
+    else
+        expand_scalar(out, pk, esc, n);
+}
+
+void parallel_expand(uint16_t *out, const uint8_t *pk, const uint16_t *esc, size_t n, int lane) {
+    if (n * kRot * 2 < kParallelCopyMin) {
+        expand_packed_rows(out, pk, esc, n);
+        return;
+    }
+    (void)pool_of(lane)->run((char *)out, (const char *)pk, n, -1, 0, esc);
 }
 
 }  // namespace iris

@@ -11,6 +11,7 @@
 #pragma once
 #include <stdint.h>
 #include <stddef.h>
+#include <sys/types.h>
 
 #include "../../include/iris_hip.h"
 
@@ -186,10 +187,13 @@ struct Hooks {
     bool group_stall = false;        // IRIS_GROUP_STALL=1: a group all-gather waits on a peer that never comes
     bool group_unordered = false;    // IRIS_GROUP_UNORDERED=1: drop the exchange-buffer ordering (shows the race)
     int upload = 0;                  // IRIS_UPLOAD=pinned|runtime (1|2): the path of writes >= 8 MB (0: the faster lately)
-    uint32_t ra_window = 0;          // IRIS_READAHEAD_WINDOW=1..8: chunks per read-ahead window (0: by size)
+    uint32_t ra_window = 0;          // IRIS_READAHEAD_WINDOW=1..64: chunks per read-ahead window (0: growing)
     uint32_t resident_budget_mb = 0; // IRIS_RESIDENT_BUDGET_MB: resident copies hold at most this (0: free memory)
+    bool ra_packed = true;           // IRIS_READAHEAD_PACKED=0: masks read-ahead rows cross the host link unpacked
     uint32_t ignored = 0;            // bit i: test hook kHookNames[i] was set without IRIS_TEST_HOOKS=1
 };
+// The bound of forming a device group when IRIS_GROUP_TIMEOUT_MS is not set (iris_group.hip)
+constexpr uint32_t kGroupInitTimeoutMs = 120000;
 // Reads the environment (the Hooks a device opened now gets).
 void read_hooks(Hooks *h);
 // "key=value ..." of h plus the process-wide knobs (IRIS_COPY_HELPERS); returns the length.
@@ -265,8 +269,10 @@ struct DoneSignal {
     uint32_t seq;
     bool armed;
 };
+// packed: the rows in the read-ahead's packed form (store_tile_packed): out holds r.n records of
+// 32 B, then r.n escape rows of 31 u16 (no completion word)
 int launch_masks_mfma(const Hooks &h, void *stream, const void *db, const void *qfrag, LaunchRange r, uint16_t *out,
-                      DoneSignal *sig = nullptr);
+                      DoneSignal *sig = nullptr, bool packed = false);
 uint32_t masks_resolve_partials(const Hooks &h, LaunchRange r);
 int launch_masks_resolve(const Hooks &h, void *stream, const void *db, const void *qfrag, LaunchRange r,
                          const uint16_t *const *shares, uint32_t parts, double *dist_out, Partial *partials);
@@ -314,6 +320,11 @@ bool partial_better(const Partial &a, const Partial &b);
 void parallel_copy(void *dst, const void *src, size_t bytes, int lane = 0);  // lane: the device ordinal
 // pread of [off, off + bytes) of fd into dst, split over the same helper threads; false if a read
 // failed or the file ended early
-bool parallel_pread(int fd, void *dst, size_t bytes, long off, int lane = 0);
+bool parallel_pread(int fd, void *dst, size_t bytes, off_t off, int lane = 0);
+// MasksEngine rows of n records in the read-ahead's packed form (store_tile_packed, iris_device.hpp:
+// 32 B per record at pk, escaped rows in full at esc) expanded into [n][31] u16 at out, split over
+// the same helper threads
+void parallel_expand(uint16_t *out, const uint8_t *pk, const uint16_t *esc, size_t n, int lane = 0);
+void expand_packed_rows(uint16_t *out, const uint8_t *pk, const uint16_t *esc, size_t n);  // one thread
 
 }  // namespace iris

@@ -437,6 +437,18 @@ void iris_api::resident_drop_all(iris_device *d) {
     d->not_resident.clear();
 }
 
+bool iris_api::resident_drop_at(iris_device *d, uintptr_t p) {
+    auto &nr = d->not_resident;
+    nr.erase(std::remove_if(nr.begin(), nr.end(), [&](const iris_device::NotResident &x) { return p >= x.lo && p < x.hi; }),
+             nr.end());
+    for (Resident *r : d->resident)
+        if (p >= r->lo && p < r->hi) {
+            drop(d, r);
+            return true;
+        }
+    return false;
+}
+
 void iris_api::resident_stats(const iris_device *d, uint64_t *count, uint64_t *bytes, int *via_fd) {
     *count = d->resident.size();
     *bytes = 0;
@@ -445,6 +457,15 @@ void iris_api::resident_stats(const iris_device *d, uint64_t *count, uint64_t *b
         *bytes += r->dev_bytes;
         *via_fd += r->fd >= 0;
     }
+}
+
+extern "C" int iris_device_drop_resident_range(iris_device_t *d, const void *ptr) {
+    IRIS_KEEP_DEVICE();
+    ARG(d && ptr, "NULL argument");
+    std::lock_guard<std::recursive_mutex> g(d->mu);
+    CHK(set_device(d));
+    (void)resident_drop_at(d, (uintptr_t)ptr);
+    return 0;
 }
 
 extern "C" int iris_device_drop_resident(iris_device_t *d) {

@@ -91,6 +91,9 @@ def load_library(path=None):
             "iris_device_alloc": ([P, ctypes.c_size_t, PP], ctypes.c_int),
             "iris_device_free": ([P, P], ctypes.c_int),
             "iris_device_drop_resident": ([P], ctypes.c_int),
+            "iris_device_drop_resident_range": ([P, P], ctypes.c_int),
+            "iris_device_kernel_stats_largest": ([P, ctypes.c_char_p, ctypes.POINTER(u64), ctypes.POINTER(ctypes.c_double)],
+                                                 ctypes.c_int),
             "iris_memcpy_d2h": ([P, P, P, ctypes.c_size_t], ctypes.c_int),
             "iris_db_create": ([P, ctypes.c_int, u64, PP], ctypes.c_int),
             "iris_db_create_ex": ([P, ctypes.c_int, u64, ctypes.c_int, PP], ctypes.c_int),
@@ -180,6 +183,7 @@ def exported_symbols():
         "iris_last_error", "iris_version", "iris_config", "iris_device_count", "iris_device_open", "iris_device_close",
         "iris_device_synchronize", "iris_device_stream", "iris_device_set_profiling", "iris_device_kernel_stats",
         "iris_device_reset_stats", "iris_device_alloc", "iris_device_free", "iris_device_drop_resident",
+        "iris_device_drop_resident_range", "iris_device_kernel_stats_largest",
         "iris_memcpy_d2h", "iris_db_create",
         "iris_db_create_ex", "iris_db_layout",
         "iris_db_destroy", "iris_db_len", "iris_db_capacity", "iris_db_kind", "iris_db_append", "iris_db_write",
@@ -497,6 +501,12 @@ class Device:
         """Frees the device's resident record-file copies (iris_device_drop_resident)."""
         _check(load_library().iris_device_drop_resident(self.handle))
 
+    def drop_resident_range(self, array):
+        """Frees the resident copy of the file mapping that holds `array`'s first byte
+        (iris_device_drop_resident_range): after changing the file through a writable mapping."""
+        a = np.asarray(array)
+        _check(load_library().iris_device_drop_resident_range(self.handle, ctypes.c_void_p(a.ctypes.data)))
+
     def stream(self):
         s = ctypes.c_void_p()
         _check(load_library().iris_device_stream(self.handle, ctypes.byref(s)))
@@ -514,6 +524,13 @@ class Device:
         _check(load_library().iris_device_kernel_stats(self.handle, name.encode(), ctypes.byref(l), ctypes.byref(ms),
                                                         ctypes.byref(it)))
         return l.value, ms.value, it.value
+
+    def kernel_stats_largest(self, name):
+        """-> (items, ms) of the largest launch of the kernel family since the last reset."""
+        it, ms = ctypes.c_uint64(), ctypes.c_double()
+        _check(load_library().iris_device_kernel_stats_largest(self.handle, name.encode(), ctypes.byref(it),
+                                                                ctypes.byref(ms)))
+        return it.value, ms.value
 
     def alloc(self, nbytes):
         p = ctypes.c_void_p()

@@ -332,16 +332,32 @@ void orc_argmin(const double *dist, uint64_t n, double *min_distance, uint64_t *
 }
 
 /* resolver combine (src/main.rs:597-612): wrapping sum of the parts' [u16;31], then decode.
- * shares is [parts][n][31], denoms is [n][31]. */
-void orc_resolver_combine(const uint16_t *shares, uint32_t parts, const uint16_t *denoms, uint64_t n,
-                          double *dist_out) {
-    for (uint64_t i = 0; i < n; ++i) {
+ * shares is [parts][n][31], denoms is [n][31].  The reference runs this loop as a rayon
+ * into_par_iter over the entries (src/main.rs:597-612); threads splits the entries the same way
+ * (the argmin after it stays sequential, src/main.rs:616-621). */
+typedef struct {
+    const uint16_t *shares;
+    uint32_t parts;
+    const uint16_t *denoms;
+    uint64_t n;
+    double *out;
+} combine_ctx;
+
+static void combine_range(void *p, uint64_t lo, uint64_t hi) {
+    const combine_ctx *c = (const combine_ctx *)p;
+    for (uint64_t i = lo; i < hi; ++i) {
         uint16_t num[ORC_ROT] = {0};
-        for (uint32_t p = 0; p < parts; ++p)
+        for (uint32_t q = 0; q < c->parts; ++q)
             for (int k = 0; k < ORC_ROT; ++k)
-                num[k] = (uint16_t)(num[k] + shares[((uint64_t)p * n + i) * ORC_ROT + k]);
-        dist_out[i] = orc_decode_distance(num, denoms + i * ORC_ROT);
+                num[k] = (uint16_t)(num[k] + c->shares[((uint64_t)q * c->n + i) * ORC_ROT + k]);
+        c->out[i] = orc_decode_distance(num, c->denoms + i * ORC_ROT);
     }
+}
+
+void orc_resolver_combine(const uint16_t *shares, uint32_t parts, const uint16_t *denoms, uint64_t n,
+                          double *dist_out, int threads) {
+    combine_ctx c = {shares, parts, denoms, n, dist_out};
+    parallel_for(n, threads, combine_range, &c);
 }
 
 /* ------------------------------------------------------------ generator */
@@ -433,19 +449,32 @@ void orc_chacha_block(const uint8_t key[32], uint64_t nonce, uint64_t counter, u
     }
 }
 
-void orc_prepare_shares(const orc_template *t, uint64_t n, uint64_t index_base, const uint8_t key[32],
-                        uint64_t nonce, uint32_t rounds, uint32_t parties, uint16_t *shares, uint64_t *masks) {
+/* prepare (src/main.rs:333-361): per template encode + EncodedBits::share(parties), a rayon
+ * par_iter over the templates in the reference (src/main.rs:337-344); threads splits them the
+ * same way (every template's keystream blocks depend only on its global index) */
+typedef struct {
+    const orc_template *t;
+    uint64_t n, index_base, nonce;
+    const uint8_t *key;
+    uint32_t rounds, parties;
+    uint16_t *shares;
+    uint64_t *masks;
+} prepare_ctx;
+
+static void prepare_range(void *p, uint64_t lo, uint64_t hi) {
+    const prepare_ctx *c = (const prepare_ctx *)p;
     uint16_t enc[ORC_BITS];
     uint8_t blk[64];
-    for (uint64_t i = 0; i < n; ++i) {
-        const uint64_t g = index_base + i;
-        orc_encode(&t[i], enc);
-        uint16_t *last = shares + ((uint64_t)(parties - 1) * n + i) * ORC_BITS;
+    const uint32_t parties = c->parties;
+    for (uint64_t i = lo; i < hi; ++i) {
+        const uint64_t g = c->index_base + i;
+        orc_encode(&c->t[i], enc);
+        uint16_t *last = c->shares + ((uint64_t)(parties - 1) * c->n + i) * ORC_BITS;
         memcpy(last, enc, sizeof enc);
         for (uint32_t j = 0; j + 1 < parties; ++j) {
-            uint16_t *sh = shares + ((uint64_t)j * n + i) * ORC_BITS;
+            uint16_t *sh = c->shares + ((uint64_t)j * c->n + i) * ORC_BITS;
             for (int b = 0; b < ORC_BITS / 32; ++b) {
-                orc_chacha_block(key, nonce, (g * (parties - 1) + j) * (ORC_BITS / 32) + (uint64_t)b, rounds, blk);
+                orc_chacha_block(c->key, c->nonce, (g * (parties - 1) + j) * (ORC_BITS / 32) + (uint64_t)b, c->rounds, blk);
                 for (int e = 0; e < 32; ++e) {
                     const uint16_t v = (uint16_t)(blk[2 * e] | (blk[2 * e + 1] << 8));
                     sh[32 * b + e] = v;
@@ -453,6 +482,13 @@ void orc_prepare_shares(const orc_template *t, uint64_t n, uint64_t index_base, 
                 }
             }
         }
-        if (masks) memcpy(masks + i * ORC_LIMBS, t[i].mask, sizeof t[i].mask);
+        if (c->masks) memcpy(c->masks + i * ORC_LIMBS, c->t[i].mask, sizeof c->t[i].mask);
     }
+}
+
+void orc_prepare_shares(const orc_template *t, uint64_t n, uint64_t index_base, const uint8_t key[32],
+                        uint64_t nonce, uint32_t rounds, uint32_t parties, uint16_t *shares, uint64_t *masks,
+                        int threads) {
+    prepare_ctx c = {t, n, index_base, nonce, key, rounds, parties, shares, masks};
+    parallel_for(n, threads, prepare_range, &c);
 }

@@ -62,7 +62,7 @@ void orc_template_distances_batch(const orc_template *query, const orc_template 
 double orc_decode_distance(const uint16_t distances[ORC_ROT], const uint16_t denominators[ORC_ROT]);
 void orc_argmin(const double *dist, uint64_t n, double *min_distance, uint64_t *min_index);
 void orc_resolver_combine(const uint16_t *shares, uint32_t parts, const uint16_t *denoms, uint64_t n,
-                          double *dist_out);
+                          double *dist_out, int threads);
 
 /* synthetic data generator */
 uint64_t orc_gen_limb(uint64_t seed, uint64_t stream, uint64_t ctr);
@@ -86,6 +86,7 @@ void orc_chacha_block(const uint8_t key[32], uint64_t nonce, uint64_t counter, u
  * encode(t) minus their sum (mod 2^16).  shares: [parties][n][12800];
  * masks (may be NULL): [n][200], the `.masks` records (src/main.rs:333-342). */
 void orc_prepare_shares(const orc_template *t, uint64_t n, uint64_t index_base, const uint8_t key[32],
-                        uint64_t nonce, uint32_t rounds, uint32_t parties, uint16_t *shares, uint64_t *masks);
+                        uint64_t nonce, uint32_t rounds, uint32_t parties, uint16_t *shares, uint64_t *masks,
+                        int threads);
 
 #endif

@@ -53,12 +53,12 @@ def load(path=None):
     lib.orc_decode_distance.argtypes = [P, P]
     lib.orc_decode_distance.restype = ctypes.c_double
     lib.orc_argmin.argtypes = [P, u64, P, P]
-    lib.orc_resolver_combine.argtypes = [P, ctypes.c_uint32, P, u64, P]
+    lib.orc_resolver_combine.argtypes = [P, ctypes.c_uint32, P, u64, P, ctypes.c_int]
     lib.orc_gen_templates.argtypes = [u64, u64, u64, P]
     lib.orc_gen_masks.argtypes = [u64, u64, u64, P]
     lib.orc_gen_shares.argtypes = [u64, u64, u64, P]
     lib.orc_chacha_block.argtypes = [P, u64, u64, ctypes.c_uint32, P]
-    lib.orc_prepare_shares.argtypes = [P, u64, u64, P, u64, ctypes.c_uint32, ctypes.c_uint32, P, P]
+    lib.orc_prepare_shares.argtypes = [P, u64, u64, P, u64, ctypes.c_uint32, ctypes.c_uint32, P, P, ctypes.c_int]
     if path is None:
         _lib = lib
     return lib
@@ -178,12 +178,12 @@ def argmin(dist):
     return float(d[0]), int(i[0])
 
 
-def resolver_combine(shares, denoms):
+def resolver_combine(shares, denoms, threads=None):
     shares = np.ascontiguousarray(shares, np.uint16)  # [parts, n, 31]
     denoms = np.ascontiguousarray(denoms, np.uint16)  # [n, 31]
     parts, n = shares.shape[0], shares.shape[1]
     out = np.empty(n, np.float64)
-    load().orc_resolver_combine(_p(shares), parts, _p(denoms), n, _p(out))
+    load().orc_resolver_combine(_p(shares), parts, _p(denoms), n, _p(out), _threads(threads))
     return out
 
 
@@ -214,7 +214,7 @@ def chacha_block(key, nonce, counter, rounds=20):
     return out.tobytes()
 
 
-def prepare_shares(templates, key, nonce=0, parties=3, index_base=0, rounds=12):
+def prepare_shares(templates, key, nonce=0, parties=3, index_base=0, rounds=12, threads=None):
     """EncodedBits::share of encode(t) with the ChaCha stream of orc_prepare_shares:
     returns (shares [parties][n][12800] u16, masks [n][200] u64)."""
     t = np.ascontiguousarray(np.asarray(templates, np.uint64).reshape(-1, 400))
@@ -224,5 +224,5 @@ def prepare_shares(templates, key, nonce=0, parties=3, index_base=0, rounds=12):
     shares = np.zeros((parties, n, 12800), np.uint16)
     masks = np.zeros((n, 200), np.uint64)
     load().orc_prepare_shares(_p(t), n, int(index_base), _p(k), int(nonce), int(rounds), int(parties), _p(shares),
-                              _p(masks))
+                              _p(masks), _threads(threads))
     return shares, masks

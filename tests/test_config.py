@@ -9,7 +9,8 @@ import iris_hip as ih
 
 TEST_HOOKS = ["IRIS_TILES_PER_WAVE", "IRIS_FUSED_REDUCE", "IRIS_BATCH_KERNEL", "IRIS_SCHEDULE",
               "IRIS_LOAD_PREAD", "IRIS_GROUP_DELAY_US", "IRIS_GROUP_STALL", "IRIS_GROUP_UNORDERED", "IRIS_UPLOAD",
-              "IRIS_LOAD_WINDOWS", "IRIS_READAHEAD_WINDOW", "IRIS_RESIDENT_BUDGET_MB"]
+              "IRIS_LOAD_WINDOWS", "IRIS_READAHEAD_WINDOW", "IRIS_RESIDENT_BUDGET_MB",
+              "IRIS_READAHEAD_PACKED"]
 
 
 @pytest.fixture(autouse=True)
@@ -21,8 +22,14 @@ def clean_env(monkeypatch):
 
 def test_defaults():
     c = ih.config()
-    assert c == {"readahead": "1", "auto_resident": "1", "group_timeout_ms": "auto", "copy_helpers": "3",
-                 "test_hooks": "0"}
+    assert c == {"readahead": "1", "auto_resident": "1", "group_timeout_ms": "auto", "group_init_timeout_ms": "120000",
+                 "copy_helpers": "3", "test_hooks": "0"}
+
+
+def test_group_timeout_sets_the_formation_bound(monkeypatch):
+    monkeypatch.setenv("IRIS_GROUP_TIMEOUT_MS", "6000")
+    c = ih.config()
+    assert c["group_timeout_ms"] == "6000" and c["group_init_timeout_ms"] == "6000"
 
 
 def test_test_hooks_ignored_without_opt_in(monkeypatch):

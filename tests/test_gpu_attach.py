@@ -8,6 +8,7 @@ import numpy as np
 import pytest
 
 import iris_hip as ih
+import readahead_policy as ra_policy
 from oracle import oracle_c as oc
 
 pytestmark = pytest.mark.gpu
@@ -115,7 +116,8 @@ def launches(dev, name):
 def test_attached_chunk_walk_readahead(device, hooked_device, kind, readahead):
     """The reference's loop (src/main.rs:427-431, 511-516): consecutive equal chunks of the
     attached file, the last one short.  With readahead every chunk after the first comes from
-    the engine's read-ahead windows (several chunks per launch), every record computed once."""
+    the engine's read-ahead windows (growing: 2, 4, ... chunks per launch, tests/readahead_policy.py),
+    every record computed once."""
     if readahead == "0":  # a production knob, read when the device opens
         device = hooked_device(IRIS_READAHEAD="0")
         assert device.config()["readahead"] == "0"
@@ -142,10 +144,12 @@ def test_attached_chunk_walk_readahead(device, hooked_device, kind, readahead):
                 nl, _, items = device.kernel_stats(kname)
                 if readahead == "0":
                     assert nl == per_walk * (walk + 1) and items == n * (walk + 1)
-                elif walk == 0:  # chunk 0, then one window of the rest: every record computed once
-                    assert nl == 2 and items == n, (nl, items)
+                elif walk == 0:  # chunk 0, then the growing windows: every record computed once
+                    assert nl == len(ra_policy.windows(n, chunk)) and items == n, (nl, items)
+                    assert ra_policy.counters(device) == (nl, n, max(ra_policy.windows(n, chunk)))
                 else:  # the second walk recomputes at most its first chunk (the window its
-                    assert nl <= 3 and items <= n + chunk, (nl, items)  # rows were in was regrown)
+                    # rows were in was regrown)
+                    assert nl <= 2 * len(ra_policy.windows(n, chunk)) + 1 and items <= 2 * n + chunk, (nl, items)
             assert launches(device, "pack") == 0
             # out of order: every call still returns its own rows (misses recompute)
             for a, b in ((2000 % n, 2000 % n + 7), (0, chunk), (0, chunk), (n - 5, n), (chunk, 2 * chunk), (1, 2)):

@@ -120,7 +120,10 @@ def test_bench_rccl_single_rank():
         assert r.returncode == 0, r.stderr[-3000:]
         d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
         assert d["n_gpus"] == 1 and d["check"]["ok"] and d["ranks_seen"] == 1
-        assert "ncclCommInitRank" in d["backend"] and "RCCL" in d["config"]["exchange"]
+        assert "helper-thread ncclCommInitRank (bounded)" in d["backend"] and "RCCL" in d["config"]["exchange"]
+        # the formation's wall time and bound, for the first multi-GPU record to say what ran
+        assert 0 < d["group_form_s"] < d["rccl_init_timeout_ms"] / 1e3
+        assert d["rccl_init_timeout_ms"] == 120000
         # what the library's communicator saw: one rank, on this box's GPU (its PCI bus id)
         assert d["rccl_nranks"] == 1 and len(d["rccl_devices"]) == 1
         assert re.fullmatch(r"[0-9a-fA-F]{4}:[0-9a-fA-F]{2}:[0-9a-fA-F]{2}\.[0-9a-fA-F]", d["rccl_devices"][0])

@@ -233,7 +233,7 @@ def test_group_rejects_duplicate_device_and_bad_args():
 
 
 def test_group_single_rank_communicator():
-    """The multi-process form (non-blocking ncclCommInitRankConfig) with one rank: what each
+    """The multi-process form (helper-thread ncclCommInitRank (bounded)) with one rank: what each
     torchrun rank of bench.py builds; RCCL itself reports one rank on this GPU."""
     uid = ih.Group.unique_id()
     assert len(uid) == 128
@@ -263,6 +263,17 @@ try:
 except ih.IrisError as e:
     err = str(e)
 dt = time.monotonic() - t0
+# a second 2-rank formation while the first init is still pending inside RCCL: refused at once
+t1 = time.monotonic()
+err2 = None
+try:
+    ih.Group.rank(0, 2, 0, ih.Group.unique_id())
+except ih.IrisError as e:
+    err2 = str(e)
+dt2 = time.monotonic() - t1
+probe = ih.Device(0)
+abandoned = probe.config()["abandoned_inits"]
+probe.close()
 n = 2000
 ref = oc.gen_templates(80, 0, n)
 query = ref[777].copy()
@@ -277,7 +288,7 @@ with ih.Group.rank(0, 1, 0, ih.Group.unique_id()) as g:
         gdb.write(0, ref)
         m2 = gdb.search(query)
 dev.close()
-print(json.dumps({"err": err, "dt": dt, "want": [int(idx), float(best)],
+print(json.dumps({"err": err, "dt": dt, "err2": err2, "dt2": dt2, "abandoned": abandoned, "want": [int(idx), float(best)],
                   "single": [int(m1.index), m1.distance], "group": [int(m2.index), m2.distance]}))
 sys.stdout.flush()
 """
@@ -286,8 +297,10 @@ sys.stdout.flush()
 def test_group_missing_peer_fails_within_bound(tmp_path):
     """A 2-rank group whose second rank never comes: forming it must fail within the bound
     (IRIS_GROUP_TIMEOUT_MS, read when the group's device opens) instead of hanging in RCCL's
-    init; the same process's GPU then searches and forms a 1-rank group normally, and the
-    process exits although the abandoned init never finished.  Run in a child process so that
+    init; a second 2-rank formation while that init is still pending is refused at once (one
+    abandoned init per device at most, iris_config abandoned_inits=1/1); the same process's GPU
+    then searches and forms a 1-rank group normally, and the process exits although the abandoned
+    init never finished.  Run in a child process so that
     its exit is part of what is tested."""
     import json
     import os
@@ -308,6 +321,10 @@ def test_group_missing_peer_fails_within_bound(tmp_path):
     d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     assert d["err"] and "did not complete within 6000 ms" in d["err"], d
     assert d["dt"] < 6 + 10, d  # the bound, plus opening the device
+    # bounded leftovers: the second multi-rank attempt is refused without waiting, and says why
+    assert d["err2"] and "still pending" in d["err2"] and "fresh process" in d["err2"], d
+    assert d["dt2"] < 2, d
+    assert d["abandoned"] == "1/1", d
     want_idx, want_d = d["want"]
     assert d["single"][0] == want_idx and d["group"][0] == want_idx == 777
     assert np.float64(d["single"][1]).view(np.uint64) == np.float64(want_d).view(np.uint64)

@@ -14,6 +14,7 @@ import numpy as np
 import pytest
 
 import iris_hip as ih
+import readahead_policy as ra_policy
 from oracle import oracle_c as oc
 
 pytestmark = pytest.mark.gpu
@@ -322,3 +323,119 @@ def test_budget_evicts_least_recently_used_and_refuses_too_large(hooked_device, 
     finally:
         dev.set_profiling(False)
     del files
+
+
+def walk_counted(device, eng, recs, chunk):
+    device.reset_stats()
+    out = walk(eng, recs, chunk)
+    device.synchronize()
+    return out, ra_policy.counters(device)
+
+
+@pytest.mark.parametrize("kind,n,chunk", [(ih.KIND_MASKS, 1_200_000, CHUNK), (ih.KIND_SHARES, 100_000, 2_000)],
+                         ids=["masks-1.2M", "shares-100k"])
+def test_long_walk_windows_grow(device, hooked_device, tmp_path, kind, n, chunk):
+    """A long walk of a mapped file (masks: 1.2M records in the resolver's 20k chunks, 1.9 GB;
+    shares: 100k in 2 000-record chunks, 2.6 GB): after the untimed first walk, a walk with a
+    fresh engine reads ahead in windows of 1, 2, 4, ... chunks up to the rows cap, then shrinking
+    to the walk's end -- counted by the library (readahead_windows: launches, records, largest
+    window), each record computed exactly once.  Rows equal the oracle on samples and, all of them,
+    the rows of the same walk on a device that computes every call alone (IRIS_READAHEAD=0)."""
+    path = tmp_path / "long.records"
+    gen(kind, SEED + 40, n).tofile(path)
+    recs = mapped(path, kind, n)
+    rng = np.random.default_rng(8)
+    want_windows = ra_policy.windows(n, chunk)
+    qt = oc.gen_templates(SEED + 41, 0, 1)[0]
+    q = qt[200:] if kind == ih.KIND_MASKS else oc.encode(qt)
+    Eng = ih.MasksEngine if kind == ih.KIND_MASKS else ih.DistanceEngine
+    with Eng(device, q) as eng:
+        walk(eng, recs, chunk)  # makes the file resident
+    with Eng(device, q) as eng:
+        out, (launches, records, largest) = walk_counted(device, eng, recs, chunk)
+    assert records == n, (records, n)  # every record once
+    assert (launches, largest) == (len(want_windows), max(want_windows)), (launches, largest, want_windows)
+    assert max(want_windows) >= 16 * chunk
+    idx = np.unique(np.concatenate([rng.choice(n, 300, replace=False), [0, n - 1, chunk - 1, chunk]]))
+    sample = np.ascontiguousarray(recs[idx])
+    want = oc.masks_batch(q, sample) if kind == ih.KIND_MASKS else oc.distance_batch(q, sample)
+    assert (out[idx] == want).all()
+    plain = hooked_device(IRIS_READAHEAD="0")
+    with Eng(plain, q) as eng:
+        ref = walk(eng, recs, chunk)
+    assert (out == ref).all()
+    del recs
+
+
+def structured_masks(n, rng, block_every=3):
+    """Masks where every `block_every`-th record is a block of columns (an occlusion-like mask:
+    columns [c0, c0 + w) of every row), the rest uniform random: against a block query the block
+    records' counts change by 64 per column of rotation, so most of their rows span far more than
+    a byte and take the packed form's escape path (store_tile_packed)."""
+    out = oc.gen_masks(int(rng.integers(1 << 30)), 0, n)
+    for i in range(0, n, block_every):
+        c0, w = int(rng.integers(0, 200)), int(rng.integers(20, 120))
+        bits = np.zeros((64, 200), np.uint8)
+        bits[:, (np.arange(w) + c0) % 200] = 1
+        out[i] = np.packbits(bits.reshape(12800), bitorder="little").view(np.uint64)
+    return out
+
+
+def test_packed_rows_escape_path(device, hooked_device, tmp_path):
+    """The masks read-ahead's rows cross the host link packed (32 B per record, a base + 31 byte
+    offsets); a row whose 31 counts span more than a byte escapes to a full row.  A block query
+    mask (columns 40..109) against a file of random and block masks: every row of a 20k-chunk walk
+    equals the oracle's, escaped and packed alike, and equals the same walk with the packing off
+    (IRIS_READAHEAD_PACKED=0)."""
+    n = 90_001
+    rng = np.random.default_rng(9)
+    host = structured_masks(n, rng)
+    qbits = np.zeros((64, 200), np.uint8)
+    qbits[:, 40:110] = 1
+    q = np.packbits(qbits.reshape(12800), bitorder="little").view(np.uint64)
+    want = oc.masks_batch(q, host)
+    spans = want.max(axis=1).astype(int) - (want.min(axis=1).astype(int) // 64) * 64
+    assert (spans > 255).sum() > n // 6 and (spans <= 255).sum() > n // 2  # both forms occur
+    path = tmp_path / "s.masks"
+    host.tofile(path)
+    recs = mapped(path, ih.KIND_MASKS, n)
+    with ih.MasksEngine(device, q) as eng:
+        for _ in range(2):  # the first walk fills the copy, the second is all read-ahead windows
+            assert (walk(eng, recs) == want).all()
+    unpacked = hooked_device(IRIS_READAHEAD_PACKED="0")
+    with ih.MasksEngine(unpacked, q) as eng:
+        assert (walk(eng, recs) == want).all()
+        assert (walk(eng, recs, chunk=7_777) == want).all()
+    del recs
+
+
+def test_drop_resident_range_after_writes_through_a_mapping(device, tmp_path):
+    """Records rewritten in place through a second, writable mapping of the file (np.memmap r+, the
+    store path whose timestamps the per-call check may not see once the pages are dirty): after
+    iris_device_drop_resident_range on the read-only mapping, the next walk copies the file afresh
+    and serves the new rows.  The call leaves other files' copies alone and is a no-op on an
+    address without a copy."""
+    kind, n = ih.KIND_MASKS, 45_000
+    pa, pb = tmp_path / "a.masks", tmp_path / "b.masks"
+    old, new, other = gen(kind, SEED + 50, n), gen(kind, SEED + 51, n), gen(kind, SEED + 52, n)
+    old.tofile(pa)
+    other.tofile(pb)
+    recs, recs_b = mapped(pa, kind, n), mapped(pb, kind, n)
+    eng, want_fn = engine_and_oracle(device, kind, SEED + 53)
+    with eng:
+        assert (walk(eng, recs) == want_fn(old)).all()
+        assert (walk(eng, recs_b) == want_fn(other)).all()
+        assert device.resident()[0] == 2
+        rw = np.memmap(pa, dtype=np.uint64, mode="r+", shape=(n, 200))
+        sl = slice(1_000, 31_000)
+        rw[sl] = new[sl]
+        rw.flush()
+        del rw
+        old[sl] = new[sl]
+        device.drop_resident_range(recs[5])  # any address inside the mapping
+        assert device.resident()[0] == 1  # b's copy stays
+        device.drop_resident_range(np.zeros(4))  # no copy there
+        assert device.resident()[0] == 1
+        assert (walk(eng, recs) == want_fn(old)).all()
+        assert device.resident()[0] == 2
+    del recs, recs_b
