@@ -72,7 +72,7 @@ int iris_api::db_write_pinned(iris_db *db, uint64_t index, const void *records, 
     const uint64_t ch = std::max<uint64_t>(64, piece / k.rec_bytes / 64 * 64);
     const size_t slot = (size_t)ch * k.rec_bytes;
     CHK(ensure_upin(d));  // host first: an IRIS_E_NOMEM with the slots in place is the device's
-    CHK(ensure(d->staging, kUploadSlots * slot));
+    CHK(ensure(d, d->staging, kUploadSlots * slot));
     int rc = 0;
     uint64_t c = 0;
     for (uint64_t done = 0; done < n && rc == 0; done += ch, ++c) {
@@ -156,7 +156,7 @@ int db_write_runtime(iris_db *db, uint64_t index, const void *records, uint64_t 
     iris_device *d = db->dev;
     const KindInfo &k = db->k;
     const uint64_t ch = chunk_records(k);
-    CHK(ensure(d->staging, std::min<uint64_t>(n, ch) * k.rec_bytes));
+    CHK(ensure(d, d->staging, std::min<uint64_t>(n, ch) * k.rec_bytes));
     for (uint64_t done = 0; done < n; done += ch) {
         const uint64_t m = std::min<uint64_t>(ch, n - done);
         HIPCHK(hipMemcpyAsync(d->staging.p, (const char *)records + done * k.rec_bytes, m * k.rec_bytes,
@@ -181,7 +181,7 @@ int temp_db(iris_device *d, int kind, uint64_t cap, TempDb &t) {
     t.db.cap = (cap + t.db.k.block - 1) / t.db.k.block * t.db.k.block;
     t.db.len = 0;
     const size_t bytes = std::max<uint64_t>(1, t.db.cap / t.db.k.block) * block_bytes(t.db.k);
-    CHK(ensure(d->tempdb, bytes));
+    CHK(ensure(d, d->tempdb, bytes));
     t.db.data = d->tempdb.p;
     // the last block's records past the range stay zero (as a fresh database's)
     HIPCHK(hipMemsetAsync(t.db.data, 0, bytes, d->stream));
@@ -226,7 +226,7 @@ int run_u16_engine(iris_engine *e, const iris_db *db, uint64_t first, uint64_t n
         const int rc = run_u16_engine_pinned(e, db, first, n, out);
         if (rc != IRIS_E_NOMEM) return rc;
     }
-    CHK(ensure(d->out_a, std::min<uint64_t>(n, kU16Chunk) * kRot * 2));
+    CHK(ensure(d, d->out_a, std::min<uint64_t>(n, kU16Chunk) * kRot * 2));
     for (uint64_t done = 0; done < n; done += kU16Chunk) {
         const uint64_t m = std::min<uint64_t>(kU16Chunk, n - done);
         CHK(enqueue_u16_engine(e, db, first + done, m, (uint16_t *)d->out_a.p));
@@ -508,8 +508,7 @@ int qbuf_take(iris_device *d, size_t bytes, void **p, size_t *got) {
         d->qpool.erase(d->qpool.begin() + bi);
         return 0;
     }
-    hipError_t e = hipMalloc(p, bytes);
-    if (e != hipSuccess) return fail(IRIS_E_NOMEM, std::string("hipMalloc query buffer: ") + hipGetErrorString(e));
+    CHK(dev_malloc(d, p, bytes, "query buffer"));
     *got = bytes;
     return 0;
 }
@@ -795,6 +794,7 @@ int iris_device_synchronize(iris_device_t *d) {
     ARG(d, "device is NULL");
     std::lock_guard<std::recursive_mutex> g(d->mu);
     CHK(set_device(d));
+    resident_sweep(d);  // copies of mappings that are gone free their memory (at most once a second)
     return sync(d);
 }
 
@@ -860,9 +860,7 @@ int iris_device_alloc(iris_device_t *d, size_t bytes, void **ptr) {
     ARG(d && ptr, "NULL argument");
     std::lock_guard<std::recursive_mutex> g(d->mu);
     CHK(set_device(d));
-    hipError_t e = hipMalloc(ptr, std::max<size_t>(bytes, 1));
-    if (e != hipSuccess) return fail(IRIS_E_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
-    return 0;
+    return dev_malloc(d, ptr, std::max<size_t>(bytes, 1), "iris_device_alloc");
 }
 
 int iris_device_free(iris_device_t *d, void *ptr) {
@@ -918,19 +916,13 @@ int iris_db_create_ex(iris_device_t *d, int kind, uint64_t capacity, int layout,
         return fail(IRIS_E_NOMEM, "database capacity overflows the address space");
     }
     db->cap = capacity == 0 ? 0 : blocks * db->k.block;
-    hipError_t e = hipMalloc(&db->data, bytes);
-    if (e != hipSuccess && !d->resident.empty()) {  // the caller's database before cached file copies
-        (void)hipGetLastError();
-        resident_drop_all(d);
-        e = hipMalloc(&db->data, bytes);
-    }
-    if (e != hipSuccess) {
+    // the caller's database before cached file copies (evicted least recently used first)
+    if (dev_malloc(d, &db->data, bytes, "database") != 0) {
         delete db;
-        return fail(IRIS_E_NOMEM, std::string("hipMalloc database (") + std::to_string(bytes) +
-                                      " B): " + hipGetErrorString(e));
+        return IRIS_E_NOMEM;
     }
     // zeroed padding records: a zero mask gives den = 0, i.e. "no candidate"
-    e = hipMemsetAsync(db->data, 0, bytes, d->stream);
+    hipError_t e = hipMemsetAsync(db->data, 0, bytes, d->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(d->stream);
     if (e != hipSuccess) {
         (void)hipFree(db->data);
@@ -1014,7 +1006,7 @@ int iris_db_read(const iris_db_t *db, uint64_t first, uint64_t n, void *records)
         // device while the helper threads copy slot c - 1 into the caller's array
         const uint64_t ch = std::max<uint64_t>(64, kUploadSlot / k.rec_bytes / 64 * 64);
         const size_t slot = (size_t)ch * k.rec_bytes;
-        CHK(ensure(d->staging, kUploadSlots * slot));
+        CHK(ensure(d, d->staging, kUploadSlots * slot));
         const uint64_t chunks = (n + ch - 1) / ch;
         int rc = 0;
         auto enqueue = [&](uint64_t c) -> int {
@@ -1041,7 +1033,7 @@ int iris_db_read(const iris_db_t *db, uint64_t first, uint64_t n, void *records)
         return rs;
     }
     const uint64_t ch = chunk_records(k);
-    CHK(ensure(d->staging, std::min<uint64_t>(n, ch) * k.rec_bytes));
+    CHK(ensure(d, d->staging, std::min<uint64_t>(n, ch) * k.rec_bytes));
     for (uint64_t done = 0; done < n; done += ch) {
         const uint64_t m = std::min<uint64_t>(ch, n - done);
         CHK(timed(d, "unpack", m, [&] { return launch_unpack(d->stream, k, db->data, d->staging.p, first + done, m); }));
@@ -1262,6 +1254,7 @@ int iris_engine_batch_process_host(iris_engine_t *e, const void *records, uint64
     uint64_t rfirst = 0, rend = 0;
     CHK(resident_slice(d, e->kind, records, n, &rdb, &rfirst, &rend));
     if (rdb) {
+        PinResident pin(d, rdb);  // a workspace allocation below may evict copies: not this one
         if (readahead_ok(rdb, n)) return readahead_u16_call(e, rdb, rfirst, n, rend, out);
         CHK(ra_wait(e));
         return run_u16_engine(e, rdb, rfirst, n, out);
@@ -1297,8 +1290,8 @@ int iris_template_counts(iris_engine_t *e, const iris_db_t *db, uint64_t first, 
     if (n == 0 || (!num_out && !den_out)) return 0;
     const uint64_t ch = 4ull << 20;
     const size_t bytes = std::min<uint64_t>(n, ch) * kRot * 2;
-    CHK(ensure(d->out_a, bytes));
-    CHK(ensure(d->out_b, bytes));
+    CHK(ensure(d, d->out_a, bytes));
+    CHK(ensure(d, d->out_b, bytes));
     for (uint64_t done = 0; done < n; done += ch) {
         const uint64_t m = std::min<uint64_t>(ch, n - done);
         LaunchRange r{first + done, m};
@@ -1335,7 +1328,7 @@ int iris_api::search_enqueue(iris_engine_t *e, const iris_db_t *db, uint64_t fir
     if (layout == IRIS_LAYOUT_TILES && fused_search_ok(d->hooks, r)) {
         // small range: the kernel's last workgroup reduces and writes dst itself (no reduce launch)
         CHK(ensure_ticket(d));
-        CHK(ensure(d->partials, (size_t)mfma_search_partials(d->hooks, r) * sizeof(Partial)));
+        CHK(ensure(d, d->partials, (size_t)mfma_search_partials(d->hooks, r) * sizeof(Partial)));
         const FusedFinish fin{(uint32_t *)d->ticket.p, dst, idx_base, host_done, seq};
         uint32_t written = 0;
         CHK(timed(d, "template_search", n, [&] {
@@ -1368,7 +1361,7 @@ int iris_api::search_enqueue(iris_engine_t *e, const iris_db_t *db, uint64_t fir
         // the reduce that last read this buffer (two searches ago) precedes the overwrite
         HIPCHK(hipStreamWaitEvent(d->stream, d->apart_read[b], 0));
     }
-    CHK(ensure(*buf, pbytes));
+    CHK(ensure(d, *buf, pbytes));
     Partial *part = (Partial *)buf->p;
     uint32_t written = 0;
     CHK(timed(d, "template_search", n, [&] {
@@ -1442,7 +1435,7 @@ static int pair_search_locked(iris_engine_t *a, iris_engine_t *b, const iris_db_
     iris_device *d = a->dev;
     LaunchRange r{first, n};
     const uint32_t np = multi_search_partials(r, 2);
-    CHK(ensure(d->partials, (size_t)std::max<uint32_t>(2 * np, 1) * sizeof(Partial)));
+    CHK(ensure(d, d->partials, (size_t)std::max<uint32_t>(2 * np, 1) * sizeof(Partial)));
     CHK(ensure_host_result(d, 2 * sizeof(Partial)));
     const void *qf[2] = {a->qfrag, b->qfrag};
     uint32_t written = 0;
@@ -1581,7 +1574,7 @@ int iris_template_distances(iris_engine_t *e, const iris_db_t *db, uint64_t firs
     if (n == 0) return 0;
     ARG(out, "out is NULL");
     const uint64_t ch = 16ull << 20;
-    CHK(ensure(d->out_a, std::min<uint64_t>(n, ch) * sizeof(double)));
+    CHK(ensure(d, d->out_a, std::min<uint64_t>(n, ch) * sizeof(double)));
     for (uint64_t done = 0; done < n; done += ch) {
         const uint64_t m = std::min<uint64_t>(ch, n - done);
         iris_match_t ignored;
@@ -1656,7 +1649,7 @@ int iris_template_batch_search(iris_engine_t *e, const iris_db_t *db, uint64_t f
     const uint32_t nqp = geo.nqg * geo.qper;
     std::vector<Partial> res(nqp);
     if (n > 0) {
-        CHK(ensure(d->partials, (size_t)nqp * geo.G * sizeof(Partial)));
+        CHK(ensure(d, d->partials, (size_t)nqp * geo.G * sizeof(Partial)));
         CHK(ensure_host_result(d, (size_t)nqp * sizeof(Partial)));
         CHK(timed(d, "template_batch", n * e->nq, [&] {
             return launch_batch(d->hooks, d->stream, db->data, e->qfrag, r, geo, (Partial *)d->partials.p,
@@ -1711,7 +1704,7 @@ int iris_resolver_search(iris_device_t *d, const uint16_t *const *shares, uint32
     std::lock_guard<std::recursive_mutex> g(d->mu);
     CHK(set_device(d));
     const uint32_t np = resolver_partials(n);
-    CHK(ensure(d->partials, (size_t)std::max<uint32_t>(np, 1) * sizeof(Partial)));
+    CHK(ensure(d, d->partials, (size_t)std::max<uint32_t>(np, 1) * sizeof(Partial)));
     CHK(timed(d, "resolver", n, [&] {
         return launch_resolver(d->stream, shares, parts, denoms, n, dist_out_device, (Partial *)d->partials.p);
     }));
@@ -1743,17 +1736,17 @@ int iris_resolver_search_masks(iris_engine_t *e, const iris_db_t *db, uint64_t f
     Partial res{};
     if (db->k.layout == IRIS_LAYOUT_TILES) {
         const uint32_t np = n ? masks_resolve_partials(d->hooks, r) : 0;
-        CHK(ensure(d->partials, (size_t)std::max<uint32_t>(np, 1) * sizeof(Partial)));
+        CHK(ensure(d, d->partials, (size_t)std::max<uint32_t>(np, 1) * sizeof(Partial)));
         CHK(timed(d, "masks_resolve", n, [&] {
             return launch_masks_resolve(d->hooks, d->stream, db->data, e->qfrag, r, shares_device, parts, dist_out_device,
                                         (Partial *)d->partials.p);
         }));
         CHK(resolver_finish(d, np, &res));
     } else {
-        CHK(ensure(d->out_a, std::max<uint64_t>(n, 1) * kRot * 2));
+        CHK(ensure(d, d->out_a, std::max<uint64_t>(n, 1) * kRot * 2));
         CHK(timed(d, "masks", n, [&] { return launch_masks(d->stream, db->data, e->qtab, r, (uint16_t *)d->out_a.p); }));
         const uint32_t np = resolver_partials(n);
-        CHK(ensure(d->partials, (size_t)std::max<uint32_t>(np, 1) * sizeof(Partial)));
+        CHK(ensure(d, d->partials, (size_t)std::max<uint32_t>(np, 1) * sizeof(Partial)));
         CHK(timed(d, "resolver", n, [&] {
             return launch_resolver(d->stream, shares_device, parts, (const uint16_t *)d->out_a.p, n, dist_out_device,
                                    (Partial *)d->partials.p);
@@ -1774,7 +1767,7 @@ int iris_resolver_search_host(iris_device_t *d, const uint16_t *const *shares, u
     CHK(set_device(d));
     const uint64_t ch = std::min<uint64_t>(n, 1ull << 20);
     const size_t row = (size_t)kRot * 2;
-    CHK(ensure(d->staging, std::max<uint64_t>(ch, 1) * row * (parts + 1)));
+    CHK(ensure(d, d->staging, std::max<uint64_t>(ch, 1) * row * (parts + 1)));
     iris_match_t best;
     match_from(Partial{}, false, 0, &best);
     for (uint64_t done = 0; done < n; done += ch) {

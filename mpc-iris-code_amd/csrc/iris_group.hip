@@ -780,8 +780,8 @@ int iris_group_db_create(iris_group_t *g, int kind, uint64_t total, int layout, 
         iris_device *d = g->devs[i];
         std::lock_guard<std::recursive_mutex> l(d->mu);
         rc = set_device(d);
-        if (rc == 0) rc = ensure(gdb->send[i], (size_t)kSendRing * spd * sizeof(Partial));
-        if (rc == 0) rc = ensure(gdb->recv[i], (size_t)gdb->S * sizeof(Partial));
+        if (rc == 0) rc = ensure(d, gdb->send[i], (size_t)kSendRing * spd * sizeof(Partial));
+        if (rc == 0) rc = ensure(d, gdb->recv[i], (size_t)gdb->S * sizeof(Partial));
         for (uint32_t b = 0; rc == 0 && b < kSendRing; ++b)
             if (hipEventCreateWithFlags(&gdb->sent[i][b], hipEventDisableTiming) != hipSuccess) {
                 gdb->sent[i][b] = nullptr;
@@ -1075,8 +1075,8 @@ int iris_group_template_batch_search(iris_group_db_t *gdb, const iris_template_t
     for (size_t i = 0; i < L && rc == 0; ++i) {
         iris_device *d = g->devs[i];
         rc = set_device(d);
-        if (rc == 0) rc = ensure(send[i], (size_t)spd * stride * sizeof(Partial));
-        if (rc == 0) rc = ensure(recv[i], (size_t)S * stride * sizeof(Partial));
+        if (rc == 0) rc = ensure(d, send[i], (size_t)spd * stride * sizeof(Partial));
+        if (rc == 0) rc = ensure(d, recv[i], (size_t)S * stride * sizeof(Partial));
         if (rc == 0) rc = ensure_host_result(d, (size_t)stride * sizeof(Partial));
         if (rc == 0 && !(reached[i] = take_event(d))) rc = fail(IRIS_E_HIP, "hipEventCreate failed");
         if (rc == 0 && !(done[i] = take_event(d))) rc = fail(IRIS_E_HIP, "hipEventCreate failed");
@@ -1102,7 +1102,7 @@ int iris_group_template_batch_search(iris_group_db_t *gdb, const iris_template_t
                 const BatchGeometry geo = batch_geometry(d->hooks, LaunchRange{0, gdb->count[s]}, nq);
                 pmax = std::max(pmax, (size_t)geo.nqg * geo.qper * geo.G * sizeof(Partial));
             }
-            rc = ensure(d->partials, pmax);
+            rc = ensure(d, d->partials, pmax);
             for (uint32_t j = 0; rc == 0 && j < spd; ++j) {
                 const size_t s = i * spd + j;
                 if (gdb->count[s] == 0) continue;

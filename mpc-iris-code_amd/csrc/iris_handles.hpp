@@ -152,6 +152,9 @@ struct iris_device {
     std::vector<NotResident> not_resident;
     uint64_t resident_clock = 0;
     std::string resident_skip;  // why the last mapping refused was not made resident (iris_config)
+    // the copy a host-slice call is running on (or filling): never evicted under it (PinResident)
+    const struct iris_db *resident_pin = nullptr;
+    std::chrono::steady_clock::time_point resident_swept{};  // last sweep for copies of vanished mappings
     // read-ahead launches, the records they computed and the largest window, since the last
     // iris_device_reset_stats (iris_config "readahead_windows")
     uint64_t ra_launches = 0, ra_records = 0, ra_window_max = 0;
@@ -243,14 +246,18 @@ struct KeepDevice {
 };
 #define IRIS_KEEP_DEVICE() iris_api::KeepDevice keep_device_
 
-inline int ensure(DevBuf &b, size_t bytes) {
+// hipMalloc on the device; when it fails, resident file copies (iris_resident.hip, a cache) are
+// evicted least recently used first -- never the one a call is running on -- and it is tried
+// again.  IRIS_E_NOMEM once nothing is left to evict.  Caller holds the device lock.
+int dev_malloc(struct iris_device *d, void **p, size_t bytes, const char *what);
+
+inline int ensure(struct iris_device *d, DevBuf &b, size_t bytes) {
     if (bytes <= b.cap) return 0;
     if (b.p) HIPCHK(hipFree(b.p));
     b.p = nullptr;
     b.cap = 0;
     size_t want = std::max(bytes, (size_t)4096);
-    hipError_t e = hipMalloc(&b.p, want);
-    if (e != hipSuccess) return fail(IRIS_E_NOMEM, std::string("hipMalloc workspace: ") + hipGetErrorString(e));
+    CHK(dev_malloc(d, &b.p, want, "workspace"));
     b.cap = want;
     return 0;
 }
@@ -397,7 +404,7 @@ inline void db_detach(iris_db *db) {
 
 inline int ensure_ticket(iris_device *d) {
     if (d->ticket.p) return 0;
-    CHK(ensure(d->ticket, 4096));  // the top word + 8 sub-tickets 256 B apart (iris_device.hpp)
+    CHK(ensure(d, d->ticket, 4096));  // the top word + 8 sub-tickets 256 B apart (iris_device.hpp)
     HIPCHK(hipMemsetAsync(d->ticket.p, 0, 4096, d->stream));
     return 0;
 }
@@ -439,6 +446,19 @@ int db_store_locked(iris_db *db, uint64_t index, const void *records, uint64_t n
 int resident_slice(iris_device *d, int kind, const void *ptr, uint64_t n, iris_db **db, uint64_t *first,
                    uint64_t *end);
 void resident_drop_all(iris_device *d);  // frees every resident copy (waits for the device's streams)
+// frees the least recently used copy that no call is running on; false if there is none
+bool resident_evict_one(iris_device *d);
+// frees the copies whose mapping or file is gone (at most once a second unless forced)
+void resident_sweep(iris_device *d, bool force = false);
+// marks a resident copy as in use by the current call (no eviction frees it meanwhile)
+struct PinResident {
+    iris_device *d;
+    const iris_db *prev;
+    PinResident(iris_device *dev, const iris_db *db) : d(dev), prev(dev->resident_pin) { d->resident_pin = db; }
+    ~PinResident() { d->resident_pin = prev; }
+    PinResident(const PinResident &) = delete;
+    PinResident &operator=(const PinResident &) = delete;
+};
 // frees the copy of the mapping holding p and forgets refusals of addresses there; true if one was freed
 bool resident_drop_at(iris_device *d, uintptr_t p);
 // count and device bytes of the resident copies, and how many check their file through a held

@@ -402,6 +402,7 @@ void read_hooks(Hooks *h) {
     if (const char *v = env("IRIS_READAHEAD")) h->readahead = v[0] != '0';
     if (const char *v = env("IRIS_AUTO_RESIDENT")) h->auto_resident = v[0] != '0';
     if (const char *v = env("IRIS_GROUP_TIMEOUT_MS")) h->group_timeout_ms = env_u32(v, 24u * 3600 * 1000);
+    if (const char *v = env("IRIS_RESIDENT_MAX_MB")) h->resident_max_mb = env_u32(v, 1u << 30);
     const char *t = env("IRIS_TEST_HOOKS");
     h->test = t && t[0] == '1';
     for (int i = 0; i < kNumHooks; ++i) {
@@ -437,6 +438,7 @@ size_t format_hooks(const Hooks &h, char *buf, size_t len) {
                     (h.group_timeout_ms ? std::to_string(h.group_timeout_ms) : std::string("auto")) +
                     " group_init_timeout_ms=" +
                     std::to_string(h.group_timeout_ms ? h.group_timeout_ms : kGroupInitTimeoutMs) +
+                    " resident_max_mb=" + (h.resident_max_mb ? std::to_string(h.resident_max_mb) : std::string("auto")) +
                     " copy_helpers=" + std::to_string(copy_helpers()) + " test_hooks=" + std::to_string(h.test);
     if (h.test)
         s += " tiles_per_wave=" + (h.tiles_per_wave ? std::to_string(h.tiles_per_wave) : std::string("auto")) +

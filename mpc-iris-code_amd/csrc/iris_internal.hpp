@@ -175,6 +175,7 @@ struct Hooks {
     bool readahead = true;           // IRIS_READAHEAD=0: no read-ahead of host-output engine calls
     bool auto_resident = true;       // IRIS_AUTO_RESIDENT=0: host slices of read-only file mappings upload per call
     uint32_t group_timeout_ms = 0;   // IRIS_GROUP_TIMEOUT_MS: bound of a group exchange wait (0: auto)
+    uint32_t resident_max_mb = 0;    // IRIS_RESIDENT_MAX_MB: resident file copies hold at most this (0: half the device)
     // test-only hooks (IRIS_TEST_HOOKS=1)
     bool test = false;
     int tiles_per_wave = 0;          // IRIS_TILES_PER_WAVE=1|4: pins the TILES kernels' variant (0: by range)

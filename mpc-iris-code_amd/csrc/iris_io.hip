@@ -129,7 +129,7 @@ int iris_db_load_file(iris_db_t *db, const char *path, uint64_t first, uint64_t 
 
     const uint64_t ch = std::max<uint64_t>(1, kIoChunkBytes / k.rec_bytes);
     const size_t chb = ch * k.rec_bytes;
-    CHK(ensure(d->staging, 2 * chb));
+    CHK(ensure(d, d->staging, 2 * chb));
     const uint64_t base = db->len;
     Event done[2];
     for (int b = 0; b < 2; ++b) HIPCHK(hipEventCreateWithFlags(&done[b].e, hipEventDisableTiming));
@@ -277,7 +277,7 @@ int iris_db_save_file(const iris_db_t *db, const char *path, uint64_t first, uin
         HIPCHK(hipHostMalloc(&host[b].p, chb, hipHostMallocDefault));
         HIPCHK(hipEventCreateWithFlags(&ready[b].e, hipEventDisableTiming));
     }
-    CHK(ensure(d->staging, 2 * chb));
+    CHK(ensure(d, d->staging, 2 * chb));
     // issue chunk i's unpack + D2H, then write chunk i-1 while it runs
     uint64_t prev_off = 0, prev_m = 0;
     for (uint64_t off = 0, i = 0; off < n || prev_m; ++i) {
@@ -520,7 +520,7 @@ extern "C" int iris_prepare_shares(const iris_db_t *templates, uint64_t first, u
     const size_t per = tb + mb + (direct ? 0 : (size_t)parties * sb);
     const uint64_t ch = std::max<uint64_t>(64, (kStagingBytes / per) / 64 * 64);
     const uint64_t m0 = std::min<uint64_t>(ch, n);
-    CHK(ensure(d->staging, m0 * per));
+    CHK(ensure(d, d->staging, m0 * per));
     char *st_t = (char *)d->staging.p, *st_m = st_t + m0 * tb, *st_s = st_m + m0 * mb;
     std::vector<uint64_t> base(parties), tf(parties);
     std::vector<void *> dbp(parties);

@@ -229,33 +229,37 @@ Resident *make_resident(iris_device *d, int kind, uintptr_t p, uint64_t n) {
         if (!file_stat(o, &ost) || ost.st_ino != o->st.st_ino || ost.st_dev != o->st.st_dev || !vma_same(o, true))
             drop(d, o);
     }
-    // room: the device's free memory less a reserve, after evicting older copies if need be
+    // room: the device's free memory less a reserve, after evicting older copies if need be, and at
+    // most the cap of all copies together: IRIS_RESIDENT_MAX_MB, else half the device (a participant
+    // and a resolver process sharing a GPU cannot take all of it from each other); the test hook
+    // IRIS_RESIDENT_BUDGET_MB stands in for a full device
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return refuse("hipMemGetInfo failed");
     const size_t reserve = std::max<size_t>(2ull << 30, total_b / 32);
     size_t evictable = 0;
-    for (Resident *r : d->resident) evictable += r->dev_bytes;
-    // test hook: the copies together may hold at most this much (the eviction and refusal paths
-    // without filling a 288-GB device)
-    const size_t budget = (size_t)d->hooks.resident_budget_mb << 20;
-    if (dev_bytes + reserve > free_b + evictable || (budget && dev_bytes > budget))
-        return refuse("the file (" + std::to_string(dev_bytes >> 20) + " MB on the device) does not fit the free memory");
-    auto lru_drop = [&] {
-        auto lru = std::min_element(d->resident.begin(), d->resident.end(),
-                                    [](const Resident *a, const Resident *b) { return a->last_use < b->last_use; });
-        evictable -= (*lru)->dev_bytes;
-        drop(d, *lru);
-    };
-    while (dev_bytes + reserve > free_b && !d->resident.empty()) {
-        lru_drop();
+    for (Resident *r : d->resident)
+        if (r->db != d->resident_pin) evictable += r->dev_bytes;
+    const size_t cap = d->hooks.resident_budget_mb ? (size_t)d->hooks.resident_budget_mb << 20
+                       : d->hooks.resident_max_mb   ? (size_t)d->hooks.resident_max_mb << 20
+                                                    : total_b / 2;
+    size_t held = 0;
+    for (Resident *r : d->resident) held += r->dev_bytes;
+    if (dev_bytes + reserve > free_b + evictable || dev_bytes > cap || held - evictable + dev_bytes > cap)
+        return refuse("the file (" + std::to_string(dev_bytes >> 20) + " MB on the device) does not fit the free memory "
+                      "or the copies' cap (" + std::to_string(cap >> 20) + " MB)");
+    while (dev_bytes + reserve > free_b && resident_evict_one(d)) {
         if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return refuse("hipMemGetInfo failed");
     }
-    while (budget && evictable + dev_bytes > budget && !d->resident.empty()) lru_drop();
+    for (;;) {
+        held = 0;
+        for (Resident *r : d->resident) held += r->dev_bytes;
+        if (held + dev_bytes <= cap || !resident_evict_one(d)) break;
+    }
     Resident *r = new (std::nothrow) Resident();
     if (!r) return refuse("out of host memory");
     r->fd = fd;  // owned by r from here
     r->db = new (std::nothrow) iris_db();
-    if (!r->db || hipMalloc(&r->db->data, dev_bytes) != hipSuccess) {
+    if (!r->db || dev_malloc(d, &r->db->data, dev_bytes, "resident copy") != 0) {
         (void)hipGetLastError();
         if (r->db) r->db->data = nullptr;
         free_copy(d, r);
@@ -375,6 +379,7 @@ int iris_api::resident_slice(iris_device *d, int kind, const void *ptr, uint64_t
                              uint64_t *end) {
     *db = nullptr;
     if (!d->hooks.auto_resident || n == 0) return 0;
+    resident_sweep(d);
     const uintptr_t p = (uintptr_t)ptr;
     const size_t rb = kind_info(kind, IRIS_LAYOUT_TILES).rec_bytes;
     for (int attempt = 0; attempt < 2; ++attempt) {
@@ -411,6 +416,7 @@ int iris_api::resident_slice(iris_device *d, int kind, const void *ptr, uint64_t
             continue;
         }
         const uint64_t f = (p - r->base) / rb;
+        PinResident pin(d, r->db);  // the fill's workspaces may evict copies: not this one
         if (fill(d, r, f, n) != 0) {  // a short read (the file shrank) or an I/O error: this call uploads
             const uintptr_t lo = r->lo, hi = r->hi;
             drop(d, r);
@@ -435,6 +441,43 @@ int iris_api::resident_slice(iris_device *d, int kind, const void *ptr, uint64_t
 void iris_api::resident_drop_all(iris_device *d) {
     while (!d->resident.empty()) drop(d, d->resident.back());
     d->not_resident.clear();
+}
+
+bool iris_api::resident_evict_one(iris_device *d) {
+    Resident *lru = nullptr;
+    for (Resident *r : d->resident)
+        if (r->db != d->resident_pin && (!lru || r->last_use < lru->last_use)) lru = r;
+    if (!lru) return false;
+    drop(d, lru);
+    return true;
+}
+
+void iris_api::resident_sweep(iris_device *d, bool force) {
+    const auto t = std::chrono::steady_clock::now();
+    if (d->resident.empty() || (!force && t - d->resident_swept < std::chrono::seconds(1))) return;
+    d->resident_swept = t;
+    for (size_t i = d->resident.size(); i-- > 0;) {
+        Resident *r = d->resident[i];
+        if (r->db == d->resident_pin) continue;
+        struct stat st;
+        if (!file_stat(r, &st) || st.st_ino != r->st.st_ino || st.st_dev != r->st.st_dev || !vma_same(r, true))
+            drop(d, r);  // its mapping was unmapped or replaced, or its file is gone
+    }
+}
+
+int iris_api::dev_malloc(iris_device *d, void **p, size_t bytes, const char *what) {
+    hipError_t e = hipMalloc(p, bytes);
+    if (e == hipSuccess) return 0;
+    (void)hipGetLastError();
+    resident_sweep(d, true);
+    for (;;) {
+        e = hipMalloc(p, bytes);
+        if (e == hipSuccess) return 0;
+        (void)hipGetLastError();
+        if (!resident_evict_one(d)) break;
+    }
+    *p = nullptr;
+    return fail(IRIS_E_NOMEM, std::string("hipMalloc ") + what + " (" + std::to_string(bytes) + " B): " + hipGetErrorString(e));
 }
 
 bool iris_api::resident_drop_at(iris_device *d, uintptr_t p) {

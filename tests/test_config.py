@@ -16,14 +16,20 @@ TEST_HOOKS = ["IRIS_TILES_PER_WAVE", "IRIS_FUSED_REDUCE", "IRIS_BATCH_KERNEL", "
 @pytest.fixture(autouse=True)
 def clean_env(monkeypatch):
     for k in TEST_HOOKS + ["IRIS_TEST_HOOKS", "IRIS_READAHEAD", "IRIS_AUTO_RESIDENT", "IRIS_GROUP_TIMEOUT_MS",
-                           "IRIS_COPY_HELPERS"]:
+                           "IRIS_COPY_HELPERS", "IRIS_RESIDENT_MAX_MB"]:
         monkeypatch.delenv(k, raising=False)
 
 
 def test_defaults():
     c = ih.config()
     assert c == {"readahead": "1", "auto_resident": "1", "group_timeout_ms": "auto", "group_init_timeout_ms": "120000",
-                 "copy_helpers": "3", "test_hooks": "0"}
+                 "resident_max_mb": "auto", "copy_helpers": "3", "test_hooks": "0"}
+
+
+def test_resident_cap_is_a_production_knob(monkeypatch):
+    monkeypatch.setenv("IRIS_RESIDENT_MAX_MB", "4096")
+    c = ih.config()
+    assert c["resident_max_mb"] == "4096" and "ignored" not in c
 
 
 def test_group_timeout_sets_the_formation_bound(monkeypatch):

@@ -439,3 +439,47 @@ def test_drop_resident_range_after_writes_through_a_mapping(device, tmp_path):
         assert (walk(eng, recs) == want_fn(old)).all()
         assert device.resident()[0] == 2
     del recs, recs_b
+
+
+def test_copies_of_unmapped_files_are_swept(device, tmp_path):
+    """A copy whose mapping was unmapped frees its device memory at the next device sync (or
+    host-slice call) a second later, without a make_resident pass to notice it."""
+    import time
+    kind, n = ih.KIND_MASKS, 25_000
+    path = tmp_path / "u.masks"
+    gen(kind, SEED + 60, n).tofile(path)
+    recs = mapped(path, kind, n)
+    eng, _ = engine_and_oracle(device, kind, SEED + 61)
+    with eng:
+        walk(eng, recs)
+    assert device.resident()[0] == 1
+    recs._mmap.close()
+    del recs
+    gc.collect()
+    time.sleep(1.2)
+    device.synchronize()
+    assert device.resident() == (0, 0), device.config()
+
+
+def test_device_alloc_evicts_resident_copies(device, tmp_path):
+    """Device memory held by resident copies is a cache: an iris_device_alloc that does not fit
+    beside them evicts them (least recently used first) instead of failing."""
+    kind, n = ih.KIND_MASKS, 1_300_000  # a ~2 GB copy
+    path = tmp_path / "e.masks"
+    gen(kind, SEED + 62, n).tofile(path)
+    recs = mapped(path, kind, n)
+    eng, _ = engine_and_oracle(device, kind, SEED + 63)
+    with eng:
+        walk(eng, recs[:40_000])
+    count, held = device.resident()
+    assert count == 1 and held >= n * 1600
+    free, _ = device.memory()
+    ptrs = []
+    try:
+        ptrs.append(device.alloc(free - (1 << 30)))  # leaves 1 GB beside the 2-GB copy
+        ptrs.append(device.alloc(2 << 30))  # fits only once the copy is gone
+        assert device.resident() == (0, 0)
+    finally:
+        for p in ptrs:
+            device.free(p)
+    del recs
