@@ -285,6 +285,7 @@ int ra_wait(iris_engine *e) {
     if (!ra.computed[0]) return 0;
     iris_device *d = e->dev;
     if (d->aux) HIPCHK(hipStreamSynchronize(d->aux));
+    if (d->aux2) HIPCHK(hipStreamSynchronize(d->aux2));
     if (d->profiling) fold_done(d);
     return 0;
 }
@@ -413,16 +414,19 @@ int ra_launch(iris_engine *e, const iris_db *a, uint64_t first, uint64_t n, int 
     // (built there when the engine was created) and any write to the database.  An idle device
     // stream (the steady state of a chunk walk: its work is all on the side stream) needs no
     // event -- the cross-stream wait costs ~10 us per launch (profiles/r03_readahead.txt)
+    // buffer b's windows run on their own side stream: the next window's kernel is not queued
+    // behind this one's drain (the two write different buffers and only read the database)
+    hipStream_t side = b ? d->aux2 : d->aux;
     const hipError_t idle = hipStreamQuery(d->stream);
     if (idle != hipSuccess) {
         if (idle != hipErrorNotReady) return fail(IRIS_E_HIP, std::string("hipStreamQuery: ") + hipGetErrorString(idle));
         if (!d->ra_order) HIPCHK(hipEventCreateWithFlags(&d->ra_order, hipEventDisableTiming));
         HIPCHK(hipEventRecord(d->ra_order, d->stream));
-        HIPCHK(hipStreamWaitEvent(d->aux, d->ra_order, 0));
+        HIPCHK(hipStreamWaitEvent(side, d->ra_order, 0));
     }
     ra.win[b].live = false;
-    CHK(enqueue_u16_engine(e, a, first, n, (uint16_t *)ra.rows[b], d->aux, nullptr, ra_packed(e)));
-    HIPCHK(hipEventRecord(ra.computed[b], d->aux));
+    CHK(enqueue_u16_engine(e, a, first, n, (uint16_t *)ra.rows[b], side, nullptr, ra_packed(e)));
+    HIPCHK(hipEventRecord(ra.computed[b], side));
     ra.win[b] = Readahead::Window{a, a->version, first, n, true};
     d->ra_launches += 1;
     d->ra_records += n;
@@ -625,7 +629,7 @@ void device_teardown(iris_device *d) {
         (void)hipStreamSynchronize(d->stream);
         for (DevBuf *b : {&d->partials, &d->result, &d->staging, &d->out_a, &d->out_b, &d->ticket, &d->tempdb})
             if (b->p) (void)hipFree(b->p);
-        if (d->aux) (void)hipStreamSynchronize(d->aux);
+        side_sync(d);
         for (int b = 0; b < 2; ++b) {
             if (d->apart[b].p) (void)hipFree(d->apart[b].p);
             if (d->apart_read[b]) (void)hipEventDestroy(d->apart_read[b]);
@@ -636,6 +640,7 @@ void device_teardown(iris_device *d) {
             if (d->upin_ev[b]) (void)hipEventDestroy(d->upin_ev[b]);
         }
         if (d->aux) (void)hipStreamDestroy(d->aux);
+        if (d->aux2) (void)hipStreamDestroy(d->aux2);
         if (d->host_result) (void)hipHostFree(d->host_result);
         if (d->host_done) (void)hipHostFree(d->host_done);
         for (void *b : d->slot_blocks) (void)hipHostFree(b);
@@ -948,7 +953,7 @@ int iris_db_destroy(iris_db_t *db) {
         std::lock_guard<std::recursive_mutex> g(d->mu);
         (void)hipSetDevice(d->ordinal);
         (void)hipStreamSynchronize(d->stream);
-        if (d->aux) (void)hipStreamSynchronize(d->aux);  // a read-ahead kernel may still read it
+        side_sync(d);  // a read-ahead kernel may still read it
         db_detach(db);
         if (db->data) (void)hipFree(db->data);
     }

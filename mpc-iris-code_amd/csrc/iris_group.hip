@@ -110,7 +110,7 @@ void group_teardown(iris_group *g) {
         live = true;
         (void)hipSetDevice(g->devs[i]->ordinal);
         (void)hipStreamSynchronize(g->devs[i]->stream);
-        if (g->devs[i]->aux) (void)hipStreamSynchronize(g->devs[i]->aux);
+        side_sync(g->devs[i]);
     }
     // One thread owns all local communicators: finalize them inside one RCCL group (each flushes
     // its outstanding work without waiting for the others), then destroy them.  Aborted
@@ -616,7 +616,7 @@ void gdb_free_locked(iris_group_db *gdb) {
         iris_device *d = g->devs[i];
         std::lock_guard<std::recursive_mutex> l(d->mu);
         (void)hipSetDevice(d->ordinal);
-        if (d->aux) (void)hipStreamSynchronize(d->aux);
+        side_sync(d);
         if (gdb->send[i].p) (void)hipFree(gdb->send[i].p);
         if (gdb->recv[i].p) (void)hipFree(gdb->recv[i].p);
         if (i < gdb->sent.size())
@@ -928,7 +928,7 @@ int iris_group_template_search_async(iris_group_db_t *gdb, const iris_template_t
             for (iris_device *d : g->devs) {
                 (void)hipSetDevice(d->ordinal);
                 (void)hipStreamSynchronize(d->stream);
-                if (d->aux) (void)hipStreamSynchronize(d->aux);
+                side_sync(d);
             }
         }
         if (drained)  // otherwise aborted work may still write them: leaked rather than reused

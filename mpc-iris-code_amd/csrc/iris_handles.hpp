@@ -118,6 +118,9 @@ struct iris_device {
     // this one's kernel ends: partials alternate between two buffers, each guarded by the
     // event recorded after the last reduce that read it (created on first use)
     hipStream_t aux = nullptr;
+    // read-ahead windows alternate between aux (buffer 0) and aux2 (buffer 1), so that a window's
+    // kernel starts on the CUs the one before it leaves while it drains (created with aux)
+    hipStream_t aux2 = nullptr;
     DevBuf apart[2];
     hipEvent_t apart_read[2] = {nullptr, nullptr}, apart_written[2] = {nullptr, nullptr};
     int apart_next = 0;
@@ -378,6 +381,7 @@ inline void fold_done(iris_device *d) {
 inline int sync(iris_device *d) {
     HIPCHK(hipStreamSynchronize(d->stream));
     if (d->aux) HIPCHK(hipStreamSynchronize(d->aux));
+    if (d->aux2) HIPCHK(hipStreamSynchronize(d->aux2));
     fold_done(d);
     return 0;
 }
@@ -411,7 +415,14 @@ inline int ensure_ticket(iris_device *d) {
 
 inline int ensure_aux(iris_device *d) {
     if (!d->aux) HIPCHK(hipStreamCreateWithFlags(&d->aux, hipStreamNonBlocking));
+    if (!d->aux2) HIPCHK(hipStreamCreateWithFlags(&d->aux2, hipStreamNonBlocking));
     return 0;
+}
+
+// Waits for the side streams (errors ignored: teardown paths)
+inline void side_sync(iris_device *d) {
+    if (d->aux) (void)hipStreamSynchronize(d->aux);
+    if (d->aux2) (void)hipStreamSynchronize(d->aux2);
 }
 
 // Shared by the API translation units (defined in iris_api.hip).

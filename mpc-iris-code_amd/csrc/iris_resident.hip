@@ -87,7 +87,7 @@ bool same_time(const struct timespec &a, const struct timespec &b) {
 void free_copy(iris_device *d, Resident *r) {
     // a read-ahead kernel on the side stream may still read the copy
     (void)hipStreamSynchronize(d->stream);
-    if (d->aux) (void)hipStreamSynchronize(d->aux);
+    side_sync(d);
     if (r->db) {
         if (r->db->data) (void)hipFree(r->db->data);
         delete r->db;

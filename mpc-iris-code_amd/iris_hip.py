@@ -762,8 +762,17 @@ class _Engine:
         `db` is a Database (records [first, first+n)) or a host array / list of records.
         `out` is a [n, 31] uint16 array (filled in place)."""
         lib = load_library()
-        if out.dtype != np.uint16 or not out.flags["C_CONTIGUOUS"] or out.ndim != 2 or out.shape[1] != ROTATIONS:
+        if out.dtype != np.uint16 or not out.flags.c_contiguous or out.ndim != 2 or out.shape[1] != ROTATIONS:
             raise IrisError(-1, "out must be a C-contiguous [n, 31] uint16 array")
+        dt, width = _REC_DTYPE[self.kind]
+        if (isinstance(db, np.ndarray) and db.dtype == dt and db.ndim == 2 and db.shape[1] == width
+                and db.flags.c_contiguous and out.shape[0] == db.shape[0]):
+            # the chunk walk's call (a contiguous slice of the caller's record array): passed as is,
+            # with none of the conversions below (~11 -> ~4 us of Python per call)
+            rc = lib.iris_engine_batch_process_host(self.handle, db.ctypes.data, db.shape[0], out.ctypes.data)
+            if rc:
+                _check(rc)
+            return out
         if isinstance(db, Database):
             n = (len(db) - first) if n is None else n
             if out.shape[0] != n:  # assert_eq!(out.len(), db.len()) (src/lib.rs:43,70)
