@@ -1,7 +1,7 @@
 """Per-call times of the reference's chunk walk (20 000-record batch_process calls, one engine
 per walk as the participant builds one per request) over a mapped record file (the library's
 resident copy, no attach) and over an attached anonymous array, side by side:
-    python tools/walk_calls.py [masks|shares] [walks]"""
+    python tools/walk_calls.py [masks|shares] [walks] [records]"""
 import os
 import sys
 import tempfile
@@ -16,10 +16,12 @@ kind_name = sys.argv[1] if len(sys.argv) > 1 else "shares"
 walks = int(sys.argv[2]) if len(sys.argv) > 2 else 4
 shares = kind_name == "shares"
 n, chunk = (200_000, 20_000) if shares else (2_000_000, 20_000)
+if len(sys.argv) > 3:
+    n = int(sys.argv[3])
 kind = ih.KIND_SHARES if shares else ih.KIND_MASKS
 rng = np.random.default_rng(3)
 host = (rng.integers(0, 65536, (n, 12800), dtype=np.uint16) if shares
-        else rng.integers(0, 2**63, (n, 200), dtype=np.uint64))
+        else rng.integers(0, 2**63, (n, 200), dtype=np.uint64))  # noqa: E501
 path = os.path.join(tempfile.gettempdir(), f"walk_calls_{os.getpid()}.rec")
 host.tofile(path)
 mm = np.memmap(path, dtype=host.dtype, mode="r", shape=host.shape)
@@ -54,8 +56,10 @@ db.attach_host(host)
 for label, arr in (("mmap", mm), ("attached", host)):
     for w in range(walks):
         t_eng, times, t_all = walk(arr)
-        print(f"{label} walk {w}: engine {t_eng * 1e6:.0f} us, walk {t_all * 1e3:.3f} ms, calls us:",
-              " ".join(f"{x * 1e6:.0f}" for x in times), flush=True)
+        st = sorted(times)
+        print(f"{label} walk {w}: engine {t_eng * 1e6:.0f} us, walk {t_all * 1e3:.3f} ms ({n / t_all:.3g} records/s), "
+              f"calls us median {st[len(st) // 2] * 1e6:.1f} p90 {st[len(st) * 9 // 10] * 1e6:.1f}, first ones:",
+              " ".join(f"{x * 1e6:.0f}" for x in times[:12]), flush=True)
 print("config:", {k: v for k, v in dev.config().items() if k.startswith("resident")})
 db.close()
 dev.close()
