@@ -797,19 +797,48 @@ def run_aux(args, dev):
         dev.synchronize()
         extra["kernel_times_from"] = "a separate profiled pass of the same steps (the timed steps run unprofiled)"
         ra = [int(x) for x in dev.config().get("readahead_windows", "0/0/0").split("/")]
-        big_items, big_ms = dev.kernel_stats_largest("shares" if shares_wl else "masks")
+        walk_stats = dev.kernel_stats(kname)
+        # the walk's largest window as one launch on its own (in the walk, consecutive windows run on
+        # two side streams and overlap, so their event times are not per-kernel durations): the same
+        # engine kernel over that many resident records, [u16;31] rows to HBM
+        big = ra[2]
+        alone = None
+        if big:
+            with ih.Database(dev, kind, big) as bdb:
+                bdb.generate(big, SEED + 3)
+                bout = dev.alloc(big * ROT * 2)
+                try:
+                    with new_engine() as beng:
+                        beng.batch_process_device(bdb, bout, 0, big)
+                        dev.synchronize()
+                        dev.reset_stats()
+                        dev.set_profiling(True)
+                        for _ in range(5):
+                            beng.batch_process_device(bdb, bout, 0, big)
+                        dev.synchronize()
+                        dev.set_profiling(False)
+                finally:
+                    dev.free(bout)
+            bl, bms, _ = dev.kernel_stats("shares" if shares_wl else "masks")
+            bms /= max(1, bl)
+            alone = {"records": big, "kernel_ms": bms,
+                     "hbm_frac": big * rec_bytes / (bms * 1e-3) / 1e9 / HBM_PEAK_GBS if bms else None,
+                     "is": "the largest window's size as one device-output launch on its own, 5 launches"}
         extra["readahead"] = {
             "launches_per_walk": ra[0] / args.steps, "records_computed_per_walk": ra[1] / args.steps,
             "largest_window_records": ra[2],
-            "largest_launch": {"records": big_items, "kernel_ms": big_ms,
-                               "hbm_frac": (big_items * rec_bytes / (big_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
-                                            if big_ms else None)},
+            "largest_window_kernel_alone": alone,
             "windows": "1, 2, 4, ... chunks up to 64 MB of rows, at most half of what is left of the walk",
             "rows_over_host_link": ("packed: 32 B per record (base + 31 byte offsets, full-row escape)"
                                     if not shares_wl else "[u16;31]: 62 B per record")}
     dev.set_profiling(False)
-    launches, kms, items = dev.kernel_stats(kname)
+    launches, kms, items = walk_stats if separate else dev.kernel_stats(kname)
     achieved = rec_bytes * items / (kms * 1e-3) / 1e9
+    if separate:
+        # host-slice walks: end to end, the records' bytes over the walk's wall time (their windows'
+        # kernels overlap on two side streams, so summed kernel times are not a duration)
+        achieved = rec_bytes * n * args.steps / elapsed / 1e9
+        extra["roofline_is"] = "end to end: the walked records' bytes / the timed walks' wall time"
     if args.workload == "resolve-masks":  # denominators from the (separately checked) masks engine
         denoms = np.empty((n, ROT), np.uint16)
         eng.batch_process(denoms, mdb)
