@@ -98,7 +98,7 @@ const char *iris_version(void);
  * (IRIS_TILES_PER_WAVE, IRIS_FUSED_REDUCE, IRIS_BATCH_KERNEL, IRIS_SCHEDULE,
  * IRIS_LOAD_PREAD, IRIS_LOAD_WINDOWS, IRIS_GROUP_DELAY_US, IRIS_GROUP_STALL,
  * IRIS_GROUP_UNORDERED, IRIS_UPLOAD, IRIS_READAHEAD_WINDOW, IRIS_RESIDENT_BUDGET_MB,
- * IRIS_READAHEAD_PACKED) take effect only with IRIS_TEST_HOOKS=1;
+ * IRIS_READAHEAD_PACKED, IRIS_READAHEAD_WINDOW_MAX) take effect only with IRIS_TEST_HOOKS=1;
  * otherwise they are ignored and listed as "ignored=...".  With dev != NULL the
  * device's own facts follow: numa_node= (host NUMA node of its PCI function, -1
  * unknown), upload_gbps=P/R (recent rates of large writes through the pinned

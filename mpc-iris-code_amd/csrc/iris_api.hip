@@ -241,14 +241,13 @@ int run_u16_engine(iris_engine *e, const iris_db *db, uint64_t first, uint64_t n
 // calls of at most this many records (62 MB of rows per buffer) go through the read-ahead
 constexpr uint64_t kReadaheadMax = 1ull << 20;
 // A walk's read-ahead windows grow geometrically: the walk's first window is one chunk, each later
-// one twice the chunks of the window before it, up to kWindowRowsMax of rows per buffer (~1M
-// records), and never more than half of what is left of the resident run (at least one chunk).  A
-// launch costs a ramp and a drain (~74 us of a 100k-share window's 446 us, profiles/
-// r05u_shares_window_kernels.txt), so a long walk's big windows run at the full-launch rate; the
-// first calls keep the latency of small ones, and the walk's tail windows shrink so that the rows
-// of its last window (copied out after the device is done) are few.
-constexpr size_t kWindowRowsMax = 64ull << 20;
-
+// one twice the chunks of the window before it, up to kWindowRecords records (and kWindowRowsMax of
+// rows per buffer).  Consecutive windows run on two side streams, so a window's kernel starts on
+// the CUs the one before it leaves while it drains: the ramp and drain of a launch (~74 us of a
+// 100k-share window's 446 us on one stream, profiles/r05u_shares_window_kernels.txt) no longer
+// call for big windows, and a call waits for its whole window, so windows beyond ~160k records
+// only delay the host (a 3M-mask walk: 1.03e9 records/s from C++ with windows up to 880k,
+// profiles/r06c_walk_host_masks.txt; measured per cap in profiles/r06d_window_caps.txt).
 // A MasksEngine window's rows cross the host link packed (store_tile_packed, iris_device.hpp): 32 B
 // per record, then an escape row of 31 u16 per record that only rows spanning more than a byte
 // use; the copy-out expands them into the caller's [u16; 31] (parallel_expand).  The resolver's
@@ -258,16 +257,21 @@ bool ra_packed(const iris_engine *e) { return e->kind == IRIS_KIND_MASKS && e->d
 // bytes of a read-ahead buffer per record
 size_t ra_rec_bytes(const iris_engine *e) { return ra_packed(e) ? kPackedRecBytes + kRot * 2 : kRot * 2; }
 
-uint64_t window_chunks_max(uint64_t n) { return std::max<uint64_t>(1, kWindowRowsMax / ((size_t)n * kRot * 2)); }
+constexpr uint64_t kWindowRecords = 160000;
+constexpr size_t kWindowRowsMax = 64ull << 20;
+
+uint64_t window_chunks_max(const iris_db *db, uint64_t n) {
+    uint64_t w = std::max<uint64_t>(1, kWindowRecords / n);
+    if (db->dev->hooks.ra_window_max) w = db->dev->hooks.ra_window_max;  // test hook: another cap
+    return std::max<uint64_t>(1, std::min<uint64_t>(w, kWindowRowsMax / ((size_t)n * kRot * 2)));
+}
 
 // Records of a walk's window of chunks of n records that follows a window of `prev` records (0: the
 // walk's first window), with `avail` records left in the run.
 uint64_t window_records(const iris_db *db, uint64_t n, uint64_t prev, uint64_t avail) {
     uint64_t w = prev ? 2 * ((prev + n - 1) / n) : 1;
-    const uint64_t left = (avail + n - 1) / n;
-    w = std::min(w, std::max<uint64_t>(1, (left + 1) / 2));
     if (db->dev->hooks.ra_window) w = db->dev->hooks.ra_window;  // test hook: a fixed window
-    w = std::min(w, window_chunks_max(n));
+    w = std::min(w, window_chunks_max(db, n));
     return std::min<uint64_t>(w * n, avail);
 }
 
@@ -459,7 +463,7 @@ int readahead_u16_call(iris_engine *e, const iris_db *a, uint64_t first, uint64_
         // a walk's window follows the one the walk was in; a random-access call computes its range
         const uint64_t wn = walk ? window_records(a, n, ra.grow ? ra.grow : n, end - first) : n;
         // new buffers take the walk's largest window (not reallocated under it as the windows grow)
-        const uint64_t reserve = std::min<uint64_t>(window_chunks_max(n) * n, end - first);
+        const uint64_t reserve = std::min<uint64_t>(window_chunks_max(a, n) * n, end - first);
         CHK(ra_launch(e, a, first, std::max(wn, n), b, true, nullptr, reserve));
         ra.grow = std::max(wn, n);
     }

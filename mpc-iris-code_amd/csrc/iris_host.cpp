@@ -407,7 +407,7 @@ constexpr const char *kHookNames[] = {"IRIS_TILES_PER_WAVE",  "IRIS_FUSED_REDUCE
                                       "IRIS_SCHEDULE",        "IRIS_LOAD_PREAD",   "IRIS_GROUP_DELAY_US",
                                       "IRIS_GROUP_STALL",     "IRIS_GROUP_UNORDERED", "IRIS_UPLOAD",
                                       "IRIS_LOAD_WINDOWS",    "IRIS_READAHEAD_WINDOW", "IRIS_RESIDENT_BUDGET_MB",
-                                      "IRIS_READAHEAD_PACKED"};
+                                      "IRIS_READAHEAD_PACKED", "IRIS_READAHEAD_WINDOW_MAX"};
 constexpr int kNumHooks = (int)(sizeof(kHookNames) / sizeof(kHookNames[0]));
 
 const char *env(const char *name) {
@@ -451,6 +451,7 @@ void read_hooks(Hooks *h) {
         case 10: h->ra_window = env_u32(v, 64); break;
         case 11: h->resident_budget_mb = env_u32(v, 1u << 30); break;
         case 12: h->ra_packed = v[0] != '0'; break;
+        case 13: h->ra_window_max = env_u32(v, 1024); break;
         }
     }
 }
@@ -473,6 +474,7 @@ size_t format_hooks(const Hooks &h, char *buf, size_t len) {
              " load_windows=" + std::to_string(h.load_windows) + " readahead_window=" + std::to_string(h.ra_window) +
              " resident_budget_mb=" + std::to_string(h.resident_budget_mb) +
              " readahead_packed=" + std::to_string(h.ra_packed) +
+             " readahead_window_max=" + std::to_string(h.ra_window_max) +
              " group_delay_us=" + std::to_string(h.group_delay_us) +
              " group_stall=" + std::to_string(h.group_stall) + " group_unordered=" + std::to_string(h.group_unordered) +
              " upload=" + upload_names[h.upload & 3];

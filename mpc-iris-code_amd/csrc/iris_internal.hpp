@@ -191,6 +191,7 @@ struct Hooks {
     uint32_t ra_window = 0;          // IRIS_READAHEAD_WINDOW=1..64: chunks per read-ahead window (0: growing)
     uint32_t resident_budget_mb = 0; // IRIS_RESIDENT_BUDGET_MB: resident copies hold at most this (0: free memory)
     bool ra_packed = true;           // IRIS_READAHEAD_PACKED=0: masks read-ahead rows cross the host link unpacked
+    uint32_t ra_window_max = 0;      // IRIS_READAHEAD_WINDOW_MAX=1..1024: cap of a read-ahead window, chunks (0: by records)
     uint32_t ignored = 0;            // bit i: test hook kHookNames[i] was set without IRIS_TEST_HOOKS=1
 };
 // The bound of forming a device group when IRIS_GROUP_TIMEOUT_MS is not set (iris_group.hip)

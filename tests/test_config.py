@@ -10,7 +10,7 @@ import iris_hip as ih
 TEST_HOOKS = ["IRIS_TILES_PER_WAVE", "IRIS_FUSED_REDUCE", "IRIS_BATCH_KERNEL", "IRIS_SCHEDULE",
               "IRIS_LOAD_PREAD", "IRIS_GROUP_DELAY_US", "IRIS_GROUP_STALL", "IRIS_GROUP_UNORDERED", "IRIS_UPLOAD",
               "IRIS_LOAD_WINDOWS", "IRIS_READAHEAD_WINDOW", "IRIS_RESIDENT_BUDGET_MB",
-              "IRIS_READAHEAD_PACKED"]
+              "IRIS_READAHEAD_PACKED", "IRIS_READAHEAD_WINDOW_MAX"]
 
 
 @pytest.fixture(autouse=True)
