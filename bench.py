@@ -828,7 +828,7 @@ def run_aux(args, dev):
             "launches_per_walk": ra[0] / args.steps, "records_computed_per_walk": ra[1] / args.steps,
             "largest_window_records": ra[2],
             "largest_window_kernel_alone": alone,
-            "windows": "1, 2, 4, ... chunks up to 64 MB of rows, at most half of what is left of the walk",
+            "windows": "1, 2, 4, ... chunks up to 160 000 records, alternating between two side streams",
             "rows_over_host_link": ("packed: 32 B per record (base + 31 byte offsets, full-row escape)"
                                     if not shares_wl else "[u16;31]: 62 B per record")}
     dev.set_profiling(False)

@@ -50,7 +50,10 @@ using namespace iris_api;
 namespace {
 
 constexpr size_t kGranuleBytes = 256ull << 20;  // residency unit of a copy
-constexpr size_t kFillRunBytes = 4ull << 30;    // a fill reads ahead up to this much in one pipelined write
+// a fill reads ahead up to this much in one pipelined write, under the device lock: 1 GB keeps a
+// first walk's fill near the load path's rate while another thread's calls on the device wait at
+// most ~25 ms for it (4 GB runs held them ~0.1 s)
+constexpr size_t kFillRunBytes = 1ull << 30;
 constexpr size_t kSnapBytes = 64;              // probe snapshot of every 64th record
 constexpr uint64_t kSnapStride = 64;
 constexpr size_t kNotResidentMax = 4096;       // remembered ineligible address ranges
@@ -67,6 +70,7 @@ struct Resident {
     std::string link;          // /proc/self/map_files/<lo>-<hi>
     int fd = -1;               // >= 0: map_files unreadable; the mapped file, held open
     uint64_t inode = 0;        // of the mapping (/proc/self/maps)
+    uint64_t vma_off = 0;      // the mapping's file offset (/proc/self/maps)
     std::string path;
     std::chrono::steady_clock::time_point vma_checked;
     struct stat st {};
@@ -152,15 +156,17 @@ bool file_stat(const Resident *r, struct stat *st) {
     return r->fd >= 0 ? fstat(r->fd, st) == 0 : stat(r->link.c_str(), st) == 0;
 }
 
-// Whether the mapping is still the one the copy was made of.  map_files answers that with every
-// stat; the descriptor form re-reads /proc/self/maps when asked (now) and at least every 200 ms.
+// Whether the mapping is still the one the copy was made of: the same range, file, path, file
+// offset and read-only.  map_files answers the file with every stat but not the offset (the same
+// file mapped again at the same address from another offset), so both forms re-read
+// /proc/self/maps when asked (now) and at least every 200 ms; the slice probe covers a remap in
+// between.
 bool vma_same(Resident *r, bool now) {
-    if (r->fd < 0) return true;
     const auto t = std::chrono::steady_clock::now();
     if (!now && t - r->vma_checked < std::chrono::milliseconds(200)) return true;
     Vma v;
     if (!find_vma(r->lo, &v) || v.lo != r->lo || v.hi != r->hi || v.inode != r->inode || v.path != r->path ||
-        v.perms[1] != '-')
+        v.off != r->vma_off || v.perms[1] != '-')
         return false;
     r->vma_checked = t;
     return true;
@@ -283,6 +289,7 @@ Resident *make_resident(iris_device *d, int kind, uintptr_t p, uint64_t n) {
     r->nrec = nrec;
     r->link = link;
     r->inode = v.inode;
+    r->vma_off = v.off;
     r->path = v.path;
     r->vma_checked = std::chrono::steady_clock::now();
     r->st = st;

@@ -483,3 +483,24 @@ def test_device_alloc_evicts_resident_copies(device, tmp_path):
         for p in ptrs:
             device.free(p)
     del recs
+
+
+def test_same_file_remapped_at_another_offset(device, tmp_path):
+    """The same file unmapped and mapped again from another file offset (64 records = 100 KiB in,
+    page aligned), wherever the new mapping lands -- at the old address the file's inode, size and
+    times all still match: the rows are those of the records at the new offset."""
+    kind, n, skip = ih.KIND_MASKS, 40_000, 64
+    path = tmp_path / "o.masks"
+    host = gen(kind, SEED + 70, n)
+    host.tofile(path)
+    eng, want_fn = engine_and_oracle(device, kind, SEED + 71)
+    want = want_fn(host)
+    with eng:
+        a = mapped(path, kind, n)
+        assert (walk(eng, a) == want).all()
+        a._mmap.close()
+        del a
+        gc.collect()
+        b = np.memmap(path, dtype=np.uint64, mode="r", offset=skip * 1600, shape=(n - skip, 200))
+        assert (walk(eng, b) == want[skip:]).all()
+        del b
