@@ -266,12 +266,24 @@ int iris_engine_batch_process_device(iris_engine_t *engine, const iris_db_t *db,
  * participant and resolver walk (src/main.rs:386-391, 426-431; 455-460,
  * 511-516) -- runs on the device's copy of that file's records, made on first
  * use (read from the file in 256-MB granules, a call's missing ones and up to
- * 4 GB after them at once; a read that comes up short -- the file shrank --
- * drops the copy and the call uploads its slice) and kept; every call re-checks the
- * file behind the mapping (device, inode, size, mtime, ctime) and probes three
- * records of the slice, and a changed file is copied afresh.  Files that do not
- * fit the device's free memory (less a reserve) and IRIS_AUTO_RESIDENT=0 keep
- * the upload path.  Any other slice is uploaded (PCIe) and packed first. */
+ * 1 GB after them at once; a read that comes up short -- the file shrank --
+ * drops the copy and the call uploads its slice) and kept.  Like the reference,
+ * which maps the file once and treats it as immutable (src/main.rs:389; "Sync
+ * from database" is a TODO at :402,415), the copy stands for the file as it was
+ * read.  What every call re-checks: the file behind the mapping (device, inode,
+ * size, mtime, ctime), so write(2), truncate, replace or rename-over, and a
+ * mapping unmapped or replaced at the same address, drop the copy; the mapping's
+ * file offset, at least every 200 ms; and three 64-byte snapshots of records in
+ * the slice, which catch a change inside them whose timestamps did not move.
+ * What it cannot see: stores through a writable MAP_SHARED mapping (this process's
+ * or another's) into pages already dirty, which move no timestamp, outside the
+ * three probed snapshots -- such records are served as they were read, for as
+ * long as the copy lives.  A caller that changes its file that way calls
+ * iris_device_drop_resident_range.  Copies are a cache: together at most
+ * IRIS_RESIDENT_MAX_MB (default half the device), evicted least recently used
+ * when a device allocation would fail, freed when their mapping is gone.  Files
+ * that do not fit and IRIS_AUTO_RESIDENT=0 keep the upload path.  Any other
+ * slice is uploaded (PCIe) and packed first. */
 int iris_engine_batch_process_host(iris_engine_t *engine, const void *db, uint64_t n, uint16_t *out);
 /* Frees the device's resident file copies (a failing iris_db_create does so too
  * before it retries); iris_config reports them as resident=count/bytes. */
