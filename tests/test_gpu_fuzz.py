@@ -113,3 +113,56 @@ def test_fused_reduce_equals_reduce_kernel(device, hooked_device):
             if it % 25 == 0:
                 best, idx = oc.argmin(oc.template_distances(q, ref[first:first + cnt]))
                 assert a.index == idx + first + 7 and a.distance == best
+
+
+@pytest.mark.parametrize("tiles_per_wave", ["auto", "1", "4"])
+def test_fuzz_readahead_walks(device, hooked_device, tiles_per_wave):
+    """The read-ahead (growing windows on two side streams; masks rows packed to 32 B with a
+    full-row escape) under random walks over a resident database: 40 walks of random chunk sizes
+    (1..4 000 records) from random starting records, some abandoned after a few calls, some
+    broken by a random-access call, against the oracle's rows.  Masks are a mix of random and
+    block (occlusion-like) records, so packed and escaped rows interleave within tiles; the query
+    alternates between a random and a block mask."""
+    if tiles_per_wave != "auto":
+        device = hooked_device(IRIS_TILES_PER_WAVE=tiles_per_wave)
+    rng = np.random.default_rng(77)
+    n = 30_000
+    masks = oc.gen_masks(78, 0, n)
+    for i in range(0, n, 4):
+        c0, w = int(rng.integers(0, 200)), int(rng.integers(10, 150))
+        bits = np.zeros((64, 200), np.uint8)
+        bits[:, (np.arange(w) + c0) % 200] = 1
+        masks[i] = np.packbits(bits.reshape(12800), bitorder="little").view(np.uint64)
+    qblock = np.zeros((64, 200), np.uint8)
+    qblock[:, 30:130] = 1
+    queries = [oc.gen_masks(79, 0, 1)[0], np.packbits(qblock.reshape(12800), bitorder="little").view(np.uint64)]
+    wants = [oc.masks_batch(q, masks) for q in queries]
+    shares = np.random.default_rng(80).integers(0, 2**16, (3_000, 12800), dtype=np.uint16)
+    qs = shares[17].copy()
+    want_s = oc.distance_batch(qs, shares)
+    with ih.Database(device, ih.KIND_MASKS, n) as mdb, ih.Database(device, ih.KIND_SHARES, len(shares)) as sdb:
+        mdb.append(masks)
+        sdb.append(shares)
+        for walk in range(40):
+            kind = "shares" if walk % 5 == 4 else "masks"
+            db, total = (sdb, len(shares)) if kind == "shares" else (mdb, n)
+            want = want_s if kind == "shares" else wants[walk % 2]
+            eng = ih.DistanceEngine(device, qs) if kind == "shares" else ih.MasksEngine(device, queries[walk % 2])
+            with eng:
+                chunk = int(rng.integers(1, 4_001 if kind == "masks" else 400))
+                a = int(rng.integers(0, total))
+                calls = int(rng.integers(1, 40))
+                for c in range(calls):
+                    if a >= total:
+                        break
+                    if c and rng.random() < 0.1:  # a random-access call inside the walk
+                        r0 = int(rng.integers(0, total))
+                        r1 = min(total, r0 + int(rng.integers(1, 3_000)))
+                        out = np.empty((r1 - r0, ROT), np.uint16)
+                        eng.batch_process(out, db, first=r0, n=r1 - r0)
+                        assert (out == want[r0:r1]).all(), (walk, "random", r0, r1)
+                    m = min(chunk, total - a)
+                    out = np.empty((m, ROT), np.uint16)
+                    eng.batch_process(out, db, first=a, n=m)
+                    assert (out == want[a:a + m]).all(), (walk, kind, chunk, a, m)
+                    a += m
