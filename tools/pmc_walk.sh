@@ -20,7 +20,7 @@ for c in ("FETCH_SIZE", "WRITE_SIZE"):
     s, k = 0.0, set()
     for f in glob.glob(f"{o}/pmc_walk_{c}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
-            if r["Counter_Name"] == c and "masks_" in r["Kernel_Name"]:
+            if r["Counter_Name"] == c and ("masks_mfma_kernel" in r["Kernel_Name"] or "masks_split_kernel" in r["Kernel_Name"]):
                 s += float(r["Counter_Value"])
                 k.add(r["Kernel_Name"].split("(")[0])
     tot[c] = (s, sorted(k))
