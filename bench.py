@@ -688,6 +688,7 @@ def run_aux(args, dev):
             extra["first_walk_s"] = time.perf_counter() - t_first
             extra["resident"] = dict(zip(("count", "bytes"), dev.resident()))
         extra["host_pages_numa"] = {"pages_by_node": pages_nodes(host), "gpu_node": dev.config().get("numa_node")}
+        extra["copy_helpers"] = int(dev.config().get("copy_helpers", 0))  # copy-out threads besides the caller
         if args.attached:  # the mmap'd file's device copy (iris_db_attach_host), made once
             adb = ih.Database(dev, kind, n)
             t_att = time.perf_counter()
