@@ -222,8 +222,6 @@ void build_query_tile(const iris_template_t *q, uint32_t *tile) {
 
 #include <errno.h>
 #include <immintrin.h>
-#include <sched.h>
-#include <stdio.h>
 #include <unistd.h>
 
 namespace iris {
@@ -390,34 +388,15 @@ class CopyPool {
 
 constexpr size_t kParallelCopyMin = 256 << 10;
 
-// CPUs this process may use: its affinity mask, or the cgroup's CPU quota if that grants less
-// (the GPU boxes: 256 CPUs in the mask, a quota of 16).
-int usable_cpus() {
-    cpu_set_t set;
-    int n = sched_getaffinity(0, sizeof(set), &set) == 0 ? CPU_COUNT(&set) : 1;
-    if (FILE *f = fopen("/sys/fs/cgroup/cpu.max", "re")) {
-        char q[32] = {0};
-        long long per = 0;
-        if (fscanf(f, "%31s %lld", q, &per) == 2 && strcmp(q, "max") != 0 && per > 0) {
-            const long long quota = atoll(q);
-            n = std::min<int>(n, (int)std::max<long long>(1, (quota + per - 1) / per));
-        }
-        fclose(f);
-    }
-    return std::max(1, n);
-}
+// Helper threads per device pool (3: with the caller, 4 parts).  7 were measured on the boxes'
+// 16-CPU quota for a 3M-mask walk's copy-out and gave no reliable gain: 1.24 / 1.09 / 0.95e9
+// records/s against 1.12 / 1.17 / 1.11e9 with 3, alternating on one box and across boxes
+// (profiles/r06k_helpers_ab.txt).  IRIS_COPY_HELPERS (0..15) overrides; read when the pool is created.
+constexpr int kCopyHelpers = 3;
 
-// Helper threads per device pool: half the usable CPUs less the caller, 1..7 -- 7 on the boxes'
-// 16-CPU quota, where a 3M-mask walk's copy-out (the packed rows expanded into the caller's
-// array) ran 1.24e9 records/s against 1.12e9 with 3 (profiles/r06h7_bench_host-masks_mmap.jsonl,
-// r06e); 3 on this container's 8 CPUs.  The reference runs these loops on rayon's all-core pool.
-// IRIS_COPY_HELPERS (0..15) overrides; read when the pool is created.
 int copy_helpers() {
     const char *e = getenv("IRIS_COPY_HELPERS");
-    if (!e || !*e) {
-        static const int dflt = std::max(1, std::min(7, usable_cpus() / 2 - 1));
-        return dflt;
-    }
+    if (!e || !*e) return kCopyHelpers;
     const int v = atoi(e);
     return v < 0 ? 0 : v > 15 ? 15 : v;
 }

@@ -20,23 +20,10 @@ def clean_env(monkeypatch):
         monkeypatch.delenv(k, raising=False)
 
 
-def default_helpers():
-    """Half the usable CPUs (affinity mask, capped by the cgroup quota) less the caller, 1..7."""
-    import os
-    n = len(os.sched_getaffinity(0))
-    try:
-        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
-        if q != "max":
-            n = min(n, max(1, -(-int(q) // int(per))))
-    except OSError:
-        pass
-    return max(1, min(7, n // 2 - 1))
-
-
 def test_defaults():
     c = ih.config()
     assert c == {"readahead": "1", "auto_resident": "1", "group_timeout_ms": "auto", "group_init_timeout_ms": "120000",
-                 "resident_max_mb": "auto", "copy_helpers": str(default_helpers()), "test_hooks": "0"}
+                 "resident_max_mb": "auto", "copy_helpers": "3", "test_hooks": "0"}
 
 
 def test_resident_cap_is_a_production_knob(monkeypatch):
