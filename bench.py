@@ -370,6 +370,31 @@ def cpu_baseline(args, reserve=0):
             "host": info, **extra}
 
 
+def cxx_walk(shares, n, path, walks=6):
+    """tools/walk_host (C++ against the C ABI, as the reference's Rust participant / resolver would
+    call it) walking the bench's own mapped file in 20 000-record calls, one engine per walk, in a
+    child process with its own device context (its first walk makes the file resident there):
+    the records/s of the walks after the first, without the Python binding's ~3.5 us per call."""
+    exe = ROOT / "tools" / "walk_host"
+    try:
+        if not exe.exists():
+            subprocess.run(["g++", "-O2", "-std=c++17", "-I", str(ROOT / "include"), str(ROOT / "tools" / "walk_host.cpp"),
+                            "-L", str(ROOT / "mpc-iris-code_amd"), "-liris_hip",
+                            f"-Wl,-rpath,{ROOT / 'mpc-iris-code_amd'}", "-Wl,-rpath-link,/opt/rocm/lib", "-o", str(exe)],
+                           check=True, capture_output=True, timeout=120)
+        r = subprocess.run([str(exe), "shares" if shares else "masks", str(n), str(walks), str(path)],
+                           capture_output=True, text=True, timeout=300)
+        rates = [float(l.split(",")[1].split()[0]) for l in r.stdout.splitlines() if l.startswith("walk ")][1:]
+        calls = [l for l in r.stdout.splitlines() if l.startswith("calls after walk 0")]
+        if r.returncode != 0 or not rates:
+            return {"error": (r.stderr or r.stdout)[-300:]}
+        rates.sort()
+        return {"records_per_s_median": rates[len(rates) // 2], "records_per_s_walks": rates,
+                "calls": calls[0] if calls else None, "source": "tools/walk_host.cpp"}
+    except Exception as ex:  # reported, never fatal
+        return {"error": str(ex)[-300:]}
+
+
 def load_traffic(workload, n_per_launch, layout):
     """HBM bytes per launch of the workload's kernel from the committed PMC run
     (profiles/*_pmc_<workload>[_lanes].json, FETCH_SIZE/WRITE_SIZE in separate passes,
@@ -880,6 +905,8 @@ def run_aux(args, dev):
                 if args.workload == "host-shares" else check_masks_rows(qt[200:], host[sample]))
         ok = bool((hout[sample] == want).all())
         check = {"sampled_outputs_checked": len(sample), "ok": ok}
+        if file_walk:  # the same walk of the same file from C++, no Python between the calls
+            extra["cxx_walk"] = cxx_walk(shares_wl, n, mpath)
         if mpath is not None:
             del host
             mpath.unlink()

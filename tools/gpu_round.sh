@@ -29,6 +29,7 @@ bench_args() {
     host-shares_attached) echo "--workload host-shares --attached --steps 3 --warmup 1" ;;
     host-masks_mmap) echo "--workload host-masks --mmap --steps 10 --warmup 2" ;;
     host-shares_mmap) echo "--workload host-shares --mmap --steps 10 --warmup 2" ;;
+    host-shares_mmap2m) echo "--workload host-shares --mmap --n-per-gpu 2000000 --steps 10 --warmup 2" ;;
     host-masks_mmap_off) echo "--workload host-masks --mmap --steps 3 --warmup 1 --no-auto-resident" ;;
     *) return 1 ;;
     esac

@@ -2,7 +2,7 @@
 // on-device generator, mapped PROT_READ / MAP_SHARED (memmap2's Mmap::map, src/main.rs:389,458),
 // walked in 20 000-record iris_engine_batch_process_host calls with a fresh engine per walk
 // (src/main.rs:426-431, 511-516).  Prints per-walk records/s and per-call percentiles.
-//   walk_host masks|shares RECORDS WALKS
+//   walk_host masks|shares RECORDS WALKS [FILE]   (FILE: walk an existing record file instead)
 // build: g++ -O2 -std=c++17 -I include tools/walk_host.cpp -L mpc-iris-code_amd -liris_hip
 //        -Wl,-rpath,$PWD/mpc-iris-code_amd -Wl,-rpath-link,/opt/rocm/lib -o tools/walk_host
 #include <fcntl.h>
@@ -41,8 +41,9 @@ int main(int argc, char **argv) {
     iris_device_t *dev = nullptr;
     CK(iris_device_open(0, &dev));
     const char *tmp = getenv("TMPDIR") ? getenv("TMPDIR") : "/tmp";
-    const std::string path = std::string(tmp) + "/walk_host_" + std::to_string(getpid()) + ".rec";
-    {
+    const bool given = argc > 4;
+    const std::string path = given ? std::string(argv[4]) : std::string(tmp) + "/walk_host_" + std::to_string(getpid()) + ".rec";
+    if (!given) {
         const uint64_t per = (1ull << 30) / rb;
         iris_db_t *g = nullptr;
         CK(iris_db_create(dev, kind, std::min(n, per), &g));
@@ -90,7 +91,7 @@ int main(int argc, char **argv) {
     std::printf("config: %s\n", cfg);
     munmap((void *)map, n * rb);
     ::close(fd);
-    ::unlink(path.c_str());
+    if (!given) ::unlink(path.c_str());
     iris_device_close(dev);
     return 0;
 }
