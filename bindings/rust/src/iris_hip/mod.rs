@@ -18,7 +18,7 @@ use std::{
     ffi::{CStr, CString},
     fmt,
     marker::PhantomData,
-    os::raw::c_int,
+    os::raw::{c_int, c_void},
     path::Path,
     ptr,
     sync::{Arc, OnceLock},
@@ -104,6 +104,18 @@ impl Device {
         let (mut free, mut total) = (0usize, 0usize);
         check(unsafe { ffi::iris_device_memory(self.raw(), &mut free, &mut total) })?;
         Ok((free, total))
+    }
+
+    /// Frees the device's copy of the record file whose mapping holds `records` (the participant's
+    /// or resolver's mmap'd slice): for a process that rewrites its file through a writable mapping,
+    /// which the per-call staleness check does not see (iris_device_drop_resident_range).
+    pub fn drop_resident_range<T>(&self, records: &[T]) -> Result<()> {
+        check(unsafe { ffi::iris_device_drop_resident_range(self.raw(), records.as_ptr() as *const c_void) })
+    }
+
+    /// Frees every resident file copy of the device (iris_device_drop_resident).
+    pub fn drop_resident(&self) -> Result<()> {
+        check(unsafe { ffi::iris_device_drop_resident(self.raw()) })
     }
 }
 

@@ -72,6 +72,10 @@ public:
     Device &operator=(const Device &) = delete;
     iris_device_t *handle() const { return h_; }
     void synchronize() const { check(iris_device_synchronize(h_)); }
+    // Frees the resident copy of the file mapping holding `p` (after rewriting the file through a
+    // writable mapping, which the per-call check does not see); drop_resident() frees them all.
+    void drop_resident_range(const void *p) const { check(iris_device_drop_resident_range(h_, p)); }
+    void drop_resident() const { check(iris_device_drop_resident(h_)); }
     // The process-wide device the value types' per-pair GPU calls use (ordinal 0).
     static Device &default_device() {
         static Device d(0);
