@@ -387,7 +387,7 @@ def cxx_walk(shares, n, path, walks=6):
         rates = [float(l.split(",")[1].split()[0]) for l in r.stdout.splitlines() if l.startswith("walk ")][1:]
         calls = [l for l in r.stdout.splitlines() if l.startswith("calls after walk 0")]
         if r.returncode != 0 or not rates:
-            return {"error": (r.stderr or r.stdout)[-300:]}
+            return {"error": f"rc={r.returncode} " + (r.stderr + r.stdout)[-300:]}
         rates.sort()
         return {"records_per_s_median": rates[len(rates) // 2], "records_per_s_walks": rates,
                 "calls": calls[0] if calls else None, "source": "tools/walk_host.cpp"}

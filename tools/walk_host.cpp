@@ -32,6 +32,7 @@ static double now_us() {
 }
 
 int main(int argc, char **argv) {
+    setvbuf(stdout, nullptr, _IOLBF, 0);  // line-buffered: a run that dies still shows its walks
     const bool shares = argc > 1 && std::string(argv[1]) == "shares";
     const uint64_t n = argc > 2 ? strtoull(argv[2], nullptr, 10) : (shares ? 1000000 : 3000000);
     const int walks = argc > 3 ? atoi(argv[3]) : 8;
