@@ -375,15 +375,15 @@ def cxx_walk(shares, n, path, walks=6):
     call it) walking the bench's own mapped file in 20 000-record calls, one engine per walk, in a
     child process with its own device context (its first walk makes the file resident there):
     the records/s of the walks after the first, without the Python binding's ~3.5 us per call."""
-    exe = ROOT / "tools" / "walk_host"
+    exe = pathlib.Path(tempfile.gettempdir()) / f"walk_host_{os.getpid()}"  # built from this tree's source
     try:
-        if not exe.exists():
-            subprocess.run(["g++", "-O2", "-std=c++17", "-I", str(ROOT / "include"), str(ROOT / "tools" / "walk_host.cpp"),
-                            "-L", str(ROOT / "mpc-iris-code_amd"), "-liris_hip",
-                            f"-Wl,-rpath,{ROOT / 'mpc-iris-code_amd'}", "-Wl,-rpath-link,/opt/rocm/lib", "-o", str(exe)],
-                           check=True, capture_output=True, timeout=120)
+        subprocess.run(["g++", "-O2", "-std=c++17", "-I", str(ROOT / "include"), str(ROOT / "tools" / "walk_host.cpp"),
+                        "-L", str(ROOT / "mpc-iris-code_amd"), "-liris_hip",
+                        f"-Wl,-rpath,{ROOT / 'mpc-iris-code_amd'}", "-Wl,-rpath-link,/opt/rocm/lib", "-o", str(exe)],
+                       check=True, capture_output=True, timeout=120)
         r = subprocess.run([str(exe), "shares" if shares else "masks", str(n), str(walks), str(path)],
                            capture_output=True, text=True, timeout=300)
+        exe.unlink(missing_ok=True)
         rates = [float(l.split(",")[1].split()[0]) for l in r.stdout.splitlines() if l.startswith("walk ")][1:]
         calls = [l for l in r.stdout.splitlines() if l.startswith("calls after walk 0")]
         if r.returncode != 0 or not rates:
