@@ -240,6 +240,16 @@ int run_u16_engine(iris_engine *e, const iris_db *db, uint64_t first, uint64_t n
 
 // calls of at most this many records (62 MB of rows per buffer) go through the read-ahead
 constexpr uint64_t kReadaheadMax = 1ull << 20;
+// A MasksEngine window's rows cross the host link packed (store_tile_packed, iris_device.hpp): 32 B
+// per record, then an escape row of 31 u16 per record that only rows spanning more than a byte
+// use; the copy-out expands them into the caller's [u16; 31] (parallel_expand).  The resolver's
+// 20 000-mask walk is bound by its rows crossing the host link (~44 GB/s: 23 us of a 28-us call
+// with the rows unpacked).
+constexpr size_t kPackedRecBytes = 32;
+bool ra_packed(const iris_engine *e) { return e->kind == IRIS_KIND_MASKS && e->dev->hooks.ra_packed; }
+// bytes of a read-ahead buffer per record
+size_t ra_rec_bytes(const iris_engine *e) { return ra_packed(e) ? kPackedRecBytes + kRot * 2 : kRot * 2; }
+
 // A walk's read-ahead windows grow geometrically: the walk's first window is one chunk, each later
 // one twice the chunks of the window before it, up to kWindowRecords records (and kWindowRowsMax of
 // rows per buffer).  Consecutive windows run on two side streams, so a window's kernel starts on
@@ -248,15 +258,6 @@ constexpr uint64_t kReadaheadMax = 1ull << 20;
 // call for big windows, and a call waits for its whole window, so windows beyond ~160k records
 // only delay the host (a 3M-mask walk: 1.03e9 records/s from C++ with windows up to 880k,
 // profiles/r06c_walk_host_masks.txt; measured per cap in profiles/r06d_window_caps.txt).
-// A MasksEngine window's rows cross the host link packed (store_tile_packed, iris_device.hpp): 32 B
-// per record, then an escape row of 31 u16 per record that only rows spanning more than a byte
-// use; the copy-out expands them into the caller's [u16; 31] (parallel_expand).  The resolver's
-// 20 000-mask walk is bound by its rows crossing the host link (~44 GB/s, 23 us of a 28-us call).
-constexpr size_t kPackedRecBytes = 32;
-bool ra_packed(const iris_engine *e) { return e->kind == IRIS_KIND_MASKS && e->dev->hooks.ra_packed; }
-// bytes of a read-ahead buffer per record
-size_t ra_rec_bytes(const iris_engine *e) { return ra_packed(e) ? kPackedRecBytes + kRot * 2 : kRot * 2; }
-
 constexpr uint64_t kWindowRecords = 160000;
 constexpr size_t kWindowRowsMax = 64ull << 20;
 
@@ -282,7 +283,7 @@ bool readahead_ok(const iris_db *db, uint64_t n) {
     return db->dev->hooks.readahead && n <= kReadaheadMax && db->k.layout == IRIS_LAYOUT_TILES;
 }
 
-// Waits for the engine's read-ahead kernels (side stream): the row buffers may be reused or freed
+// Waits for the engine's read-ahead kernels (side streams): the row buffers may be reused or freed
 // when this returns.  The windows' rows stay valid (a change of the database changes its version).
 int ra_wait(iris_engine *e) {
     Readahead &ra = e->ra;
