@@ -30,6 +30,27 @@ HERE = pathlib.Path(__file__).resolve().parent
 # IRIS_HIP_LIB points at an alternative in-tree build (kernel experiments under tools/)
 LIB_PATH = pathlib.Path(os.environ.get("IRIS_HIP_LIB", HERE / "libiris_hip.so"))
 
+
+def _load_pycall():
+    """The per-call fast path (csrc/iris_pycall.c, built beside the library and linked to it): the
+    host-slice engine call without ctypes' per-call marshalling; None where it is not built or a
+    non-default library is in use (IRIS_HIP_LIB)."""
+    p = HERE / "_iris_pycall.so"
+    if "IRIS_HIP_LIB" in os.environ or not p.exists():
+        return None
+    import importlib.util
+    try:
+        spec = importlib.util.spec_from_file_location("_iris_pycall", p)
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+    except (ImportError, OSError):
+        return None
+    return mod
+
+
+_pycall = _load_pycall()
+_NULL = ctypes.c_void_p()
+
 COLS, ROWS, BITS, LIMBS, ROTATIONS = 200, 64, 12800, 200, 31
 KIND_MASKS, KIND_SHARES, KIND_TEMPLATES = 1, 2, 3
 LAYOUT_DEFAULT, LAYOUT_LANES, LAYOUT_TILES = 0, 1, 2
@@ -768,8 +789,12 @@ class _Engine:
         if (isinstance(db, np.ndarray) and db.dtype == dt and db.ndim == 2 and db.shape[1] == width
                 and db.flags.c_contiguous and out.shape[0] == db.shape[0]):
             # the chunk walk's call (a contiguous slice of the caller's record array): passed as is,
-            # with none of the conversions below (~11 -> ~4 us of Python per call)
-            rc = lib.iris_engine_batch_process_host(self.handle, db.ctypes.data, db.shape[0], out.ctypes.data)
+            # with none of the conversions below, through the buffer protocol where the fast path
+            # is built (csrc/iris_pycall.c), else ctypes
+            if _pycall is not None:
+                rc = _pycall.batch_process_host((self.handle or _NULL).value or 0, db, out, db.itemsize * width)
+            else:
+                rc = lib.iris_engine_batch_process_host(self.handle, db.ctypes.data, db.shape[0], out.ctypes.data)
             if rc:
                 _check(rc)
             return out
