@@ -865,6 +865,15 @@ def run_aux(args, dev):
         # kernels overlap on two side streams, so summed kernel times are not a duration)
         achieved = rec_bytes * n * args.steps / elapsed / 1e9
         extra["roofline_is"] = "end to end: the walked records' bytes / the timed walks' wall time"
+        if args.mmap or args.attached:
+            # the rows crossing the host link (kernel stores into pinned memory): packed masks rows
+            # 32 B per record, shares rows 62 B; against the measured device -> pinned-host rate of
+            # kernel stores at window sizes (53.1 GB/s for 5 MB, profiles/r06h_ubench_d2h.txt)
+            row_bytes = 62 if shares_wl else 32
+            link = row_bytes * n * args.steps / elapsed / 1e9
+            extra["host_link"] = {"row_bytes_per_record": row_bytes, "achieved_GBps": link,
+                                  "measured_GBps": 53.1, "frac": link / 53.1,
+                                  "source": "tools/ubench_d2h.hip (profiles/r06h_ubench_d2h.txt)"}
     if args.workload == "resolve-masks":  # denominators from the (separately checked) masks engine
         denoms = np.empty((n, ROT), np.uint16)
         eng.batch_process(denoms, mdb)
