@@ -34,7 +34,14 @@ LIB_PATH = pathlib.Path(os.environ.get("IRIS_HIP_LIB", HERE / "libiris_hip.so"))
 def _load_pycall():
     """The per-call fast path (csrc/iris_pycall.c, built beside the library and linked to it): the
     host-slice engine call without ctypes' per-call marshalling; None where it is not built or a
-    non-default library is in use (IRIS_HIP_LIB)."""
+    non-default library is in use (IRIS_HIP_LIB).  Loaded on the first such call, after
+    load_library(), so that importing this module loads no HIP runtime: a process that imports
+    torch later (bench.py's ranks) keeps the load order it had without the fast path (torch bundles
+    its own libamdhip64.so.7; whichever is mapped first serves both)."""
+    global _pycall
+    if _pycall is not _UNLOADED:
+        return _pycall
+    _pycall = None
     p = HERE / "_iris_pycall.so"
     if "IRIS_HIP_LIB" in os.environ or not p.exists():
         return None
@@ -45,10 +52,12 @@ def _load_pycall():
         spec.loader.exec_module(mod)
     except (ImportError, OSError):
         return None
+    _pycall = mod
     return mod
 
 
-_pycall = _load_pycall()
+_UNLOADED = object()
+_pycall = _UNLOADED
 _NULL = ctypes.c_void_p()
 
 COLS, ROWS, BITS, LIMBS, ROTATIONS = 200, 64, 12800, 200, 31
@@ -791,8 +800,9 @@ class _Engine:
             # the chunk walk's call (a contiguous slice of the caller's record array): passed as is,
             # with none of the conversions below, through the buffer protocol where the fast path
             # is built (csrc/iris_pycall.c), else ctypes
-            if _pycall is not None:
-                rc = _pycall.batch_process_host((self.handle or _NULL).value or 0, db, out, db.itemsize * width)
+            pc = _pycall if _pycall is not _UNLOADED else _load_pycall()
+            if pc is not None:
+                rc = pc.batch_process_host((self.handle or _NULL).value or 0, db, out, db.itemsize * width)
             else:
                 rc = lib.iris_engine_batch_process_host(self.handle, db.ctypes.data, db.shape[0], out.ctypes.data)
             if rc:

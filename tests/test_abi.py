@@ -108,13 +108,15 @@ def test_python_fast_path_extension():
     used: it passes the caller's buffers to iris_engine_batch_process_host unchanged, so its
     errors are the library's (a NULL engine: IRIS_E_ARG), and a length mismatch between the
     records and the rows is refused before the call."""
-    assert ih._pycall is not None, "mpc-iris-code_amd/_iris_pycall.so not built"
+    ih.load_library()
+    pc = ih._load_pycall()
+    assert pc is not None and ih._pycall is pc, "mpc-iris-code_amd/_iris_pycall.so not built"
     recs, out = np.zeros((2, 200), np.uint64), np.zeros((2, 31), np.uint16)
-    assert ih._pycall.batch_process_host(0, recs, out, 1600) == ih.load_library().iris_engine_batch_process_host(
+    assert pc.batch_process_host(0, recs, out, 1600) == ih.load_library().iris_engine_batch_process_host(
         None, recs.ctypes.data, 2, out.ctypes.data) == -1
     assert "engine is NULL" in ih.load_library().iris_last_error().decode()
-    assert ih._pycall.batch_process_host(0, recs, np.zeros((3, 31), np.uint16), 1600) == -1  # 2 records, 3 rows
+    assert pc.batch_process_host(0, recs, np.zeros((3, 31), np.uint16), 1600) == -1  # 2 records, 3 rows
     with pytest.raises(ValueError):  # rows must be writable
         ro = np.zeros((2, 31), np.uint16)
         ro.setflags(write=False)
-        ih._pycall.batch_process_host(0, recs, ro, 1600)
+        pc.batch_process_host(0, recs, ro, 1600)

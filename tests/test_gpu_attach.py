@@ -359,7 +359,9 @@ def test_device_output_rows_visible_to_unordered_reader(device, kind):
     rather than catching the unfixed timing window."""
     import ctypes
 
-    hip = ctypes.CDLL("libamdhip64.so")
+    # the runtime the library runs on: the loaded object of its NEEDED soname (a process that also
+    # imports torch maps torch's bundled libamdhip64.so too; "libamdhip64.so" may name that one)
+    hip = ctypes.CDLL("libamdhip64.so.7")
     hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
     if kind == ih.KIND_MASKS:
         n, chunk = 60_000, 20_000
