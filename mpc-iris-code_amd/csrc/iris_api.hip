@@ -332,11 +332,13 @@ constexpr uint64_t kPinnedRowsChunk = 1ull << 20;
 // The host-output form for TILES databases: each chunk's kernel stores its rows straight into one
 // of two pinned host buffers (16-B runs over the host link, as the read-ahead does), and the helper
 // threads copy them to `out` while the next chunk's kernel runs.  The copy engines' D2H into a
-// caller's pageable array ran at 3-8 GB/s on some boxes (profiles/r03_host_rows.txt).
+// caller's pageable array ran at 3-8 GB/s on some boxes (profiles/r03_host_rows.txt).  MasksEngine
+// rows cross the link packed, as the read-ahead's do (ra_packed), and are expanded on the way out.
 int run_u16_engine_pinned(iris_engine *e, const iris_db *db, uint64_t first, uint64_t n, uint16_t *out) {
     iris_device *d = e->dev;
     const uint64_t ch = std::min<uint64_t>(n, kPinnedRowsChunk);
-    const size_t want = std::max<size_t>((size_t)ch * kRot * 2, 4096);
+    const bool pk = ra_packed(e);
+    const size_t want = std::max<size_t>((size_t)ch * ra_rec_bytes(e), 4096);
     void *rows[2] = {nullptr, nullptr};
     size_t got[2] = {0, 0};
     hipEvent_t ev[2] = {nullptr, nullptr};
@@ -350,7 +352,7 @@ int run_u16_engine_pinned(iris_engine *e, const iris_db *db, uint64_t first, uin
     // copied out, and rows[c & 1] was last read by the (synchronous) copy of chunk c - 2
     auto launch = [&](uint64_t c) -> int {
         const uint64_t a = c * ch, m = std::min<uint64_t>(ch, n - a);
-        CHK(enqueue_u16_engine(e, db, first + a, m, (uint16_t *)rows[c & 1]));
+        CHK(enqueue_u16_engine(e, db, first + a, m, (uint16_t *)rows[c & 1], nullptr, nullptr, pk));
         HIPCHK(hipEventRecord(ev[c & 1], d->stream));
         return 0;
     };
@@ -361,7 +363,12 @@ int run_u16_engine_pinned(iris_engine *e, const iris_db *db, uint64_t first, uin
         if (rc == 0 && hipEventSynchronize(ev[c & 1]) != hipSuccess) rc = fail(IRIS_E_HIP, "hipEventSynchronize");
         if (rc == 0) {
             const uint64_t a = c * ch, m = std::min<uint64_t>(ch, n - a);
-            parallel_copy(out + a * kRot, rows[c & 1], (size_t)m * kRot * 2, d->ordinal);
+            if (pk) {
+                const uint8_t *p = (const uint8_t *)rows[c & 1];
+                parallel_expand(out + a * kRot, p, (const uint16_t *)(p + m * kPackedRecBytes), m, d->ordinal);
+            } else {
+                parallel_copy(out + a * kRot, rows[c & 1], (size_t)m * kRot * 2, d->ordinal);
+            }
         }
     }
     // on failure a kernel may still be storing into the buffers: drain before they go back
