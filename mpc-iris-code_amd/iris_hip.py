@@ -39,21 +39,22 @@ def _load_pycall():
     torch later (bench.py's ranks) keeps the load order it had without the fast path (torch bundles
     its own libamdhip64.so.7; whichever is mapped first serves both)."""
     global _pycall
-    if _pycall is not _UNLOADED:
-        return _pycall
-    _pycall = None
-    p = HERE / "_iris_pycall.so"
-    if "IRIS_HIP_LIB" in os.environ or not p.exists():
-        return None
-    import importlib.util
-    try:
-        spec = importlib.util.spec_from_file_location("_iris_pycall", p)
-        mod = importlib.util.module_from_spec(spec)
-        spec.loader.exec_module(mod)
-    except (ImportError, OSError):
-        return None
-    _pycall = mod
-    return mod
+    with _lock:
+        if _pycall is not _UNLOADED:
+            return _pycall
+        _pycall = None
+        p = HERE / "_iris_pycall.so"
+        if "IRIS_HIP_LIB" in os.environ or not p.exists():
+            return None
+        import importlib.util
+        try:
+            spec = importlib.util.spec_from_file_location("_iris_pycall", p)
+            mod = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(mod)
+        except (ImportError, OSError):
+            return None
+        _pycall = mod
+        return mod
 
 
 _UNLOADED = object()
