@@ -504,3 +504,55 @@ def test_same_file_remapped_at_another_offset(device, tmp_path):
         b = np.memmap(path, dtype=np.uint64, mode="r", offset=skip * 1600, shape=(n - skip, 200))
         assert (walk(eng, b) == want[skip:]).all()
         del b
+
+
+def test_resident_cap_production_knob(monkeypatch, tmp_path):
+    """IRIS_RESIDENT_MAX_MB (production knob, no test opt-in): the copies together hold at most
+    that much; a file above it is refused (it uploads per call, iris_config says why), one below
+    it is kept.  Rows equal the oracle either way."""
+    kind, small, big = ih.KIND_MASKS, 60_000, 150_000  # 96 MB and 240 MB
+    files = []
+    for i, cnt in enumerate((small, big)):
+        p = tmp_path / f"cap{i}.masks"
+        h = gen(kind, SEED + 80 + i, cnt)
+        h.tofile(p)
+        files.append((h, mapped(p, kind, cnt)))
+    with monkeypatch.context() as m:
+        m.setenv("IRIS_RESIDENT_MAX_MB", "200")
+        dev = ih.Device(0)
+    try:
+        assert dev.config()["resident_max_mb"] == "200" and "ignored" not in dev.config()
+        eng, want_fn = engine_and_oracle(dev, kind, SEED + 82)
+        with eng:
+            assert (walk(eng, files[0][1]) == want_fn(files[0][0])).all()
+            assert dev.resident()[0] == 1
+            assert (walk(eng, files[1][1]) == want_fn(files[1][0])).all()
+            assert "cap" in dev.config()["resident_skip"], dev.config()
+            assert dev.resident()[0] == 1 and dev.resident()[1] < 200 << 20
+    finally:
+        dev.drop_resident()
+        dev.close()
+    del files
+
+
+def test_kernel_stats_largest(device):
+    """iris_device_kernel_stats_largest: the largest launch of a kernel family since the last reset
+    (a walk's biggest read-ahead window) and its duration."""
+    n = 50_000
+    q = oc.gen_masks(SEED + 90, 0, 1)[0]
+    with ih.Database(device, ih.KIND_MASKS, n) as db, ih.MasksEngine(device, q) as eng:
+        db.generate(n, SEED + 91)
+        out = device.alloc(n * 31 * 2)
+        try:
+            device.reset_stats()
+            device.set_profiling(True)
+            for m in (1_000, n, 7_000):
+                eng.batch_process_device(db, out, 0, m)
+            device.synchronize()
+            items, ms = device.kernel_stats_largest("masks")
+            assert items == n and ms > 0
+            device.reset_stats()
+            assert device.kernel_stats_largest("masks") == (0, 0.0)
+        finally:
+            device.set_profiling(False)
+            device.free(out)
