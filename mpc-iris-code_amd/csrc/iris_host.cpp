@@ -294,49 +294,69 @@ const bool kHaveAvx512 = __builtin_cpu_supports("avx512bw") && __builtin_cpu_sup
 // Helper threads (one pool per device) for copying an engine call's rows out of pinned memory
 // into the caller's buffer (read-ahead, iris_api.hip) and a large write's records into the pinned
 // upload slots: one core reads ~25 GB/s from DRAM, so a 1.24-MB participant-sized chunk costs
-// ~45 us on one thread.  The helpers spin for a while after each
-// job (calls of a chunk walk arrive every few tens of us) and then block.
+// ~45 us on one thread.  A job is split into twice as many parts as there are threads, and parts
+// are claimed from one atomic word (the job's number in the high half, the next part in the low
+// half): the caller works through them too, so a helper that is still asleep when a job starts (the
+// first call of a walk after a pause) costs a share of the work, not its wake-up latency.  The
+// helpers spin for a while after each job (calls of a chunk walk arrive every few tens of us) and
+// then block.
 class CopyPool {
    public:
-    explicit CopyPool(int helpers) : pid_(getpid()) {
-        for (int i = 0; i < helpers; ++i) threads_.emplace_back([this, i] { worker(i + 1); });
+    explicit CopyPool(int helpers) : pid_(getpid()), nthreads_(helpers + 1) {
+        for (int i = 0; i < helpers; ++i) threads_.emplace_back([this] { worker(); });
         for (auto &t : threads_) t.detach();  // never joined: the pool lives as long as the process
     }
     pid_t pid() const { return pid_; }
-    int parts() const { return (int)threads_.size() + 1; }
 
     // src != nullptr: memcpy; else pread from fd at file offset off.  Returns false if a read failed
     // (an I/O error, or the file ended before `bytes`).  esc != nullptr: expand `bytes` packed
     // MasksEngine records at src (escape rows at esc) into dst instead.
     bool run(char *dst, const char *src, size_t bytes, int fd = -1, off_t off = 0, const uint16_t *esc = nullptr) {
-        std::lock_guard<std::mutex> one(run_mu_);  // one copy at a time (devices may call concurrently)
+        std::lock_guard<std::mutex> one(run_mu_);  // one job at a time (devices may call concurrently)
         dst_ = dst;
         src_ = src;
         esc_ = esc;
         bytes_ = bytes;
         fd_ = fd;
         off_ = off;
+        nparts_ = 2 * nthreads_;
         ok_.store(true, std::memory_order_relaxed);
-        remaining_.store(parts() - 1, std::memory_order_relaxed);
+        done_.store(0, std::memory_order_relaxed);
+        const uint64_t job = ++job_;
+        claim_.store(job << 32, std::memory_order_release);  // publishes the fields above
         {
             std::lock_guard<std::mutex> l(mu_);
-            gen_.fetch_add(1, std::memory_order_release);
+            gen_.store(job, std::memory_order_release);
         }
         cv_.notify_all();
-        part(0);
-        while (remaining_.load(std::memory_order_acquire) != 0) __builtin_ia32_pause();
+        work(job);
+        while (done_.load(std::memory_order_acquire) != nparts_) __builtin_ia32_pause();
         return ok_.load(std::memory_order_acquire);
     }
 
    private:
+    // claims and runs parts of job `job` until none is left (or a newer job has replaced it)
+    void work(uint64_t job) {
+        for (;;) {
+            uint64_t v = claim_.load(std::memory_order_acquire);
+            int k;
+            do {
+                if ((v >> 32) != (job & 0xFFFFFFFFu) || (int)(v & 0xFFFFFFFFu) >= nparts_) return;
+                k = (int)(v & 0xFFFFFFFFu);
+            } while (!claim_.compare_exchange_weak(v, v + 1, std::memory_order_acq_rel, std::memory_order_acquire));
+            part(k);
+            done_.fetch_add(1, std::memory_order_release);
+        }
+    }
     void part(int id) {
+        const int np = nparts_;
         if (esc_) {  // bytes_ records, split on record boundaries
-            const size_t per = (bytes_ + parts() - 1) / parts();
+            const size_t per = (bytes_ + np - 1) / np;
             const size_t a = std::min(bytes_, (size_t)id * per), b = std::min(bytes_, a + per);
             if (a < b) expand_packed_rows((uint16_t *)dst_ + kRot * a, (const uint8_t *)src_ + 32 * a, esc_ + kRot * a, b - a);
             return;
         }
-        const size_t per = ((bytes_ + parts() - 1) / parts() + 63) & ~(size_t)63;
+        const size_t per = ((bytes_ + np - 1) / np + 63) & ~(size_t)63;
         const size_t a = std::min(bytes_, (size_t)id * per), b = std::min(bytes_, a + per);
         if (a >= b) return;
         if (src_) {
@@ -353,7 +373,7 @@ class CopyPool {
             done += (size_t)r;
         }
     }
-    void worker(int id) {
+    void worker() {
         uint64_t seen = 0;
         for (;;) {
             uint64_t g;
@@ -367,16 +387,19 @@ class CopyPool {
                 }
             }
             seen = g;
-            part(id);
-            remaining_.fetch_sub(1, std::memory_order_release);
+            work(g);
         }
     }
     pid_t pid_;
+    const int nthreads_;  // helpers + the caller
     std::vector<std::thread> threads_;
     std::mutex run_mu_, mu_;
     std::condition_variable cv_;
-    std::atomic<uint64_t> gen_{0};
-    std::atomic<int> remaining_{0};
+    std::atomic<uint64_t> gen_{0};    // the newest job's number (wakes the helpers)
+    std::atomic<uint64_t> claim_{0};  // (job number << 32) | next unclaimed part
+    std::atomic<int> done_{0};        // parts of the current job finished
+    uint64_t job_ = 0;
+    int nparts_ = 1;
     char *dst_ = nullptr;
     const char *src_ = nullptr;
     const uint16_t *esc_ = nullptr;
