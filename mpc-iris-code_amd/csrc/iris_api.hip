@@ -451,7 +451,7 @@ int ra_launch(iris_engine *e, const iris_db *a, uint64_t first, uint64_t n, int 
 // from a read-ahead window that holds them (same version of the same database), else they are
 // computed now -- a whole window of consecutive chunks when the call continues a walk.  While a
 // window's rows are copied out, the window after it is already computed into the other buffer
-// (one launch of up to kWindowMax chunks, so a chunk pays a fraction of a launch's ramp), and a
+// (one launch of a growing number of chunks, window_records, on the other side stream), and a
 // random-access caller never pays for rows it does not ask for.  The copy is the CPU's, split
 // over helper threads: the copy engines' D2H of these 1.24 MB took 31 us on one box and
 // 150-275 us (8 GB/s) on others, and queued behind the side stream's event it fell into the slow
