@@ -482,6 +482,8 @@ class Ranks:
         self.backend = None
         self.ordinal = 0
         self.group_form_s = None
+        self.rccl_error = None  # why the RCCL group did not form (the run fell back to gloo)
+        self.stray_group = None
         if args.single_process:
             if "WORLD_SIZE" in os.environ and self.world > 1:
                 raise SystemExit("error: --single-process drives every GPU from one process; do not launch ranks")
@@ -530,7 +532,24 @@ class Ranks:
         elif self.dist is not None and self.rccl:
             box = [ih.Group.unique_id() if self.rank == 0 else None]
             self.dist.broadcast_object_list(box, src=0)
-            self.group = ih.Group.rank(self.ordinal, self.world, self.rank, box[0])
+            err = None
+            try:
+                self.group = ih.Group.rank(self.ordinal, self.world, self.rank, box[0])
+            except Exception as ex:  # bounded: a formation that cannot finish fails, never hangs
+                err = f"rank {self.rank}: {ex}"
+            # every rank learns whether every rank formed the group, so all take the same path
+            errs = [None] * self.world
+            self.dist.all_gather_object(errs, err)
+            failed = [e for e in errs if e]
+            if failed:
+                if os.environ.get("IRIS_RCCL_FALLBACK", "1") == "0":
+                    raise SystemExit(f"error: the RCCL group did not form: {'; '.join(failed)}")
+                # the search still runs, its winners exchanged over gloo (the rehearsal path), and
+                # the line says so; a communicator that formed on this rank only is left open
+                # (tearing it down would wait for the ranks that failed)
+                self.rccl_error = "; ".join(failed)
+                self.stray_group, self.group, self.rccl = self.group, None, False
+                self.backend = "gloo exchange (fallback: the RCCL group did not form on every rank)"
         # wall time of forming the group (RCCL init + the bus-id all-gather), max over ranks below
         self.group_form_s = time.perf_counter() - t0 if self.group is not None else None
         return self.group
@@ -1266,6 +1285,7 @@ def main():
             "rccl_nranks": group.rccl_nranks if group is not None else None,
             "rccl_devices": group.rccl_devices if group is not None else None,
             "group_form_s": group_form_s,
+            **({"rccl_error": ranks.rccl_error} if ranks.rccl_error else {}),
             "rccl_init_timeout_ms": (int(dev.config()["group_init_timeout_ms"]) if group is not None else None),
             "processes": ranks.world,
             "backend": ranks.backend,
@@ -1296,7 +1316,8 @@ def main():
                 "pipelined": pipelined,
                 "exchange": ("library RCCL all-gather of 24-B shard winners + on-device merge (iris_group_*)"
                              if group is not None else
-                             "torch gloo all-gather of 32-B matches + iris_match_merge (rehearsal)"
+                             "torch gloo all-gather of 32-B matches + iris_match_merge "
+                             + ("(fallback)" if ranks.rccl_error else "(rehearsal)")
                              if rehearsal else None),
             },
             "roofline": ({

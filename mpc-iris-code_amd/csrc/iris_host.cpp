@@ -302,7 +302,7 @@ const bool kHaveAvx512 = __builtin_cpu_supports("avx512bw") && __builtin_cpu_sup
 // then block.
 class CopyPool {
    public:
-    explicit CopyPool(int helpers) : pid_(getpid()), nthreads_(helpers + 1) {
+    explicit CopyPool(int helpers) : pid_(getpid()), nthreads_(helpers + 1), nparts_(2 * (helpers + 1)) {
         for (int i = 0; i < helpers; ++i) threads_.emplace_back([this] { worker(); });
         for (auto &t : threads_) t.detach();  // never joined: the pool lives as long as the process
     }
@@ -319,7 +319,6 @@ class CopyPool {
         bytes_ = bytes;
         fd_ = fd;
         off_ = off;
-        nparts_ = 2 * nthreads_;
         ok_.store(true, std::memory_order_relaxed);
         done_.store(0, std::memory_order_relaxed);
         const uint64_t job = ++job_;
@@ -399,7 +398,7 @@ class CopyPool {
     std::atomic<uint64_t> claim_{0};  // (job number << 32) | next unclaimed part
     std::atomic<int> done_{0};        // parts of the current job finished
     uint64_t job_ = 0;
-    int nparts_ = 1;
+    const int nparts_;    // parts per job (fixed: a late helper reads it unsynchronised)
     char *dst_ = nullptr;
     const char *src_ = nullptr;
     const uint16_t *esc_ = nullptr;

@@ -127,3 +127,35 @@ def test_bench_rccl_single_rank():
         # what the library's communicator saw: one rank, on this box's GPU (its PCI bus id)
         assert d["rccl_nranks"] == 1 and len(d["rccl_devices"]) == 1
         assert re.fullmatch(r"[0-9a-fA-F]{4}:[0-9a-fA-F]{2}:[0-9a-fA-F]{2}\.[0-9a-fA-F]", d["rccl_devices"][0])
+
+
+def test_bench_rccl_fallback_when_group_cannot_form():
+    """Two torch.distributed.run ranks with the default RCCL backend on the box's one GPU (each
+    rank told that GPU is its own): RCCL refuses two ranks on one device, every rank learns that
+    over gloo, and the run still searches and exchanges its winners over gloo, saying so in the
+    line (backend, rccl_error, exchange) -- the 8-GPU record is then a measured line with the
+    reason, not a missing one.  IRIS_RCCL_FALLBACK=0 turns the refusal into an error exit."""
+    base = dict(os.environ, HIP_VISIBLE_DEVICES="0", IRIS_GROUP_TIMEOUT_MS="30000")
+    base.pop("IRIS_DIST_BACKEND", None)
+
+    def run(env):
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), str(ROOT / "bench.py"),
+               "--gpus", "2", "--steps", "2", "--warmup", "1", "--n-per-gpu", "200000", "--no-cpu-baseline",
+               "--prewarm-s", "0"]
+        return subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+
+    r = run(base)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["ranks_seen"] == 2 and d["check"]["ok"]
+    assert d["check"]["planted_index"] >= 200000  # found in rank 1's shard, over the gloo exchange
+    assert "fallback" in d["backend"] and d["rccl_error"] and d["rccl_nranks"] is None
+    assert d["config"]["exchange"].endswith("(fallback)")
+
+    r = run(dict(base, IRIS_RCCL_FALLBACK="0"))
+    assert r.returncode != 0
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert "did not form" in r.stderr
