@@ -1,0 +1,71 @@
+#!/bin/bash
+# Builds tools/diag/libiris_hip_timers.so: the library with per-phase timers in the host-slice call
+# (iris_engine_batch_process_host -> readahead_u16_call: set_device, resident_slice, window launch,
+# event wait, copy-out; IRIS_DIAG_PLAIN=1 expands with plain stores), from a patched COPY of the sources (the tree's sources stay untimed).
+# Run here (CPU); tools/diag/call_timers.sh runs the C++ walk against it on the GPU box.
+set -e
+ROOT=$(cd "$(dirname "$0")/../.." && pwd)
+W=$(mktemp -d)
+mkdir -p $W/mpc-iris-code_amd
+cp -r $ROOT/mpc-iris-code_amd/Makefile $ROOT/mpc-iris-code_amd/csrc $W/mpc-iris-code_amd/
+cp -r $ROOT/include $W/
+python3 - $W/mpc-iris-code_amd/csrc/iris_api.hip <<'PY'
+import sys
+p = sys.argv[1]; s = open(p).read()
+hdr = '''
+#include <algorithm>
+#include <array>
+#include <chrono>
+#include <cstdio>
+#include <vector>
+namespace {
+struct CallTimers {
+    std::vector<std::array<double, 8>> calls;
+    ~CallTimers() {
+        if (calls.size() < 12) return;
+        const size_t skip = calls.size() / 6;  // the first of 6 walks (resident fill, first touch of out)
+        std::fprintf(stderr, "call timers (%zu calls after walk 0, median / p90 us):", calls.size() - skip);
+        const char *nm[] = {"", "set_device", "resident_slice", "launch", "event_sync", "expand"};
+        for (int i = 1; i <= 5; ++i) {
+            std::vector<double> v;
+            for (size_t c = skip; c < calls.size(); ++c) v.push_back(calls[c][i]);
+            std::sort(v.begin(), v.end());
+            std::fprintf(stderr, " %s %.2f/%.2f", nm[i], v[v.size() / 2], v[v.size() * 9 / 10]);
+        }
+        std::fprintf(stderr, "\\n");
+    }
+} g_ct;
+thread_local std::array<double, 8> g_cur;
+thread_local double g_t0;
+inline double nowus() { return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count(); }
+inline void mark(int i) { const double t = nowus(); g_cur[i] = t - g_t0; g_t0 = t; }
+}
+'''
+def sub(old, new):
+    global s
+    assert s.count(old) == 1, old
+    s = s.replace(old, new)
+i = s.index('// ---- read-ahead of host-output engine calls')
+s = s[:i] + hdr + s[i:]
+sub('    HIPCHK(hipEventSynchronize(ra.computed[b]));\n    const uint64_t at = first - w.first;',
+    '    mark(3);\n    HIPCHK(hipEventSynchronize(ra.computed[b]));\n    mark(4);\n    const uint64_t at = first - w.first;')
+sub('(size_t)n * kRot * 2, d->ordinal);\n    }\n    if (d->profiling) fold_done(d);\n    return 0;',
+    '(size_t)n * kRot * 2, d->ordinal);\n    }\n    mark(5);\n    g_ct.calls.push_back(g_cur);\n    if (d->profiling) fold_done(d);\n    return 0;')
+sub('uint16_t *out) {\n    IRIS_KEEP_DEVICE();\n    ARG(e, "engine is NULL");\n    ARG(e->kind == IRIS_KIND_MASKS || e->kind == IRIS_KIND_SHARES, "batch_process',
+    'uint16_t *out) {\n    g_t0 = nowus();\n    IRIS_KEEP_DEVICE();\n    ARG(e, "engine is NULL");\n    ARG(e->kind == IRIS_KIND_MASKS || e->kind == IRIS_KIND_SHARES, "batch_process')
+sub('    CHK(set_device(d));\n    if (n == 0) return 0;\n    ARG(records && out, "NULL argument");\n    const KindInfo k = kind_info(e->kind);\n    // a slice of an attached',
+    '    CHK(set_device(d));\n    mark(1);\n    if (n == 0) return 0;\n    ARG(records && out, "NULL argument");\n    const KindInfo k = kind_info(e->kind);\n    // a slice of an attached')
+sub('    CHK(resident_slice(d, e->kind, records, n, &rdb, &rfirst, &rend));\n    if (rdb) {',
+    '    CHK(resident_slice(d, e->kind, records, n, &rdb, &rfirst, &rend));\n    mark(2);\n    if (rdb) {')
+open(p, 'w').write(s)
+# IRIS_DIAG_PLAIN=1: the copy-out's expansion with plain stores instead of non-temporal blocks
+h = p.replace('iris_api.hip', 'iris_host.cpp'); t = open(h).read()
+old = '    if (kHaveAvx512)\n        expand_avx512(out, pk, esc, n);'
+assert t.count(old) == 1
+t = t.replace(old, '    static const bool plain = getenv("IRIS_DIAG_PLAIN") != nullptr;\n    if (kHaveAvx512)\n        (plain ? expand_plain : expand_avx512)(out, pk, esc, n);')
+open(h, 'w').write(t)
+PY
+make -C $W/mpc-iris-code_amd -j8 LIB=libiris_hip_timers.so libiris_hip_timers.so >/dev/null
+cp $W/mpc-iris-code_amd/libiris_hip_timers.so $ROOT/tools/diag/
+rm -rf $W
+echo "built tools/diag/libiris_hip_timers.so"

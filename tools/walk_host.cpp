@@ -2,7 +2,9 @@
 // on-device generator, mapped PROT_READ / MAP_SHARED (memmap2's Mmap::map, src/main.rs:389,458),
 // walked in 20 000-record iris_engine_batch_process_host calls with a fresh engine per walk
 // (src/main.rs:426-431, 511-516).  Prints per-walk records/s and per-call percentiles.
-//   walk_host masks|shares RECORDS WALKS [FILE]   (FILE: walk an existing record file instead)
+//   walk_host masks|shares RECORDS WALKS [FILE|-] [fresh]   (FILE: walk an existing record file
+//   instead; fresh: every call's rows go to a new calloc'd chunk-sized buffer, freed after the call,
+//   as the reference's loops allocate `vec![..; chunk.len()]` per chunk, src/main.rs:429,514)
 // build: g++ -O2 -std=c++17 -I include tools/walk_host.cpp -L mpc-iris-code_amd -liris_hip
 //        -Wl,-rpath,$PWD/mpc-iris-code_amd -Wl,-rpath-link,/opt/rocm/lib -o tools/walk_host
 #include <fcntl.h>
@@ -42,7 +44,8 @@ int main(int argc, char **argv) {
     iris_device_t *dev = nullptr;
     CK(iris_device_open(0, &dev));
     const char *tmp = getenv("TMPDIR") ? getenv("TMPDIR") : "/tmp";
-    const bool given = argc > 4;
+    const bool given = argc > 4 && std::string(argv[4]) != "-";
+    const bool fresh = argc > 5 && std::string(argv[5]) == "fresh";
     const std::string path = given ? std::string(argv[4]) : std::string(tmp) + "/walk_host_" + std::to_string(getpid()) + ".rec";
     if (!given) {
         const uint64_t per = (1ull << 30) / rb;
@@ -75,9 +78,15 @@ int main(int argc, char **argv) {
         std::vector<double> t;
         for (uint64_t a = 0; a < n; a += chunk) {
             const uint64_t m = std::min(chunk, n - a);
+            uint16_t *dst = out.data() + a * 31;
+            if (fresh) dst = (uint16_t *)calloc(m * 31, 2);
             const double c = now_us();
-            CK(iris_engine_batch_process_host(e, map + a * rb, m, out.data() + a * 31));
+            CK(iris_engine_batch_process_host(e, map + a * rb, m, dst));
             t.push_back(now_us() - c);
+            if (fresh) {
+                out[a * 31] = dst[0];  // the rows are used
+                free(dst);
+            }
         }
         iris_engine_destroy(e);
         const double dt = now_us() - t0;
