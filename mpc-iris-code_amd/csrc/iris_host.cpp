@@ -302,7 +302,7 @@ const bool kHaveAvx512 = __builtin_cpu_supports("avx512bw") && __builtin_cpu_sup
 // then block.
 class CopyPool {
    public:
-    explicit CopyPool(int helpers) : pid_(getpid()), nthreads_(helpers + 1), nparts_(2 * (helpers + 1)) {
+    explicit CopyPool(int helpers) : pid_(getpid()), nthreads_(helpers + 1), nparts_(2 * nthreads_) {
         for (int i = 0; i < helpers; ++i) threads_.emplace_back([this] { worker(); });
         for (auto &t : threads_) t.detach();  // never joined: the pool lives as long as the process
     }

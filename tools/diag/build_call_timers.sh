@@ -63,6 +63,61 @@ h = p.replace('iris_api.hip', 'iris_host.cpp'); t = open(h).read()
 old = '    if (kHaveAvx512)\n        expand_avx512(out, pk, esc, n);'
 assert t.count(old) == 1
 t = t.replace(old, '    static const bool plain = getenv("IRIS_DIAG_PLAIN") != nullptr;\n    if (kHaveAvx512)\n        (plain ? expand_plain : expand_avx512)(out, pk, esc, n);')
+# IRIS_DIAG_HELPER_CPUS=a-b,c-d: the helpers run on those CPUs; IRIS_DIAG_SPREAD=1: helper i runs on the CPUs of the (i+1)-th L3 domain after the pool creator's
+# (of the CPUs this process may use); IRIS_DIAG_TOPO=1 prints the domains and where threads run
+spread = r"""
+#include <sched.h>
+#include <stdio.h>
+static std::vector<std::vector<int>> diag_l3_domains() {
+    cpu_set_t allowed; CPU_ZERO(&allowed); sched_getaffinity(0, sizeof(allowed), &allowed);
+    std::vector<std::vector<int>> doms; std::vector<std::string> keys;
+    for (int c = 0; c < CPU_SETSIZE; ++c) {
+        if (!CPU_ISSET(c, &allowed)) continue;
+        char path[128]; snprintf(path, sizeof(path), "/sys/devices/system/cpu/cpu%d/cache/index3/shared_cpu_list", c);
+        FILE *f = fopen(path, "r"); if (!f) continue;
+        char buf[256] = {}; if (!fgets(buf, sizeof(buf), f)) buf[0] = 0; fclose(f);
+        std::string k(buf); size_t i = 0;
+        for (; i < keys.size() && keys[i] != k; ++i) {}
+        if (i == keys.size()) { keys.push_back(k); doms.emplace_back(); }
+        doms[i].push_back(c);
+    }
+    return doms;
+}
+static void diag_place(int helper) {
+    static const bool on = getenv("IRIS_DIAG_SPREAD") != nullptr, topo = getenv("IRIS_DIAG_TOPO") != nullptr;
+    static std::vector<std::vector<int>> doms = diag_l3_domains();
+    static int home = sched_getcpu();
+    if (topo && helper == 0) {
+        fprintf(stderr, "diag: %zu L3 domains allowed, creator on cpu %d; sizes:", doms.size(), home);
+        for (auto &d : doms) fprintf(stderr, " %zu(first %d)", d.size(), d.empty() ? -1 : d[0]);
+        fprintf(stderr, "\n");
+    }
+    if (const char *cl = getenv("IRIS_DIAG_HELPER_CPUS")) {  // "a-b,c-d": the helpers' CPUs
+        cpu_set_t set; CPU_ZERO(&set);
+        for (const char *q = cl; *q;) {
+            char *e; const long a = strtol(q, &e, 10); long b = a;
+            if (*e == '-') b = strtol(e + 1, &e, 10);
+            for (long c = a; c <= b; ++c) CPU_SET((int)c, &set);
+            q = *e == ',' ? e + 1 : e;
+            if (e == q && *q) break;
+        }
+        sched_setaffinity(0, sizeof(set), &set);
+        return;
+    }
+    if (!on || doms.size() < 2) return;
+    size_t h = 0;
+    for (size_t i = 0; i < doms.size(); ++i) for (int c : doms[i]) if (c == home) h = i;
+    const auto &d = doms[(h + 1 + helper) % doms.size()];
+    cpu_set_t set; CPU_ZERO(&set); for (int c : d) CPU_SET(c, &set);
+    sched_setaffinity(0, sizeof(set), &set);
+}
+"""
+old = 'class CopyPool {'
+assert t.count(old) == 1
+t = t.replace(old, spread + old)
+old = '        for (int i = 0; i < helpers; ++i) threads_.emplace_back([this] { worker(); });'
+assert t.count(old) == 1
+t = t.replace(old, '        for (int i = 0; i < helpers; ++i) threads_.emplace_back([this, i] { diag_place(i); if (getenv("IRIS_DIAG_TOPO")) fprintf(stderr, "diag: helper %d on cpu %d\\n", i, sched_getcpu()); worker(); });')
 open(h, 'w').write(t)
 PY
 make -C $W/mpc-iris-code_amd -j8 LIB=libiris_hip_timers.so libiris_hip_timers.so >/dev/null
