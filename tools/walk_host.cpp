@@ -2,8 +2,8 @@
 // on-device generator, mapped PROT_READ / MAP_SHARED (memmap2's Mmap::map, src/main.rs:389,458),
 // walked in 20 000-record iris_engine_batch_process_host calls with a fresh engine per walk
 // (src/main.rs:426-431, 511-516).  Prints per-walk records/s and per-call percentiles.
-//   walk_host masks|shares RECORDS WALKS [FILE|-] [fresh]   (FILE: walk an existing record file
-//   instead; fresh: every call's rows go to a new calloc'd chunk-sized buffer, freed after the call,
+//   walk_host masks|shares RECORDS WALKS [FILE|-] [fresh]   (FILE: walk that record file instead,
+//   written first if it does not exist; fresh: every call's rows go to a new calloc'd chunk-sized buffer, freed after the call,
 //   as the reference's loops allocate `vec![..; chunk.len()]` per chunk, src/main.rs:429,514)
 // build: g++ -O2 -std=c++17 -I include tools/walk_host.cpp -L mpc-iris-code_amd -liris_hip
 //        -Wl,-rpath,$PWD/mpc-iris-code_amd -Wl,-rpath-link,/opt/rocm/lib -o tools/walk_host
@@ -47,7 +47,7 @@ int main(int argc, char **argv) {
     const bool given = argc > 4 && std::string(argv[4]) != "-";
     const bool fresh = argc > 5 && std::string(argv[5]) == "fresh";
     const std::string path = given ? std::string(argv[4]) : std::string(tmp) + "/walk_host_" + std::to_string(getpid()) + ".rec";
-    if (!given) {
+    if (!given || access(path.c_str(), F_OK) != 0) {  // a FILE that does not exist yet is written and kept
         const uint64_t per = (1ull << 30) / rb;
         iris_db_t *g = nullptr;
         CK(iris_db_create(dev, kind, std::min(n, per), &g));
