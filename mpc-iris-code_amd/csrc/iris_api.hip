@@ -291,6 +291,7 @@ int ra_wait(iris_engine *e) {
     iris_device *d = e->dev;
     if (d->aux) HIPCHK(hipStreamSynchronize(d->aux));
     if (d->aux2) HIPCHK(hipStreamSynchronize(d->aux2));
+    if (ra.on[0] == d->stream || ra.on[1] == d->stream) HIPCHK(hipStreamSynchronize(d->stream));
     if (d->profiling) fold_done(d);
     return 0;
 }
@@ -393,7 +394,8 @@ void ra_release(iris_engine *e) {
     ra = Readahead{};
 }
 
-// Enqueues the engine kernel over [first, first+n) of db on the device's side stream; it stores
+// Enqueues the engine kernel over [first, first+n) of db on the buffer's side stream (or the busy
+// device stream, below); it stores
 // the rows straight into the pinned buffer rows[b] (over the host link, no copy-engine DMA) and
 // records computed[b]; win[b] describes them from now on.  rows[b] is not being read: the host
 // copies out synchronously.  grow = false: if the buffers are too small, launch nothing
@@ -428,15 +430,25 @@ int ra_launch(iris_engine *e, const iris_db *a, uint64_t first, uint64_t n, int 
     // event -- the cross-stream wait costs ~10 us per launch (profiles/r03_readahead.txt)
     // buffer b's windows run on their own side stream: the next window's kernel is not queued
     // behind this one's drain (the two write different buffers and only read the database)
+    // An engine's first window goes on the device stream itself, behind its query tables (built
+    // there just before): no query of the stream and no cross-stream event, which had cost 6-35 us
+    // of a walk's first call (profiles/r06ae_first_call_phases.txt).  Nothing of the engine is in
+    // flight then; by its next launch the call has waited for this window, and a busy device
+    // stream orders the side stream after everything on it, this window included.
     hipStream_t side = b ? d->aux2 : d->aux;
-    const hipError_t idle = hipStreamQuery(d->stream);
-    if (idle != hipSuccess) {
-        if (idle != hipErrorNotReady) return fail(IRIS_E_HIP, std::string("hipStreamQuery: ") + hipGetErrorString(idle));
-        if (!d->ra_order) HIPCHK(hipEventCreateWithFlags(&d->ra_order, hipEventDisableTiming));
-        HIPCHK(hipEventRecord(d->ra_order, d->stream));
-        HIPCHK(hipStreamWaitEvent(side, d->ra_order, 0));
+    if (!ra.on[0] && !ra.on[1]) {
+        side = d->stream;
+    } else {
+        const hipError_t idle = hipStreamQuery(d->stream);
+        if (idle != hipSuccess) {
+            if (idle != hipErrorNotReady) return fail(IRIS_E_HIP, std::string("hipStreamQuery: ") + hipGetErrorString(idle));
+            if (!d->ra_order) HIPCHK(hipEventCreateWithFlags(&d->ra_order, hipEventDisableTiming));
+            HIPCHK(hipEventRecord(d->ra_order, d->stream));
+            HIPCHK(hipStreamWaitEvent(side, d->ra_order, 0));
+        }
     }
     ra.win[b].live = false;
+    ra.on[b] = side;
     CHK(enqueue_u16_engine(e, a, first, n, (uint16_t *)ra.rows[b], side, nullptr, ra_packed(e)));
     HIPCHK(hipEventRecord(ra.computed[b], side));
     ra.win[b] = Readahead::Window{a, a->version, first, n, true};

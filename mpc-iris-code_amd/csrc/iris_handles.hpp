@@ -198,7 +198,8 @@ struct Readahead {
     Window win[2];
     void *rows[2] = {nullptr, nullptr};      // pinned host [n][31] u16 rows
     size_t cap = 0;                          // bytes of each
-    hipEvent_t computed[2] = {nullptr, nullptr};  // side stream, after the kernel into rows[b]
+    hipEvent_t computed[2] = {nullptr, nullptr};  // after the kernel into rows[b], on stream on[b]
+    hipStream_t on[2] = {nullptr, nullptr};      // the stream of the last kernel into rows[b]
     // the previous call's range end: a call that starts there (or was read ahead) is part of a
     // walk, and only then is the next window computed speculatively (a random-access caller
     // never pays for rows it does not ask for)

@@ -33,6 +33,10 @@ struct CallTimers {
             std::fprintf(stderr, " %s %.2f/%.2f", nm[i], v[v.size() / 2], v[v.size() * 9 / 10]);
         }
         std::fprintf(stderr, "\\n");
+        const size_t per = calls.size() / 6;  // each walk's first call (a new engine's first window)
+        for (size_t c = per; c < calls.size(); c += per)
+            std::fprintf(stderr, "first call of walk %zu: set_device %.2f resident_slice %.2f launch %.2f event_sync %.2f expand %.2f (launch: aux+events %.2f, order event %.2f)\\n",
+                         c / per, calls[c][1], calls[c][2], calls[c][3], calls[c][4], calls[c][5], calls[c][6], calls[c][7]);
     }
 } g_ct;
 thread_local std::array<double, 8> g_cur;
@@ -57,6 +61,16 @@ sub('    CHK(set_device(d));\n    if (n == 0) return 0;\n    ARG(records && out,
     '    CHK(set_device(d));\n    mark(1);\n    if (n == 0) return 0;\n    ARG(records && out, "NULL argument");\n    const KindInfo k = kind_info(e->kind);\n    // a slice of an attached')
 sub('    CHK(resident_slice(d, e->kind, records, n, &rdb, &rfirst, &rend));\n    if (rdb) {',
     '    CHK(resident_slice(d, e->kind, records, n, &rdb, &rfirst, &rend));\n    mark(2);\n    if (rdb) {')
+# sub-phases of a window launch: [6] ensure_aux + event creation, [7] the order event on the device stream
+sub('    if (launched) *launched = false;\n    CHK(ensure_aux(d));',
+    '    if (launched) *launched = false;\n    const double s0 = nowus();\n    CHK(ensure_aux(d));')
+sub('    const size_t rec = ra_rec_bytes(e);\n    const size_t bytes = (size_t)n * rec;',
+    '    g_cur[6] += nowus() - s0;\n    const size_t rec = ra_rec_bytes(e);\n    const size_t bytes = (size_t)n * rec;')
+sub('    hipStream_t side = b ? d->aux2 : d->aux;\n',
+    '    hipStream_t side = b ? d->aux2 : d->aux;\n    const double s2 = nowus();\n')
+sub('    ra.win[b].live = false;\n    ra.on[b] = side;\n    CHK(enqueue_u16_engine',
+    '    g_cur[7] += nowus() - s2;\n    ra.win[b].live = false;\n    ra.on[b] = side;\n    CHK(enqueue_u16_engine')
+sub('    g_t0 = nowus();\n    IRIS_KEEP_DEVICE();', '    g_t0 = nowus();\n    g_cur[6] = g_cur[7] = 0;\n    IRIS_KEEP_DEVICE();')
 open(p, 'w').write(s)
 # IRIS_DIAG_PLAIN=1: the copy-out's expansion with plain stores instead of non-temporal blocks
 h = p.replace('iris_api.hip', 'iris_host.cpp'); t = open(h).read()
