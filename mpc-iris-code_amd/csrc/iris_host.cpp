@@ -276,6 +276,30 @@ __attribute__((target("avx512bw,avx512vl"))) void expand_avx512(uint16_t *out, c
     _mm_sfence();  // the streamed lines are globally visible before this thread reports its part done
 }
 
+// A copy whose destination lines are written with non-temporal 64-B stores (from the first 64-B
+// boundary of dst on; the source may have any alignment): the caller's array is not read for
+// ownership first, as plain stores into lines that miss the caches do (the packed rows' expansion
+// measured 1.0 against 1.9 ns per 62-B row, profiles/r06b_expand_nt_epyc.txt).
+__attribute__((target("avx512f"))) void copy_nt_avx512(char *dst, const char *src, size_t n) {
+    const size_t head = std::min<size_t>(n, (64 - ((uintptr_t)dst & 63)) & 63);
+    memcpy(dst, src, head);
+    dst += head;
+    src += head;
+    n -= head;
+    size_t i = 0;
+    for (; i + 256 <= n; i += 256) {
+        const __m512i a = _mm512_loadu_si512(src + i), b = _mm512_loadu_si512(src + i + 64),
+                      c = _mm512_loadu_si512(src + i + 128), d = _mm512_loadu_si512(src + i + 192);
+        _mm512_stream_si512((__m512i *)(dst + i), a);
+        _mm512_stream_si512((__m512i *)(dst + i + 64), b);
+        _mm512_stream_si512((__m512i *)(dst + i + 128), c);
+        _mm512_stream_si512((__m512i *)(dst + i + 192), d);
+    }
+    for (; i + 64 <= n; i += 64) _mm512_stream_si512((__m512i *)(dst + i), _mm512_loadu_si512(src + i));
+    memcpy(dst + i, src + i, n - i);
+    _mm_sfence();  // the streamed lines are globally visible before this thread reports its part done
+}
+
 void expand_scalar(uint16_t *out, const uint8_t *pk, const uint16_t *esc, size_t n) {
     for (size_t i = 0; i < n; ++i) {
         const uint8_t *p = pk + 32 * i;
@@ -300,6 +324,17 @@ const bool kHaveAvx512 = __builtin_cpu_supports("avx512bw") && __builtin_cpu_sup
 // first call of a walk after a pause) costs a share of the work, not its wake-up latency.  The
 // helpers spin for a while after each job (calls of a chunk walk arrive every few tens of us) and
 // then block.
+}  // namespace
+
+void copy_nt(char *dst, const char *src, size_t n) {
+    if (kHaveAvx512 && n >= 4096)
+        copy_nt_avx512(dst, src, n);
+    else
+        memcpy(dst, src, n);
+}
+
+namespace {
+
 class CopyPool {
    public:
     explicit CopyPool(int helpers) : pid_(getpid()), nthreads_(helpers + 1), nparts_(2 * nthreads_) {
@@ -359,7 +394,7 @@ class CopyPool {
         const size_t a = std::min(bytes_, (size_t)id * per), b = std::min(bytes_, a + per);
         if (a >= b) return;
         if (src_) {
-            memcpy(dst_ + a, src_ + a, b - a);
+            copy_nt(dst_ + a, src_ + a, b - a);
             return;
         }
         for (size_t done = a; done < b;) {

@@ -328,5 +328,7 @@ bool parallel_pread(int fd, void *dst, size_t bytes, off_t off, int lane = 0);
 // the same helper threads
 void parallel_expand(uint16_t *out, const uint8_t *pk, const uint16_t *esc, size_t n, int lane = 0);
 void expand_packed_rows(uint16_t *out, const uint8_t *pk, const uint16_t *esc, size_t n);  // one thread
+// memcpy whose destination lines are written with non-temporal stores (AVX-512, >= 4 KB); one thread
+void copy_nt(char *dst, const char *src, size_t n);
 
 }  // namespace iris

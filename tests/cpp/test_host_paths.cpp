@@ -2,7 +2,8 @@
 // MasksEngine rows (store_tile_packed's format, csrc/iris_device.hpp; csrc/iris_host.cpp
 // expand_packed_rows / parallel_expand: the AVX-512 form with its non-temporal 32-record blocks,
 // escaped rows, every alignment of the caller's array) against a scalar restatement, and the
-// helper pool's parallel_copy under concurrent callers (parts claimed by whoever is free).
+// helper pool's parallel_copy under concurrent callers (parts claimed by whoever is free), and
+// copy_nt (non-temporal stores from dst's first 64-B boundary) at every source / destination offset.
 // These are library internals, declared here as the library defines them (iris_internal.hpp).
 #include <atomic>
 #include <cstdio>
@@ -15,6 +16,7 @@ namespace iris {
 void parallel_copy(void *dst, const void *src, size_t bytes, int lane);
 void parallel_expand(uint16_t *out, const uint8_t *pk, const uint16_t *esc, size_t n, int lane);
 void expand_packed_rows(uint16_t *out, const uint8_t *pk, const uint16_t *esc, size_t n);
+void copy_nt(char *dst, const char *src, size_t n);
 }  // namespace iris
 
 static int failures = 0;
@@ -64,6 +66,24 @@ int main() {
             // nothing written past the last row
             for (size_t j = shift + n * 31; j < buf.size(); ++j) CHECK(buf[j] == 0xABCD);
             for (int j = 0; j < shift; ++j) CHECK(buf[j] == 0xABCD);
+        }
+    }
+    // copy_nt: every destination and source offset within a line, lengths around its 4-KB threshold,
+    // the 256-B unrolled body and the 64-B tail; nothing outside [dst, dst + n) is written
+    {
+        std::vector<char> src(70000 + 128);
+        for (auto &c : src) c = (char)r();
+        for (size_t n : {0, 1, 63, 64, 65, 4095, 4096, 4097, 4096 + 255, 4096 + 256 + 63, 65536 + 17}) {
+            for (int so = 0; so < 64; so += 7) {
+                for (int dof = 0; dof < 64; ++dof) {
+                    std::vector<char> buf(n + 192, (char)0x5A);
+                    char *dst = buf.data() + 64 + dof - ((uintptr_t)(buf.data() + 64) & 63);
+                    iris::copy_nt(dst, src.data() + so, n);
+                    CHECK(std::memcmp(dst, src.data() + so, n) == 0);
+                    for (char *q = buf.data(); q < dst; ++q) CHECK(*q == (char)0x5A);
+                    for (char *q = dst + n; q < buf.data() + buf.size(); ++q) CHECK(*q == (char)0x5A);
+                }
+            }
         }
     }
     // the helper pool: a participant-sized chunk (20 000 records) and a window, from 4 threads at once
