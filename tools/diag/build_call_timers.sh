@@ -97,10 +97,10 @@ static std::vector<std::vector<int>> diag_l3_domains() {
     }
     return doms;
 }
-static void diag_place(int helper) {
+static void diag_place(int helper, int creator) {
     static const bool on = getenv("IRIS_DIAG_SPREAD") != nullptr, topo = getenv("IRIS_DIAG_TOPO") != nullptr;
     static std::vector<std::vector<int>> doms = diag_l3_domains();
-    static int home = sched_getcpu();
+    const int home = creator;
     if (topo && helper == 0) {
         fprintf(stderr, "diag: %zu L3 domains allowed, creator on cpu %d; sizes:", doms.size(), home);
         for (auto &d : doms) fprintf(stderr, " %zu(first %d)", d.size(), d.empty() ? -1 : d[0]);
@@ -118,6 +118,29 @@ static void diag_place(int helper) {
         sched_setaffinity(0, sizeof(set), &set);
         return;
     }
+    if (getenv("IRIS_DIAG_NODE")) {  // the CPUs of the pool creator's NUMA node (of those allowed)
+        int node = -1;
+        for (int n = 0; n < 64 && node < 0; ++n) {
+            char path[128]; snprintf(path, sizeof(path), "/sys/devices/system/cpu/cpu%d/node%d", home, n);
+            if (access(path, F_OK) == 0) node = n;
+        }
+        char path[128]; snprintf(path, sizeof(path), "/sys/devices/system/node/node%d/cpulist", node);
+        FILE *f = fopen(path, "r"); char buf[512] = {};
+        if (!f || !fgets(buf, sizeof(buf), f)) { if (f) fclose(f); return; }
+        fclose(f);
+        cpu_set_t allowed; CPU_ZERO(&allowed); sched_getaffinity(0, sizeof(allowed), &allowed);
+        cpu_set_t set; CPU_ZERO(&set);
+        for (const char *q = buf; *q && *q != '\n';) {
+            char *e; const long a = strtol(q, &e, 10); long b = a;
+            if (*e == '-') b = strtol(e + 1, &e, 10);
+            for (long c = a; c <= b; ++c) if (CPU_ISSET((int)c, &allowed)) CPU_SET((int)c, &set);
+            q = *e == ',' ? e + 1 : e;
+            if (e == q) break;
+        }
+        if (CPU_COUNT(&set)) sched_setaffinity(0, sizeof(set), &set);
+        if (topo) fprintf(stderr, "diag: helper %d -> node %d (creator cpu %d)\n", helper, node, home);
+        return;
+    }
     if (!on || doms.size() < 2) return;
     size_t h = 0;
     for (size_t i = 0; i < doms.size(); ++i) for (int c : doms[i]) if (c == home) h = i;
@@ -131,7 +154,7 @@ assert t.count(old) == 1
 t = t.replace(old, spread + old)
 old = '        for (int i = 0; i < helpers; ++i) threads_.emplace_back([this] { worker(); });'
 assert t.count(old) == 1
-t = t.replace(old, '        for (int i = 0; i < helpers; ++i) threads_.emplace_back([this, i] { diag_place(i); if (getenv("IRIS_DIAG_TOPO")) fprintf(stderr, "diag: helper %d on cpu %d\\n", i, sched_getcpu()); worker(); });')
+t = t.replace(old, '        for (int i = 0; i < helpers; ++i) threads_.emplace_back([this, i, c = sched_getcpu()] { diag_place(i, c); if (getenv("IRIS_DIAG_TOPO")) fprintf(stderr, "diag: helper %d on cpu %d\\n", i, sched_getcpu()); worker(); });')
 open(h, 'w').write(t)
 PY
 make -C $W/mpc-iris-code_amd -j8 LIB=libiris_hip_timers.so libiris_hip_timers.so >/dev/null
