@@ -105,6 +105,16 @@ def test_value_types():
     assert (sum((s.values.astype(np.uint64) for s in shares)) & 0xFFFF == e.values).all()
 
 
+def test_python_fast_path_links_the_shipped_library():
+    """The fast path is linked to the shipped libiris_hip.so (a variant build such as
+    tools/asan_host.sh's must not relink it to its own library)."""
+    p = pathlib.Path(ih.__file__).parent / "_iris_pycall.so"
+    if not p.exists():
+        pytest.skip("no Python headers here: the fast path is not built")
+    data = p.read_bytes()
+    assert b"libiris_hip.so\0" in data and b"libiris_asan.so" not in data
+
+
 def test_python_fast_path_extension():
     """The Python mirror's per-call fast path (csrc/iris_pycall.c) is built beside the library and
     used: it passes the caller's buffers to iris_engine_batch_process_host unchanged, so its
