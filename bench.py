@@ -58,7 +58,7 @@ VALU_OPS_PER_TEMPLATE = 400 * 31 * 4   # words x rotations x (and, bitop3, 2x bc
 ROT = 31
 SEED = 20251015
 GPU_WORKLOADS = ("search", "masks", "shares", "batch")
-AUX_WORKLOADS = ("resolver", "resolve-masks", "prepare", "load", "host-shares", "host-masks", "criterion")
+AUX_WORKLOADS = ("resolver", "host-resolver", "resolve-masks", "prepare", "load", "host-shares", "host-masks", "criterion")
 
 
 def parse():
@@ -308,7 +308,7 @@ def cpu_baseline(args, reserve=0):
             value *= ROT
         sample = (f"{passes} passes of DistanceEngine::batch_process (dot_u16, src/lib.rs:42-52, "
                   f"src/arch/generic.rs:11-16) over {n} shares, per-record rate extrapolated")
-    elif wl in ("resolver", "resolve-masks"):
+    elif wl in ("resolver", "host-resolver", "resolve-masks"):
         n = 2_000_000
         rng = np.random.default_rng(SEED)
         shares = rng.integers(0, 65536, (args.parties, n, ROT), dtype=np.uint16)
@@ -626,20 +626,28 @@ def run_aux(args, dev):
     rng = np.random.default_rng(SEED)
     ptrs = []
     extra = {}
-    if args.workload == "resolver":
+    if args.workload in ("resolver", "host-resolver"):
         n = args.n_per_gpu
         shares = rng.integers(0, 65536, (P, n, ROT), dtype=np.uint16)
         denoms = rng.integers(0, 12801, (n, ROT), dtype=np.uint16)
-        for j in range(P + 1):
-            ptrs.append(dev.alloc(n * ROT * 2))
-            dev.h2d(ptrs[j], shares[j] if j < P else denoms)
+        if args.workload == "resolver":
+            for j in range(P + 1):
+                ptrs.append(dev.alloc(n * ROT * 2))
+                dev.h2d(ptrs[j], shares[j] if j < P else denoms)
 
-        def step():
-            return ih.resolver_search_device(dev, ptrs[:P], ptrs[P], n)
+            def step():
+                return ih.resolver_search_device(dev, ptrs[:P], ptrs[P], n)
+        else:
+            host_parts = list(shares)
+
+            def step():  # the rows in host memory, as they arrive from the participants
+                return ih.resolver_search(host_parts, denoms, device=dev)
 
         kname, unit = "resolver", "records/s"
         rec_bytes = (P + 1) * ROT * 2  # P share rows + the denominator row, read once
-        workload = f"resolver: {P} participants' [u16;31] outputs + denominators -> min/argmin (src/main.rs:597-621)"
+        workload = (f"resolver: {P} participants' [u16;31] outputs + denominators -> min/argmin (src/main.rs:597-621)"
+                    + (", host arrays: pinned-slot uploads overlapped with the kernels (PCIe-inclusive)"
+                       if args.workload == "host-resolver" else ""))
     elif args.workload == "resolve-masks":
         n = args.n_per_gpu
         shares = rng.integers(0, 65536, (P, n, ROT), dtype=np.uint16)
@@ -899,7 +907,7 @@ def run_aux(args, dev):
         sample = np.random.default_rng(1).choice(n, 64, replace=False)
         recs = np.stack([mdb.read(int(i), 1)[0] for i in sample])
         assert (denoms[sample] == check_masks_rows(qmask, recs)).all()
-    if args.workload in ("resolver", "resolve-masks"):
+    if args.workload in ("resolver", "host-resolver", "resolve-masks"):
         best, idx = check_resolver(shares, denoms)
         ok = m.index == idx and np.float64(m.distance).view(np.uint64) == np.float64(best).view(np.uint64)
         check = {"expected_index": int(idx), "found_index": int(m.index), "ok": bool(ok)}
@@ -964,6 +972,7 @@ def run_aux(args, dev):
     per_unit = ROT if args.workload == "criterion" else 1
     line = {
         "metric": {"resolver": "resolver records/s (share sum + decode + argmin)",
+                   "host-resolver": "resolver records/s over host arrays (share sum + decode + argmin, PCIe-inclusive)",
                    "resolve-masks": "resolver records/s (masks engine + share sum + decode + argmin, fused)",
                    "prepare": "templates prepared/s (shares + masks)",
                    "load": "templates loaded/s (file -> resident database, PCIe-inclusive)",
@@ -975,6 +984,7 @@ def run_aux(args, dev):
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None,
         "dtype": {"resolver": "u16 (wrapping share sums) -> u32 cross-multiplied fractions",
+                  "host-resolver": "u16 (wrapping share sums) -> u32 cross-multiplied fractions",
                   "resolve-masks": "fp4 e2m1 MFMA -> f32 denominators, u16 share sums",
                   "prepare": "u32 (ChaCha keystream) -> u16 shares",
                   "load": "u8 (record bytes)",
@@ -996,8 +1006,8 @@ def run_aux(args, dev):
                    "bytes_per_record": rec_bytes},
         "file_GBps": (n * 3200 * args.steps / elapsed / 1e9) if args.workload == "load" else None,
         "host_input_GBps": (n * rec_bytes * args.steps / elapsed / 1e9)
-        if args.workload in ("host-shares", "host-masks") and not args.attached
-        and not (args.mmap and not args.no_auto_resident) else None,
+        if (args.workload in ("host-shares", "host-masks") and not args.attached
+            and not (args.mmap and not args.no_auto_resident)) or args.workload == "host-resolver" else None,
         "cpu_baseline": cpu,
         "check": check,
         **extra,

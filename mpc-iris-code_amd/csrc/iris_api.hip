@@ -1786,14 +1786,77 @@ int iris_resolver_search_masks(iris_engine_t *e, const iris_db_t *db, uint64_t f
     return 0;
 }
 
-int iris_resolver_search_host(iris_device_t *d, const uint16_t *const *shares, uint32_t parts, const uint16_t *denoms,
-                              uint64_t n, uint64_t index_base, iris_match_t *out) {
-    IRIS_KEEP_DEVICE();
-    ARG(d && out, "NULL argument");
-    ARG(parts >= 1 && parts <= 8, "parts must be 1..8");
-    ARG(n == 0 || (shares && denoms), "NULL argument");
-    std::lock_guard<std::recursive_mutex> g(d->mu);
-    CHK(set_device(d));
+// The resolver step over host arrays (the participants' rows as they arrive, src/main.rs:597-621):
+// a chunk's parts and denominators are copied by the helper threads into one pinned upload slot
+// (parallel_copy, non-temporal stores), moved by the copy engine into a device staging slot, and
+// combined + decoded + reduced there (the reduce writes the chunk's winner, its index already
+// offset, into a pinned result slot), while the host fills the other slot with the next chunk; the
+// call waits once, at the end, and merges the chunks' winners in chunk order.  The runtime's own
+// copy of a pageable source ran at 29-30 GB/s for some caller arrays and 53-55 GB/s for others
+// (profiles/r04_host_upload.txt, r06am_host_resolver.txt), so, as for large database writes, the
+// call takes whichever of the two was faster lately (the device's UploadTune, shared with them).
+static int resolver_host_pinned(iris_device *d, const uint16_t *const *shares, uint32_t parts, const uint16_t *denoms,
+                                uint64_t n, uint64_t index_base, iris_match_t *out) {
+    iris_match_t best;
+    match_from(Partial{}, false, 0, &best);
+    const size_t row = (size_t)kRot * 2;
+    const uint32_t arrays = parts + 1;
+    // records per slot (the parts' rows, then the denominators), a multiple of 64
+    const uint64_t ch = std::min<uint64_t>(n, std::max<uint64_t>(64, kUploadSlot / (arrays * row) / 64 * 64));
+    const uint64_t chunks = (n + ch - 1) / ch;
+    const size_t slot = (size_t)ch * arrays * row;
+    CHK(ensure_upin(d));
+    CHK(ensure(d, d->staging, kUploadSlots * slot));
+    CHK(ensure(d, d->partials, (size_t)std::max<uint32_t>(resolver_partials(ch), 1) * sizeof(Partial)));
+    CHK(ensure_host_result(d, (size_t)chunks * sizeof(Partial)));
+    Partial *res = (Partial *)d->host_result;
+    int rc = 0;
+    for (uint64_t c = 0; c < chunks && rc == 0; ++c) {
+        const uint64_t a = c * ch, m = std::min<uint64_t>(ch, n - a);
+        const int b = (int)(c % kUploadSlots);
+        // pinned slot b was last read by the copy of chunk c - kUploadSlots (the previous call's
+        // copies ended with its sync)
+        if (c >= (uint64_t)kUploadSlots && hipEventSynchronize(d->upin_ev[b]) != hipSuccess) {
+            rc = fail(IRIS_E_HIP, "hipEventSynchronize");
+            break;
+        }
+        char *pin = (char *)d->upin[b];
+        for (uint32_t p = 0; p < arrays; ++p)
+            parallel_copy(pin + (size_t)p * m * row, (const char *)((p < parts ? shares[p] : denoms) + a * kRot), m * row,
+                          d->ordinal);
+        char *stage = (char *)d->staging.p + (size_t)b * slot;
+        if (hipMemcpyAsync(stage, pin, (size_t)arrays * m * row, hipMemcpyHostToDevice, d->stream) != hipSuccess ||
+            hipEventRecord(d->upin_ev[b], d->stream) != hipSuccess) {
+            rc = fail(IRIS_E_HIP, "hipMemcpyAsync upload");
+            break;
+        }
+        const uint16_t *dev_sh[8];
+        for (uint32_t p = 0; p < parts; ++p) dev_sh[p] = (const uint16_t *)(stage + (size_t)p * m * row);
+        const uint16_t *dden = (const uint16_t *)(stage + (size_t)parts * m * row);
+        const uint32_t np = resolver_partials(m);
+        rc = timed(d, "resolver", m, [&] {
+            return launch_resolver(d->stream, dev_sh, parts, dden, m, nullptr, (Partial *)d->partials.p);
+        });
+        // the chunk's winner, its index offset to the call's records, into result slot c
+        if (rc == 0)
+            rc = timed(d, "reduce", np, [&] { return launch_reduce(d->stream, (Partial *)d->partials.p, np, res + c, a); });
+    }
+    const int rs = sync(d);  // the pinned slots are free again and every chunk's winner is in place
+    CHK(rc);
+    CHK(rs);
+    for (uint64_t c = 0; c < chunks; ++c) {
+        iris_match_t pair[2] = {best, {}};
+        match_from(res[c], true, index_base, &pair[1]);
+        CHK(iris_match_merge(pair, 2, &best));
+    }
+    *out = best;
+    return 0;
+}
+
+// The runtime's copy of each pageable array into device staging, one chunk of up to 1M records at a
+// time, and the device-input resolver on it.
+static int resolver_host_runtime(iris_device *d, const uint16_t *const *shares, uint32_t parts, const uint16_t *denoms,
+                                 uint64_t n, uint64_t index_base, iris_match_t *out) {
     const uint64_t ch = std::min<uint64_t>(n, 1ull << 20);
     const size_t row = (size_t)kRot * 2;
     CHK(ensure(d, d->staging, std::max<uint64_t>(ch, 1) * row * (parts + 1)));
@@ -1802,19 +1865,50 @@ int iris_resolver_search_host(iris_device_t *d, const uint16_t *const *shares, u
     for (uint64_t done = 0; done < n; done += ch) {
         const uint64_t m = std::min<uint64_t>(ch, n - done);
         const uint16_t *dev_sh[8];
-        for (uint32_t p = 0; p < parts; ++p) {
+        for (uint32_t p = 0; p <= parts; ++p) {
             uint16_t *dst = (uint16_t *)((char *)d->staging.p + (size_t)p * ch * row);
-            HIPCHK(hipMemcpyAsync(dst, shares[p] + done * kRot, m * row, hipMemcpyHostToDevice, d->stream));
-            dev_sh[p] = dst;
+            HIPCHK(hipMemcpyAsync(dst, (p < parts ? shares[p] : denoms) + done * kRot, m * row, hipMemcpyHostToDevice,
+                                  d->stream));
+            if (p < parts) dev_sh[p] = dst;
         }
-        uint16_t *dden = (uint16_t *)((char *)d->staging.p + (size_t)parts * ch * row);
-        HIPCHK(hipMemcpyAsync(dden, denoms + done * kRot, m * row, hipMemcpyHostToDevice, d->stream));
+        const uint16_t *dden = (const uint16_t *)((char *)d->staging.p + (size_t)parts * ch * row);
         iris_match_t cm;
         CHK(iris_resolver_search(d, dev_sh, parts, dden, m, index_base + done, nullptr, &cm));
         iris_match_t pair[2] = {best, cm};
         CHK(iris_match_merge(pair, 2, &best));
     }
     *out = best;
+    return 0;
+}
+
+int iris_resolver_search_host(iris_device_t *d, const uint16_t *const *shares, uint32_t parts, const uint16_t *denoms,
+                              uint64_t n, uint64_t index_base, iris_match_t *out) {
+    IRIS_KEEP_DEVICE();
+    ARG(d && out, "NULL argument");
+    ARG(parts >= 1 && parts <= 8, "parts must be 1..8");
+    ARG(n == 0 || (shares && denoms), "NULL argument");
+    for (uint32_t p = 0; n && p < parts; ++p) ARG(shares[p], "NULL share array");
+    std::lock_guard<std::recursive_mutex> g(d->mu);
+    CHK(set_device(d));
+    if (n == 0) {
+        match_from(Partial{}, false, 0, out);
+        return 0;
+    }
+    const size_t bytes = (size_t)n * kRot * 2 * (parts + 1);
+    if (d->hooks.upload == 1 || d->hooks.upload == 2 || bytes < kUploadTuneMin)  // test hook, or small: one path
+        return (d->hooks.upload == 1 ? resolver_host_pinned : resolver_host_runtime)(d, shares, parts, denoms, n,
+                                                                                      index_base, out);
+    UploadTune &u = d->upload_tune;
+    const int path = u.pick();
+    const auto t0 = std::chrono::steady_clock::now();
+    int rc = path == 0 ? resolver_host_pinned(d, shares, parts, denoms, n, index_base, out)
+                       : resolver_host_runtime(d, shares, parts, denoms, n, index_base, out);
+    if (rc == IRIS_E_NOMEM && path == 0 && d->upin_cap < kUploadSlot) {  // no pinned slots: the runtime's copy
+        u.no_pinned = true;
+        return resolver_host_runtime(d, shares, parts, denoms, n, index_base, out);
+    }
+    CHK(rc);
+    u.record(path, (double)bytes / std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
     return 0;
 }
 

@@ -548,6 +548,46 @@ def test_resolver_fused_matches_oracle(device, golden):
     assert z.index == 2**64 - 1 and z.distance == np.inf
 
 
+@pytest.mark.parametrize("path", ["pinned", "runtime", "tuned"])
+def test_resolver_host_chunks(device, hooked_device, path):
+    """The host-array form across several chunks (pinned slots: 3 parts + denominators, 270 592
+    records per 64-MB slot; the runtime's copy: 1M-record chunks), each path pinned by IRIS_UPLOAD
+    and the default that picks by measured rate: 700 001 records, the best distance planted in
+    the last chunk, then (equal) also in the first, so the chunks' winners merge to the lower
+    index; and a 2-part call on garbage shares (ties at distance 0)."""
+    dev = device if path == "tuned" else hooked_device(IRIS_UPLOAD=path)
+    rng = np.random.default_rng(77)
+    n = 700_001
+    den = rng.integers(1000, 12801, (n, ROT)).astype(np.int64)
+    # shares of realistic dot products: uneq within [3/8, 1/2] of den (distances >= 0.375), the
+    # encoded dot den - 2 uneq split into 3 uniform additive shares (src/encoded_bits.rs:23-38)
+    uneq = den // 2 - ((den // 8) * rng.random((n, ROT))).astype(np.int64)
+    total = (den - 2 * uneq) % 2**16
+    parts = [rng.integers(0, 2**16, (n, ROT), dtype=np.uint16) for _ in range(2)]
+    parts.append(((total - parts[0] - parts[1]) % 2**16).astype(np.uint16))
+    den = den.astype(np.uint16)
+
+    def plant(i, u):  # distance u / 6000 at rotation 4 of record i
+        den[i, 4] = 6000
+        parts[2][i, 4] = ((6000 - 2 * u) - int(parts[0][i, 4]) - int(parts[1][i, 4])) % 2**16
+    plant(n - 3, 60)
+    want = oc.resolver_combine(np.stack(parts), den)
+    best, idx = oc.argmin(want)
+    assert idx == n - 3
+    m = ih.resolver_search(parts, den, index_base=7, device=dev)
+    assert m.index == 7 + idx and bits_eq(m.distance, best)
+    plant(12, 60)  # the same distance in the first chunk: the lower index wins
+    want = oc.resolver_combine(np.stack(parts), den)
+    best, idx = oc.argmin(want)
+    assert idx == 12
+    m = ih.resolver_search(parts, den, device=dev)
+    assert m.index == 12 and bits_eq(m.distance, best)
+    want2 = oc.resolver_combine(np.stack(parts[:2]), den)
+    best2, idx2 = oc.argmin(want2)
+    m2 = ih.resolver_search(parts[:2], den, device=dev)
+    assert m2.index == idx2 and bits_eq(m2.distance, best2)
+
+
 @pytest.mark.parametrize("offset", [0, 2, 6])
 def test_resolver_device_alignment(device, offset):
     """Device form with arrays at 16-B aligned and misaligned addresses (the kernel's
