@@ -350,7 +350,9 @@ int iris_resolver_search(iris_device_t *dev, const uint16_t *const *shares_devic
 int iris_resolver_search_masks(iris_engine_t *engine, const iris_db_t *masks_db, uint64_t first, uint64_t n,
                                const uint16_t *const *shares_device, uint32_t parts, uint64_t index_base,
                                double *dist_out_device, iris_match_t *out);
-/* Host form: shares[p] and denoms are host arrays (uploaded in chunks). */
+/* Host form: shares[p] and denoms are host arrays, uploaded in chunks -- through the device's pinned
+ * upload slots, overlapped with the kernels, or by the runtime's copy, whichever moved this
+ * device's large host uploads faster lately (as for iris_db_write); blocking, one result. */
 int iris_resolver_search_host(iris_device_t *dev, const uint16_t *const *shares, uint32_t parts,
                               const uint16_t *denoms, uint64_t n, uint64_t index_base, iris_match_t *out);
 
