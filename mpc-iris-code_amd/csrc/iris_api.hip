@@ -1787,21 +1787,22 @@ int iris_resolver_search_masks(iris_engine_t *e, const iris_db_t *db, uint64_t f
 }
 
 // The resolver step over host arrays (the participants' rows as they arrive, src/main.rs:597-621):
-// a chunk's parts and denominators are copied by the helper threads into one pinned upload slot
-// (parallel_copy, non-temporal stores), moved by the copy engine into a device staging slot, and
-// combined + decoded + reduced there (the reduce writes the chunk's winner, its index already
+// the helper threads sum a chunk's parts (the wrapping u16 sum the kernel would take first,
+// src/main.rs:601-605) into one pinned upload slot beside a copy of its denominators -- 124 B per
+// record cross the host link instead of 62 (P + 1) -- the copy engine moves the slot into a device
+// staging slot, and the records are decoded + reduced there (the reduce writes the chunk's winner, its index already
 // offset, into a pinned result slot), while the host fills the other slot with the next chunk; the
 // call waits once, at the end, and merges the chunks' winners in chunk order.  The runtime's own
 // copy of a pageable source ran at 29-30 GB/s for some caller arrays and 53-55 GB/s for others
-// (profiles/r04_host_upload.txt, r06am_host_resolver.txt), so, as for large database writes, the
-// call takes whichever of the two was faster lately (the device's UploadTune, shared with them).
+// (profiles/r04_host_upload.txt, r06am_host_resolver.txt), so, as large database writes do, the
+// call takes whichever of the two forms was faster lately (a tuner of its own, resolver_tune).
 static int resolver_host_pinned(iris_device *d, const uint16_t *const *shares, uint32_t parts, const uint16_t *denoms,
                                 uint64_t n, uint64_t index_base, iris_match_t *out) {
     iris_match_t best;
     match_from(Partial{}, false, 0, &best);
     const size_t row = (size_t)kRot * 2;
-    const uint32_t arrays = parts + 1;
-    // records per slot (the parts' rows, then the denominators), a multiple of 64
+    const uint32_t arrays = 2;
+    // records per slot (the parts' summed rows, then the denominators), a multiple of 64
     const uint64_t ch = std::min<uint64_t>(n, std::max<uint64_t>(64, kUploadSlot / (arrays * row) / 64 * 64));
     const uint64_t chunks = (n + ch - 1) / ch;
     const size_t slot = (size_t)ch * arrays * row;
@@ -1821,21 +1822,21 @@ static int resolver_host_pinned(iris_device *d, const uint16_t *const *shares, u
             break;
         }
         char *pin = (char *)d->upin[b];
-        for (uint32_t p = 0; p < arrays; ++p)
-            parallel_copy(pin + (size_t)p * m * row, (const char *)((p < parts ? shares[p] : denoms) + a * kRot), m * row,
-                          d->ordinal);
+        const uint16_t *src[8];
+        for (uint32_t p = 0; p < parts; ++p) src[p] = shares[p] + a * kRot;
+        parallel_sum_u16((uint16_t *)pin, src, (int)parts, m * kRot, d->ordinal);
+        parallel_copy(pin + m * row, (const char *)(denoms + a * kRot), m * row, d->ordinal);
         char *stage = (char *)d->staging.p + (size_t)b * slot;
         if (hipMemcpyAsync(stage, pin, (size_t)arrays * m * row, hipMemcpyHostToDevice, d->stream) != hipSuccess ||
             hipEventRecord(d->upin_ev[b], d->stream) != hipSuccess) {
             rc = fail(IRIS_E_HIP, "hipMemcpyAsync upload");
             break;
         }
-        const uint16_t *dev_sh[8];
-        for (uint32_t p = 0; p < parts; ++p) dev_sh[p] = (const uint16_t *)(stage + (size_t)p * m * row);
-        const uint16_t *dden = (const uint16_t *)(stage + (size_t)parts * m * row);
+        const uint16_t *dsum = (const uint16_t *)stage;
+        const uint16_t *dden = (const uint16_t *)(stage + m * row);
         const uint32_t np = resolver_partials(m);
         rc = timed(d, "resolver", m, [&] {
-            return launch_resolver(d->stream, dev_sh, parts, dden, m, nullptr, (Partial *)d->partials.p);
+            return launch_resolver(d->stream, &dsum, 1, dden, m, nullptr, (Partial *)d->partials.p);
         });
         // the chunk's winner, its index offset to the call's records, into result slot c
         if (rc == 0)
@@ -1898,7 +1899,7 @@ int iris_resolver_search_host(iris_device_t *d, const uint16_t *const *shares, u
     if (d->hooks.upload == 1 || d->hooks.upload == 2 || bytes < kUploadTuneMin)  // test hook, or small: one path
         return (d->hooks.upload == 1 ? resolver_host_pinned : resolver_host_runtime)(d, shares, parts, denoms, n,
                                                                                       index_base, out);
-    UploadTune &u = d->upload_tune;
+    UploadTune &u = d->resolver_tune;
     const int path = u.pick();
     const auto t0 = std::chrono::steady_clock::now();
     int rc = path == 0 ? resolver_host_pinned(d, shares, parts, denoms, n, index_base, out)

@@ -74,17 +74,19 @@ struct UploadTune {
     uint32_t n[2] = {0, 0};
     uint64_t writes = 0;
     bool no_pinned = false;  // the slots' pinned buffers could not be allocated
+    // each path is taken twice before the two are compared: its first use pays one-time setup (the
+    // pinned slots' allocation, ~ms) and is not counted
     int pick() {
         const uint64_t w = writes++;
         if (no_pinned) return 1;
-        if (n[0] == 0) return 0;
-        if (n[1] == 0) return 1;
+        if (n[0] < 2) return 0;
+        if (n[1] < 2) return 1;
         const int best = gbps[0] >= gbps[1] ? 0 : 1;
         return w % 16 == 15 ? best ^ 1 : best;
     }
     void record(int p, double rate) {
-        gbps[p] = n[p] == 0 ? rate : 0.75 * gbps[p] + 0.25 * rate;
-        ++n[p];
+        if (n[p]++ == 0) return;
+        gbps[p] = n[p] == 2 ? rate : 0.75 * gbps[p] + 0.25 * rate;
     }
 };
 
@@ -138,6 +140,7 @@ struct iris_device {
     size_t upin_cap = 0;
     hipEvent_t upin_ev[kUploadRing] = {};
     UploadTune upload_tune;
+    UploadTune resolver_tune;  // the same choice for iris_resolver_search_host (its pinned path sums the parts)
     // recorded on the device stream before every read-ahead launch and waited for by the side
     // stream: the launch follows whatever the device stream holds (the engine's query build,
     // writes to the database)

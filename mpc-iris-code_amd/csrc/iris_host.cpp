@@ -300,6 +300,28 @@ __attribute__((target("avx512f"))) void copy_nt_avx512(char *dst, const char *sr
     _mm_sfence();  // the streamed lines are globally visible before this thread reports its part done
 }
 
+// dst[i] = src[0][i] + ... + src[k-1][i] (mod 2^16), dst written with non-temporal 64-B stores from its
+// first 64-B boundary on (the sources may have any alignment)
+__attribute__((target("avx512bw"))) void sum_u16_avx512(uint16_t *dst, const uint16_t *const *src, int k, size_t n) {
+    auto scalar = [&](size_t a, size_t b) {
+        for (size_t i = a; i < b; ++i) {
+            uint16_t v = src[0][i];
+            for (int j = 1; j < k; ++j) v = (uint16_t)(v + src[j][i]);
+            dst[i] = v;
+        }
+    };
+    size_t i = std::min<size_t>(n, ((64 - ((uintptr_t)dst & 63)) & 63) / 2);
+    if ((uintptr_t)dst & 1) i = n;  // not even u16-aligned: no vector stores
+    scalar(0, i);
+    for (; i + 32 <= n; i += 32) {
+        __m512i v = _mm512_loadu_si512(src[0] + i);
+        for (int j = 1; j < k; ++j) v = _mm512_add_epi16(v, _mm512_loadu_si512(src[j] + i));
+        _mm512_stream_si512((__m512i *)(dst + i), v);
+    }
+    scalar(i, n);
+    _mm_sfence();
+}
+
 void expand_scalar(uint16_t *out, const uint8_t *pk, const uint16_t *esc, size_t n) {
     for (size_t i = 0; i < n; ++i) {
         const uint8_t *p = pk + 32 * i;
@@ -333,6 +355,18 @@ void copy_nt(char *dst, const char *src, size_t n) {
         memcpy(dst, src, n);
 }
 
+void sum_u16(uint16_t *dst, const uint16_t *const *src, int k, size_t n) {
+    if (kHaveAvx512) {
+        sum_u16_avx512(dst, src, k, n);
+        return;
+    }
+    for (size_t i = 0; i < n; ++i) {
+        uint16_t v = src[0][i];
+        for (int j = 1; j < k; ++j) v = (uint16_t)(v + src[j][i]);
+        dst[i] = v;
+    }
+}
+
 namespace {
 
 class CopyPool {
@@ -346,11 +380,15 @@ class CopyPool {
     // src != nullptr: memcpy; else pread from fd at file offset off.  Returns false if a read failed
     // (an I/O error, or the file ended before `bytes`).  esc != nullptr: expand `bytes` packed
     // MasksEngine records at src (escape rows at esc) into dst instead.
-    bool run(char *dst, const char *src, size_t bytes, int fd = -1, off_t off = 0, const uint16_t *esc = nullptr) {
+    // sums != nullptr: dst = the wrapping u16 sum of nsum arrays of `bytes` elements (sum_u16)
+    bool run(char *dst, const char *src, size_t bytes, int fd = -1, off_t off = 0, const uint16_t *esc = nullptr,
+             const uint16_t *const *sums = nullptr, int nsum = 0) {
         std::lock_guard<std::mutex> one(run_mu_);  // one job at a time (devices may call concurrently)
         dst_ = dst;
         src_ = src;
         esc_ = esc;
+        nsum_ = sums ? nsum : 0;
+        for (int j = 0; j < nsum_; ++j) sums_[j] = sums[j];
         bytes_ = bytes;
         fd_ = fd;
         off_ = off;
@@ -384,6 +422,16 @@ class CopyPool {
     }
     void part(int id) {
         const int np = nparts_;
+        if (nsum_) {  // bytes_ u16 elements, parts of whole 64-B runs
+            const size_t per = ((bytes_ + np - 1) / np + 31) & ~(size_t)31;
+            const size_t a = std::min(bytes_, (size_t)id * per), b = std::min(bytes_, a + per);
+            if (a < b) {
+                const uint16_t *srcs[kMaxSum];
+                for (int j = 0; j < nsum_; ++j) srcs[j] = sums_[j] + a;
+                sum_u16((uint16_t *)dst_ + a, srcs, nsum_, b - a);
+            }
+            return;
+        }
         if (esc_) {  // bytes_ records, split on record boundaries
             const size_t per = (bytes_ + np - 1) / np;
             const size_t a = std::min(bytes_, (size_t)id * per), b = std::min(bytes_, a + per);
@@ -437,6 +485,9 @@ class CopyPool {
     char *dst_ = nullptr;
     const char *src_ = nullptr;
     const uint16_t *esc_ = nullptr;
+    static constexpr int kMaxSum = 8;
+    const uint16_t *sums_[kMaxSum] = {};
+    int nsum_ = 0;
     size_t bytes_ = 0;
     int fd_ = -1;
     off_t off_ = 0;
@@ -585,6 +636,15 @@ void expand_packed_rows(uint16_t *out, const uint8_t *pk, const uint16_t *esc, s
         expand_avx512(out, pk, esc, n);
     else
         expand_scalar(out, pk, esc, n);
+}
+
+void parallel_sum_u16(uint16_t *dst, const uint16_t *const *src, int k, size_t n, int lane) {
+    if (k < 1 || k > 8) return;
+    if (n * 2 * (size_t)k < kParallelCopyMin) {
+        sum_u16(dst, src, k, n);
+        return;
+    }
+    (void)pool_of(lane)->run((char *)dst, nullptr, n, -1, 0, nullptr, src, k);
 }
 
 void parallel_expand(uint16_t *out, const uint8_t *pk, const uint16_t *esc, size_t n, int lane) {

@@ -330,5 +330,8 @@ void parallel_expand(uint16_t *out, const uint8_t *pk, const uint16_t *esc, size
 void expand_packed_rows(uint16_t *out, const uint8_t *pk, const uint16_t *esc, size_t n);  // one thread
 // memcpy whose destination lines are written with non-temporal stores (AVX-512, >= 4 KB); one thread
 void copy_nt(char *dst, const char *src, size_t n);
+// dst[i] = src[0][i] + ... + src[k-1][i] mod 2^16 (k <= 8): one thread / the device's helper pool
+void sum_u16(uint16_t *dst, const uint16_t *const *src, int k, size_t n);
+void parallel_sum_u16(uint16_t *dst, const uint16_t *const *src, int k, size_t n, int lane = 0);
 
 }  // namespace iris

@@ -3,7 +3,8 @@
 // expand_packed_rows / parallel_expand: the AVX-512 form with its non-temporal 32-record blocks,
 // escaped rows, every alignment of the caller's array) against a scalar restatement, and the
 // helper pool's parallel_copy under concurrent callers (parts claimed by whoever is free), and
-// copy_nt (non-temporal stores from dst's first 64-B boundary) at every source / destination offset.
+// copy_nt (non-temporal stores from dst's first 64-B boundary) at every source / destination offset,
+// and sum_u16 / parallel_sum_u16 (the resolver's wrapping share sums) against a scalar sum.
 // These are library internals, declared here as the library defines them (iris_internal.hpp).
 #include <atomic>
 #include <cstdio>
@@ -17,6 +18,8 @@ void parallel_copy(void *dst, const void *src, size_t bytes, int lane);
 void parallel_expand(uint16_t *out, const uint8_t *pk, const uint16_t *esc, size_t n, int lane);
 void expand_packed_rows(uint16_t *out, const uint8_t *pk, const uint16_t *esc, size_t n);
 void copy_nt(char *dst, const char *src, size_t n);
+void sum_u16(uint16_t *dst, const uint16_t *const *src, int k, size_t n);
+void parallel_sum_u16(uint16_t *dst, const uint16_t *const *src, int k, size_t n, int lane);
 }  // namespace iris
 
 static int failures = 0;
@@ -86,6 +89,32 @@ int main() {
             }
         }
     }
+    // sum_u16: 1..8 sources at assorted offsets, every u16 offset of the destination within a line
+    {
+        const size_t maxn = 5000;
+        std::vector<std::vector<uint16_t>> srcv(8, std::vector<uint16_t>(maxn + 64));
+        for (auto &v : srcv)
+            for (auto &x : v) x = (uint16_t)r();
+        for (int k = 1; k <= 8; ++k)
+            for (size_t n : {0, 1, 31, 32, 33, 95, 1000, 4999}) {
+                const uint16_t *src[8];
+                for (int j = 0; j < k; ++j) src[j] = srcv[j].data() + (j * 7) % 40;
+                std::vector<uint16_t> want(n);
+                for (size_t i = 0; i < n; ++i) {
+                    uint32_t v = 0;
+                    for (int j = 0; j < k; ++j) v += src[j][i];
+                    want[i] = (uint16_t)v;
+                }
+                for (int dof = 0; dof < 32; dof += 3) {
+                    std::vector<uint16_t> buf(n + 96, 0x7777);
+                    uint16_t *dst = buf.data() + 32 + dof - (((uintptr_t)(buf.data() + 32) & 63) / 2);
+                    iris::sum_u16(dst, src, k, n);
+                    CHECK(std::memcmp(dst, want.data(), n * 2) == 0);
+                    for (uint16_t *q = buf.data(); q < dst; ++q) CHECK(*q == 0x7777);
+                    for (uint16_t *q = dst + n; q < buf.data() + buf.size(); ++q) CHECK(*q == 0x7777);
+                }
+            }
+    }
     // the helper pool: a participant-sized chunk (20 000 records) and a window, from 4 threads at once
     {
         std::vector<std::thread> ts;
@@ -105,6 +134,17 @@ int main() {
                     for (auto &c : a) c = (char)rr();
                     iris::parallel_copy(b.data(), a.data(), a.size(), t % 2);
                     if (a != b) ++bad;
+                    // three share arrays of a chunk summed by the pool (the resolver's host form)
+                    const size_t ne = 1 + rr() % (2 << 20);
+                    std::vector<uint16_t> s0(ne), s1(ne), s2(ne), sum(ne + 1, 0);
+                    for (size_t i = 0; i < ne; ++i) s0[i] = (uint16_t)rr(), s1[i] = (uint16_t)rr(), s2[i] = (uint16_t)rr();
+                    const uint16_t *ss[3] = {s0.data(), s1.data(), s2.data()};
+                    iris::parallel_sum_u16(sum.data() + (it % 2), ss, 3, ne, t % 2);
+                    for (size_t i = 0; i < ne; ++i)
+                        if (sum[i + (it % 2)] != (uint16_t)(s0[i] + s1[i] + s2[i])) {
+                            ++bad;
+                            break;
+                        }
                 }
             });
         for (auto &t : ts) t.join();

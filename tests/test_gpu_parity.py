@@ -890,9 +890,10 @@ def test_large_write_paths(hooked_device, path):
 
 
 def test_upload_path_tuning(hooked_device):
-    """Without a pinned path, writes of 8 MB and more measure both paths on their first two writes and
-    then take the faster one, re-measuring the other every 16th write; iris_config reports the rates.
-    Every write stores the same records whichever path it took."""
+    """Without a pinned path, writes of 8 MB and more take each path twice (the first use of each,
+    which pays its one-time setup, is not counted), then the faster one, re-measuring the other every
+    16th write; iris_config reports the rates.  Every write stores the same records whichever path it
+    took."""
     dev = hooked_device()
     rng = np.random.default_rng(12)
     masks = rng.integers(0, 2**64, (10_000, 200), dtype=np.uint64)  # 16 MB per write
