@@ -58,7 +58,7 @@ VALU_OPS_PER_TEMPLATE = 400 * 31 * 4   # words x rotations x (and, bitop3, 2x bc
 ROT = 31
 SEED = 20251015
 GPU_WORKLOADS = ("search", "masks", "shares", "batch")
-AUX_WORKLOADS = ("resolver", "host-resolver", "resolve-masks", "prepare", "load", "host-shares", "host-masks", "criterion")
+AUX_WORKLOADS = ("resolver", "host-resolver", "resolve-masks", "host-resolve-masks", "prepare", "load", "host-shares", "host-masks", "criterion")
 
 
 def parse():
@@ -308,7 +308,7 @@ def cpu_baseline(args, reserve=0):
             value *= ROT
         sample = (f"{passes} passes of DistanceEngine::batch_process (dot_u16, src/lib.rs:42-52, "
                   f"src/arch/generic.rs:11-16) over {n} shares, per-record rate extrapolated")
-    elif wl in ("resolver", "host-resolver", "resolve-masks"):
+    elif wl in ("resolver", "host-resolver", "resolve-masks", "host-resolve-masks"):
         n = 2_000_000
         rng = np.random.default_rng(SEED)
         shares = rng.integers(0, 65536, (args.parties, n, ROT), dtype=np.uint16)
@@ -326,7 +326,7 @@ def cpu_baseline(args, reserve=0):
         value, unit = n * passes / t, "records/s"
         sample = (f"{passes} passes of the share sum + decode (parallel over entries, as the reference's rayon "
                   f"into_par_iter, src/main.rs:597-612) + sequential argmin (src/main.rs:616-621) over {n} entries")
-        if wl == "resolve-masks":
+        if wl in ("resolve-masks", "host-resolve-masks"):
             sample += " (the masks engine's denominators are not included)"
     elif wl == "prepare":
         n = 2000 * threads
@@ -648,24 +648,29 @@ def run_aux(args, dev):
         workload = (f"resolver: {P} participants' [u16;31] outputs + denominators -> min/argmin (src/main.rs:597-621)"
                     + (", host arrays: pinned-slot uploads overlapped with the kernels (PCIe-inclusive)"
                        if args.workload == "host-resolver" else ""))
-    elif args.workload == "resolve-masks":
+    elif args.workload in ("resolve-masks", "host-resolve-masks"):
         n = args.n_per_gpu
         shares = rng.integers(0, 65536, (P, n, ROT), dtype=np.uint16)
-        for j in range(P):
-            ptrs.append(dev.alloc(n * ROT * 2))
-            dev.h2d(ptrs[j], shares[j])
+        host_form = args.workload == "host-resolve-masks"
+        if not host_form:
+            for j in range(P):
+                ptrs.append(dev.alloc(n * ROT * 2))
+                dev.h2d(ptrs[j], shares[j])
         mdb = ih.Database(dev, ih.KIND_MASKS, n)
         mdb.generate(n, SEED)
         qmask = gen_records(dev, ih.KIND_MASKS, 1, SEED + 1)[0]
         eng = ih.MasksEngine(dev, qmask)
+        host_parts = list(shares)
 
-        def step():
-            return eng.resolve(mdb, ptrs[:P])
+        def step():  # host form: the rows in host memory as they arrive, summed there, the sum uploaded
+            return eng.resolve(mdb, host_parts if host_form else ptrs[:P])
 
         kname, unit = "masks_resolve", "records/s"
         rec_bytes = 1600 + P * ROT * 2  # the mask + P share rows; no denominators in memory
         workload = (f"resolver step with on-the-fly denominators: masks DB + {P} participants' [u16;31] "
-                    "outputs -> min/argmin (src/main.rs:510-519 + 597-621)")
+                    "outputs -> min/argmin (src/main.rs:510-519 + 597-621)"
+                    + (", the outputs in host memory: summed on the host, the sum uploaded (PCIe-inclusive)"
+                       if host_form else ""))
     elif args.workload == "load":
         n = min(args.n_per_gpu, 1_000_000)  # a 3.2 GB file
         fpath = pathlib.Path(tempfile.gettempdir()) / f"iris_bench_{os.getpid()}.templates"
@@ -901,13 +906,13 @@ def run_aux(args, dev):
             extra["host_link"] = {"row_bytes_per_record": row_bytes, "achieved_GBps": link,
                                   "measured_GBps": 53.1, "frac": link / 53.1,
                                   "source": "tools/ubench_d2h.hip (profiles/r06h_ubench_d2h.txt)"}
-    if args.workload == "resolve-masks":  # denominators from the (separately checked) masks engine
+    if args.workload in ("resolve-masks", "host-resolve-masks"):  # denominators from the (separately checked) masks engine
         denoms = np.empty((n, ROT), np.uint16)
         eng.batch_process(denoms, mdb)
         sample = np.random.default_rng(1).choice(n, 64, replace=False)
         recs = np.stack([mdb.read(int(i), 1)[0] for i in sample])
         assert (denoms[sample] == check_masks_rows(qmask, recs)).all()
-    if args.workload in ("resolver", "host-resolver", "resolve-masks"):
+    if args.workload in ("resolver", "host-resolver", "resolve-masks", "host-resolve-masks"):
         best, idx = check_resolver(shares, denoms)
         ok = m.index == idx and np.float64(m.distance).view(np.uint64) == np.float64(best).view(np.uint64)
         check = {"expected_index": int(idx), "found_index": int(m.index), "ok": bool(ok)}
@@ -974,6 +979,7 @@ def run_aux(args, dev):
         "metric": {"resolver": "resolver records/s (share sum + decode + argmin)",
                    "host-resolver": "resolver records/s over host arrays (share sum + decode + argmin, PCIe-inclusive)",
                    "resolve-masks": "resolver records/s (masks engine + share sum + decode + argmin, fused)",
+                   "host-resolve-masks": "resolver records/s (masks engine + decode + argmin fused; shares from host memory, PCIe-inclusive)",
                    "prepare": "templates prepared/s (shares + masks)",
                    "load": "templates loaded/s (file -> resident database, PCIe-inclusive)",
                    "host-shares": "share records/s through batch_process over host slices (PCIe-inclusive)",
@@ -986,6 +992,7 @@ def run_aux(args, dev):
         "dtype": {"resolver": "u16 (wrapping share sums) -> u32 cross-multiplied fractions",
                   "host-resolver": "u16 (wrapping share sums) -> u32 cross-multiplied fractions",
                   "resolve-masks": "fp4 e2m1 MFMA -> f32 denominators, u16 share sums",
+                  "host-resolve-masks": "fp4 e2m1 MFMA -> f32 denominators, u16 share sums",
                   "prepare": "u32 (ChaCha keystream) -> u16 shares",
                   "load": "u8 (record bytes)",
                   "host-shares": "i8 MFMA -> i32 (u16 shares as biased byte planes)",
@@ -1007,7 +1014,8 @@ def run_aux(args, dev):
         "file_GBps": (n * 3200 * args.steps / elapsed / 1e9) if args.workload == "load" else None,
         "host_input_GBps": (n * rec_bytes * args.steps / elapsed / 1e9)
         if (args.workload in ("host-shares", "host-masks") and not args.attached
-            and not (args.mmap and not args.no_auto_resident)) or args.workload == "host-resolver" else None,
+            and not (args.mmap and not args.no_auto_resident)) or args.workload == "host-resolver"
+        else (n * P * ROT * 2 * args.steps / elapsed / 1e9) if args.workload == "host-resolve-masks" else None,
         "cpu_baseline": cpu,
         "check": check,
         **extra,

@@ -270,6 +270,16 @@ extern "C" {
         dist_out_device: *mut f64,
         out: *mut IrisMatch,
     ) -> c_int;
+    pub fn iris_resolver_search_masks_host(
+        engine: *mut IrisEngine,
+        masks_db: *const IrisDb,
+        first: u64,
+        n: u64,
+        shares: *const *const u16,
+        parts: u32,
+        index_base: u64,
+        out: *mut IrisMatch,
+    ) -> c_int;
     pub fn iris_resolver_search_host(
         dev: *mut IrisDevice,
         shares: *const *const u16,

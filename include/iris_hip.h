@@ -350,6 +350,14 @@ int iris_resolver_search(iris_device_t *dev, const uint16_t *const *shares_devic
 int iris_resolver_search_masks(iris_engine_t *engine, const iris_db_t *masks_db, uint64_t first, uint64_t n,
                                const uint16_t *const *shares_device, uint32_t parts, uint64_t index_base,
                                double *dist_out_device, iris_match_t *out);
+/* iris_resolver_search_masks with the participants' outputs in host memory (src/main.rs:510-519 +
+ * 597-621: the rows as they arrive over the network; the reference's resolver computes the masks
+ * denominators itself, here fused): shares[p] are host arrays of n x 31 u16, row i = record
+ * first + i.  The parts are summed (wrapping u16) on the host while the previous chunk's sum is
+ * copied and searched; blocking, one result; indices are i + index_base. */
+int iris_resolver_search_masks_host(iris_engine_t *engine, const iris_db_t *masks_db, uint64_t first, uint64_t n,
+                                    const uint16_t *const *shares, uint32_t parts, uint64_t index_base,
+                                    iris_match_t *out);
 /* Host form: shares[p] and denoms are host arrays, uploaded in chunks -- through the device's pinned
  * upload slots, overlapped with the kernels, or by the runtime's copy, whichever moved this
  * device's large host uploads faster lately (as for iris_db_write); blocking, one result. */

@@ -488,6 +488,20 @@ public:
                                          index_base, nullptr, &m));
         return m;
     }
+    // The same with the participants' outputs in host memory (the rows as they arrive): summed on
+    // the host, the sum uploaded (iris_resolver_search_masks_host).
+    Match resolve_host(const Database &db, const std::vector<const std::vector<Rotations> *> &shares, uint64_t first,
+                       uint64_t index_base = 0) const {
+        std::vector<const uint16_t *> p;
+        const uint64_t n = shares.empty() ? 0 : shares[0]->size();
+        for (const auto *s : shares) {
+            if (s->size() != n) throw Error(IRIS_E_ARG, "share arrays of different lengths");
+            p.push_back(s->empty() ? nullptr : (*s)[0].data());
+        }
+        Match m{};
+        check(iris_resolver_search_masks_host(h_, db.handle(), first, n, p.data(), (uint32_t)p.size(), index_base, &m));
+        return m;
+    }
 };
 
 // An enqueued search (TemplateEngine::search_async): wait() once for its Match;

@@ -1786,6 +1786,97 @@ int iris_resolver_search_masks(iris_engine_t *e, const iris_db_t *db, uint64_t f
     return 0;
 }
 
+// The resolver step from host share arrays and the resident masks database (src/main.rs:510-519 +
+// 597-621, the shares as they arrive from the participants): the helper threads sum each chunk's
+// parts into a pinned upload slot (62 B per record over the host link), the copy engine moves it to a
+// device staging slot, and the fused masks + resolve kernel computes the denominators on the fly
+// against the summed rows; each chunk's winner is reduced into its own pinned result slot, the host
+// fills the next slot meanwhile, and the call waits once.  LANES databases run chunk by chunk through
+// iris_resolver_search_masks.
+int iris_resolver_search_masks_host(iris_engine_t *e, const iris_db_t *db, uint64_t first, uint64_t n,
+                                    const uint16_t *const *shares, uint32_t parts, uint64_t index_base,
+                                    iris_match_t *out) {
+    IRIS_KEEP_DEVICE();
+    ARG(e && db && out, "NULL argument");
+    ARG(parts >= 1 && parts <= 8, "parts must be 1..8");
+    ARG(e->kind == IRIS_KIND_MASKS && db->k.kind == IRIS_KIND_MASKS, "needs a masks engine and a masks database");
+    ARG(e->dev == db->dev, "engine and database live on different devices");
+    ARG(n == 0 || shares, "NULL argument");
+    for (uint32_t p = 0; n && p < parts; ++p) ARG(shares[p], "NULL share array");
+    iris_device *d = e->dev;
+    std::lock_guard<std::recursive_mutex> g(d->mu);
+    CHK(set_device(d));
+    CHK(range_ok(db, first, n));
+    iris_match_t best;
+    match_from(Partial{}, false, 0, &best);
+    if (n == 0) {
+        *out = best;
+        return 0;
+    }
+    const size_t row = (size_t)kRot * 2;
+    const uint64_t ch = std::min<uint64_t>(n, kUploadSlot / row / 64 * 64);
+    const uint64_t chunks = (n + ch - 1) / ch;
+    CHK(ensure_upin(d));
+    CHK(ensure(d, d->staging, kUploadSlots * (size_t)ch * row));
+    const bool tiles = db->k.layout == IRIS_LAYOUT_TILES;
+    uint32_t np_max = 1;
+    for (uint64_t c = 0; tiles && c < chunks; ++c)
+        np_max = std::max(np_max, masks_resolve_partials(d->hooks, LaunchRange{first + c * ch, std::min(ch, n - c * ch)}));
+    if (tiles) {
+        CHK(ensure(d, d->partials, (size_t)np_max * sizeof(Partial)));
+        CHK(ensure_host_result(d, (size_t)chunks * sizeof(Partial)));
+    }
+    Partial *res = (Partial *)d->host_result;
+    int rc = 0;
+    for (uint64_t c = 0; c < chunks && rc == 0; ++c) {
+        const uint64_t a = c * ch, m = std::min<uint64_t>(ch, n - a);
+        const int b = (int)(c % kUploadSlots);
+        // pinned slot b was last read by the copy of chunk c - kUploadSlots
+        if (c >= (uint64_t)kUploadSlots && hipEventSynchronize(d->upin_ev[b]) != hipSuccess) {
+            rc = fail(IRIS_E_HIP, "hipEventSynchronize");
+            break;
+        }
+        const uint16_t *src[8];
+        for (uint32_t p = 0; p < parts; ++p) src[p] = shares[p] + a * kRot;
+        parallel_sum_u16((uint16_t *)d->upin[b], src, (int)parts, m * kRot, d->ordinal);
+        char *stage = (char *)d->staging.p + (size_t)b * ch * row;
+        if (hipMemcpyAsync(stage, d->upin[b], m * row, hipMemcpyHostToDevice, d->stream) != hipSuccess ||
+            hipEventRecord(d->upin_ev[b], d->stream) != hipSuccess) {
+            rc = fail(IRIS_E_HIP, "hipMemcpyAsync upload");
+            break;
+        }
+        const uint16_t *dsum = (const uint16_t *)stage;
+        if (!tiles) {  // the summed rows through the LANES form, one chunk at a time
+            iris_match_t cm;
+            rc = iris_resolver_search_masks(e, db, first + a, m, &dsum, 1, index_base + a, nullptr, &cm);
+            if (rc == 0) {
+                iris_match_t pair[2] = {best, cm};
+                rc = iris_match_merge(pair, 2, &best);
+            }
+            continue;
+        }
+        const LaunchRange r{first + a, m};
+        const uint32_t np = masks_resolve_partials(d->hooks, r);
+        rc = timed(d, "masks_resolve", m, [&] {
+            return launch_masks_resolve(d->hooks, d->stream, db->data, e->qfrag, r, &dsum, 1, nullptr,
+                                        (Partial *)d->partials.p);
+        });
+        // the chunk's winner, its index offset to the call's records, into result slot c
+        if (rc == 0)
+            rc = timed(d, "reduce", np, [&] { return launch_reduce(d->stream, (Partial *)d->partials.p, np, res + c, a); });
+    }
+    const int rs = sync(d);  // the pinned slots are free again and every chunk's winner is in place
+    CHK(rc);
+    CHK(rs);
+    for (uint64_t c = 0; tiles && c < chunks; ++c) {
+        iris_match_t pair[2] = {best, {}};
+        match_from(res[c], true, index_base, &pair[1]);
+        CHK(iris_match_merge(pair, 2, &best));
+    }
+    *out = best;
+    return 0;
+}
+
 // The resolver step over host arrays (the participants' rows as they arrive, src/main.rs:597-621):
 // the helper threads sum a chunk's parts (the wrapping u16 sum the kernel would take first,
 // src/main.rs:601-605) into one pinned upload slot beside a copy of its denominators -- 124 B per

@@ -146,6 +146,8 @@ def load_library(path=None):
             "iris_templates_write_json": ([ctypes.c_char_p, P, u64], ctypes.c_int),
             "iris_resolver_search_masks": ([P, P, u64, u64, P, ctypes.c_uint32, u64, P, ctypes.POINTER(Match)],
                                            ctypes.c_int),
+            "iris_resolver_search_masks_host": ([P, P, u64, u64, P, ctypes.c_uint32, u64, ctypes.POINTER(Match)],
+                                                ctypes.c_int),
             "iris_prepare_shares": ([P, u64, u64, u64, P, u64, ctypes.c_uint32, ctypes.c_uint32, P, P], ctypes.c_int),
             "iris_masks_engine_new": ([P, P, PP], ctypes.c_int),
             "iris_distance_engine_new": ([P, P, PP], ctypes.c_int),
@@ -225,7 +227,7 @@ def exported_symbols():
         "iris_resolver_search_host", "iris_dot_bool_batch", "iris_dot_u16_batch", "iris_bits_rotated", "iris_encoded_rotated", "iris_encode",
         "iris_decode_distance", "iris_match_merge", "iris_db_load_file", "iris_db_save_file",
         "iris_templates_read_json", "iris_templates_write_json", "iris_prepare_shares",
-        "iris_db_truncate", "iris_memcpy_h2d", "iris_resolver_search_masks",
+        "iris_db_truncate", "iris_memcpy_h2d", "iris_resolver_search_masks", "iris_resolver_search_masks_host",
         "iris_query_table_sizes", "iris_engine_query_tables", "iris_host_query_tables", "iris_device_memory",
         "iris_template_search_async", "iris_pending_wait",
         "iris_db_attach_host", "iris_db_detach_host",
@@ -848,10 +850,21 @@ class MasksEngine(_Engine):
     def resolve(self, db, shares, first=0, n=None, index_base=0, dist_out_device=None):
         """The resolver step with this engine's denominators computed on the fly
         (src/main.rs:510-519 + 597-621): shares = the participants' [n,31] u16 outputs,
-        host arrays (uploaded here) or device pointers.  -> Match."""
+        host arrays or device pointers.  Host arrays (and no dist_out_device) go through
+        iris_resolver_search_masks_host: summed on the host, the sum uploaded.  -> Match."""
         if n is None:
             n = len(db) - int(first)
         dev = self.device
+        if dist_out_device is None and shares and not any(isinstance(a, int) for a in shares):
+            arrs = [_c(a, np.uint16) for a in shares]
+            for a in arrs:
+                if a.shape != (n, ROTATIONS):
+                    raise IrisError(-1, "shares must be [n, 31] uint16")
+            ptrs = (ctypes.c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
+            m = Match()
+            _check(load_library().iris_resolver_search_masks_host(self.handle, db.handle, int(first), int(n), ptrs,
+                                                                  len(arrs), int(index_base), ctypes.byref(m)))
+            return m
         tmp = []
         try:
             ptrs = []

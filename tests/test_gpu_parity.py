@@ -727,6 +727,54 @@ def test_resolver_masks_fused(device, hooked_device, layout, first, n, tiles_per
     assert ref.index == m.index and ref.rotation == m.rotation
 
 
+@pytest.mark.parametrize("layout_", ["tiles", "lanes"])
+def test_resolver_masks_host_chunks(device, layout_):
+    """MasksEngine.resolve with the participants' outputs as host arrays
+    (iris_resolver_search_masks_host: the parts summed on the host, the sum uploaded, the masks
+    denominators computed on the fly) over 1 100 037 records from record 5 -- two upload chunks of
+    1 082 368 records, the planted winner in the second -- and over a short range, against the oracle
+    and the device-pointer form."""
+    lay = {"tiles": ih.LAYOUT_TILES, "lanes": ih.LAYOUT_LANES}[layout_]
+    n, first = 1_100_037, 5
+    total = first + n + 3
+    masks = np.empty((total, 200), np.uint64)
+    for a in range(0, total, 200_000):  # the generator's templates, masks half
+        masks[a:a + 200_000] = oc.gen_templates(83, a, min(200_000, total - a))[:, 200:]
+    q = masks[first + 1_090_000].copy()
+    rng = np.random.default_rng(3)
+    with ih.Database(device, ih.KIND_MASKS, total, lay) as db, ih.MasksEngine(device, q) as eng:
+        db.append(masks)
+        den = oc.masks_batch(q, masks[first:first + n])
+        parts = [rng.integers(0, 2**16, (n, ROT), dtype=np.uint16) for _ in range(3)]
+        # realistic shares: encoded dots den - 2 uneq, uneq in [3/8, 1/2] of den; one planted near-copy
+        uneq = (den // 2 - ((den // 8) * rng.random((n, ROT))).astype(np.int64)).astype(np.int64)
+        total_dot = (den.astype(np.int64) - 2 * uneq) % 2**16
+        parts[2] = ((total_dot - parts[0] - parts[1]) % 2**16).astype(np.uint16)
+        i = 1_090_000
+        parts[2][i] = ((den[i].astype(np.int64) - 20 - parts[0][i] - parts[1][i]) % 2**16).astype(np.uint16)
+        want = oc.resolver_combine(np.stack(parts), den)
+        best, idx = oc.argmin(want)
+        assert idx == i
+        m = eng.resolve(db, parts, first=first, n=n, index_base=11)
+        assert m.index == 11 + idx and bits_eq(m.distance, best)
+        # a short range through both forms
+        sl = slice(1000, 1000 + 4321)
+        sp = [p[sl] for p in parts]
+        want_s = oc.resolver_combine(np.stack(sp), den[sl])
+        bs, js = oc.argmin(want_s)
+        mh = eng.resolve(db, sp, first=first + 1000, n=4321)
+        ptrs = []
+        try:
+            for p in sp:
+                ptrs.append(device.alloc(p.nbytes))
+                device.h2d(ptrs[-1], np.ascontiguousarray(p))
+            md = eng.resolve(db, ptrs, first=first + 1000, n=4321)
+        finally:
+            for p in ptrs:
+                device.free(p)
+        assert mh.index == md.index == js and bits_eq(mh.distance, bs) and bits_eq(md.distance, bs)
+
+
 def test_empty_ranges(device, layout):
     """Every entry point accepts an empty range (the reference's loops over empty slices)."""
     masks = oc.gen_templates(71, 0, 40)

@@ -20,6 +20,7 @@ bench_args() {
     resolver) echo "--workload resolver --steps 20 --warmup 3" ;;
     resolve-masks) echo "--workload resolve-masks --steps 20 --warmup 3" ;;
     host-resolver) echo "--workload host-resolver --steps 5 --warmup 1" ;;
+    host-resolve-masks) echo "--workload host-resolve-masks --steps 10 --warmup 2" ;;
     prepare) echo "--workload prepare --steps 2 --warmup 1" ;;
     load) echo "--workload load --steps 3 --warmup 1 --no-cpu-baseline" ;;
     host-masks) echo "--workload host-masks --steps 3 --warmup 1" ;;
