@@ -127,6 +127,29 @@ impl MasksEngine {
         })?;
         Ok(match_to_pair(&m))
     }
+
+    /// The same step with the participants' replies still in host memory (`shares[p]` holds the
+    /// n = `shares[p].len()` rows of records [first, first + n)): the library sums the parts on
+    /// the host and uploads only the sum (iris_resolver_search_masks_host).
+    pub fn resolve_host(&self, masks: &Database, first: u64, shares: &[&[[u16; 31]]]) -> Result<(f64, usize)> {
+        let n = shares.first().map_or(0, |s| s.len());
+        assert!(shares.iter().all(|s| s.len() == n), "share arrays of different lengths");
+        let ptrs: Vec<*const u16> = shares.iter().map(|s| s.as_ptr() as *const u16).collect();
+        let mut m = ffi::IrisMatch::default();
+        check(unsafe {
+            ffi::iris_resolver_search_masks_host(
+                self.h.raw,
+                masks.raw(),
+                first,
+                n as u64,
+                ptrs.as_ptr(),
+                ptrs.len() as u32,
+                0,
+                &mut m,
+            )
+        })?;
+        Ok(match_to_pair(&m))
+    }
 }
 
 /// `distances` (src/lib.rs:82-87).
