@@ -252,6 +252,15 @@ std::vector<Case> cases() {
              MasksEngine(q.mask).batch_process(den, masks);
              const Match m = resolver_search(outs, den);
              CHECK(m.index == 33 && m.distance == 0.0 && m.rotation == 4);
+             // the fused step from the host replies and a resident masks database
+             // (iris_resolver_search_masks_host): the same entry
+             {
+                 Device &d0 = Device::default_device();
+                 Database mdb(d0, IRIS_KIND_MASKS, masks.size());
+                 mdb.append(masks);
+                 const Match mh = MasksEngine(q.mask).resolve_host(mdb, {&outs[0], &outs[1], &outs[2]}, 0);
+                 CHECK(mh.index == 33 && mh.distance == 0.0 && mh.rotation == 4);
+             }
              // plaintext search on a device database finds the same entry
              Device &dev = Device::default_device();
              Database tdb(dev, IRIS_KIND_TEMPLATES, db.size());
