@@ -286,6 +286,59 @@ def test_concurrent_walks_share_one_copy(device, tmp_path):
     del recs
 
 
+def test_concurrent_walk_and_resolver_host_forms(device, tmp_path):
+    """A masks walk of a mapped file on one thread while another runs the resolver's host forms
+    (iris_resolver_search_host and iris_resolver_search_masks_host, several upload chunks each) on
+    the same device: they share the device's pinned upload slots, staging and helper pool (the
+    device lock orders them); every result equals the oracle's."""
+    import threading
+    kind, n = ih.KIND_MASKS, 90_001
+    path = tmp_path / "r.masks"
+    host = gen(kind, SEED + 17, n)
+    host.tofile(path)
+    recs = mapped(path, kind, n)
+    rng = np.random.default_rng(9)
+    nr = 600_000  # > one 541k-record slot of summed shares + denominators
+    parts = [rng.integers(0, 2**16, (nr, 31), dtype=np.uint16) for _ in range(3)]
+    den = rng.integers(0, 12801, (nr, 31), dtype=np.uint16)
+    want_r = oc.argmin(oc.resolver_combine(np.stack(parts), den))
+    mq = host[n // 3].copy()
+    sh = [p[:n] for p in parts]
+    want_m = oc.argmin(oc.resolver_combine(np.stack(sh), oc.masks_batch(mq, host)))
+    errors, ok = [], {}
+
+    def walker():
+        try:
+            for w in range(3):
+                eng, want_fn = engine_and_oracle(device, kind, SEED + 30 + w)
+                with eng:
+                    out = walk(eng, recs, chunk=CHUNK)
+                ok[("walk", w)] = bool((out == want_fn(host)).all())
+        except Exception as exc:
+            errors.append(repr(exc))
+
+    def resolver():
+        try:
+            with ih.Database(device, kind, n) as mdb, ih.MasksEngine(device, mq) as me:
+                mdb.append(host)
+                for r in range(3):
+                    m = ih.resolver_search(parts, den, device=device)
+                    ok[("host", r)] = m.index == want_r[1] and np.float64(m.distance) == np.float64(want_r[0])
+                    mm = me.resolve(mdb, sh)
+                    ok[("masks_host", r)] = mm.index == want_m[1] and np.float64(mm.distance) == np.float64(want_m[0])
+        except Exception as exc:
+            errors.append(repr(exc))
+
+    threads = [threading.Thread(target=walker), threading.Thread(target=resolver)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=100)
+    assert not errors, errors
+    assert len(ok) == 9 and all(ok.values()), ok
+    del recs
+
+
 def test_budget_evicts_least_recently_used_and_refuses_too_large(hooked_device, tmp_path):
     """IRIS_RESIDENT_BUDGET_MB (test hook) caps what the copies may hold, standing in for a full
     device: with room for one of two 160-MB files, walking the second evicts the first (least
