@@ -339,6 +339,47 @@ def test_concurrent_walk_and_resolver_host_forms(device, tmp_path):
     del recs
 
 
+def test_mpc_request_through_files(device, tmp_path):
+    """The reference's MPC request end to end through its unchanged call sites (tools/mpc_request.py
+    at test size): `prepare` writes three share files and a masks file (src/main.rs:333-361), each
+    participant walks its mapped share file in 20k batch_process calls with a fresh engine
+    (:386-431), the resolver loads the masks file and aggregates the participants' host rows with the
+    fused step (iris_resolver_search_masks_host, :455-621); the answer equals the plaintext search
+    and the oracle's."""
+    n, k, rot = 45_001, 30_000, -5
+    with ih.Database(device, ih.KIND_TEMPLATES, n) as tdb:
+        tdb.generate(n, 77)
+        templ = tdb.read(0, n)
+        q = templ[k].copy()
+        qp = ih.Bits(q[:200]).rotated(rot).limbs.copy()
+        qp[9] ^= np.uint64(0x0F0F0F0F)
+        query = np.concatenate([qp, ih.Bits(q[200:]).rotated(rot).limbs])
+        with ih.TemplateEngine(device, query) as te:
+            plain = te.search(tdb)
+        sdbs = [ih.Database(device, ih.KIND_SHARES, n) for _ in range(3)]
+        mdb = ih.Database(device, ih.KIND_MASKS, n)
+        ih.prepare_shares(tdb, sdbs, mdb, key=bytes(range(32)))
+        for i, sdb in enumerate(sdbs):
+            sdb.save_file(tmp_path / f"db.share-{i}")
+            sdb.close()
+        mdb.save_file(tmp_path / "db.masks")
+        mdb.close()
+    best, idx = oc.argmin(oc.template_distances(query, templ))
+    assert plain.index == idx == k
+    shares = [mapped(tmp_path / f"db.share-{i}", ih.KIND_SHARES, n) for i in range(3)]
+    enc_q = ih.encode(ih.Template.from_array(query))
+    rows = []
+    for i in range(3):
+        with ih.DistanceEngine(device, enc_q) as e:
+            rows.append(walk(e, shares[i]))
+    with ih.Database(device, ih.KIND_MASKS, n) as rdb, ih.MasksEngine(device, query[200:]) as me:
+        assert rdb.load_file(tmp_path / "db.masks") == n
+        m = me.resolve(rdb, rows)
+    assert m.index == plain.index == k and m.rotation == plain.rotation
+    assert np.float64(m.distance).view(np.uint64) == np.float64(best).view(np.uint64)
+    del shares
+
+
 def test_budget_evicts_least_recently_used_and_refuses_too_large(hooked_device, tmp_path):
     """IRIS_RESIDENT_BUDGET_MB (test hook) caps what the copies may hold, standing in for a full
     device: with room for one of two 160-MB files, walking the second evicts the first (least
