@@ -4,6 +4,7 @@
 #   prof    rocprofv3 kernel stats of the default bench line
 #   pmc     HBM counters of the default bench line (tools/pmc_traffic.sh's passes, into gpurun_out/pmc)
 #   walks:KIND  tools/walk_calls.py KIND (per-call times of chunk walks, mapped file and attached)
+#   mpc:N   tools/mpc_request.py N (one MPC request end to end over N templates)
 #   any other STEP is a bench line named in the table below
 # Output under gpurun_out/TAG; every GPU step has its own time limit and the script stops at
 # the first failure (no retries).
@@ -47,6 +48,10 @@ for S in "$@"; do
         timeout -k 10 900 python -u -m pytest $F -m gpu -x -v --timeout 300 --timeout-method thread > $O/tests_part.log 2>&1 ||
             { echo "tests rc=$?"; grep -E "FAILED|Error|error|assert" $O/tests_part.log | tail -20; tail -5 $O/tests_part.log; exit 1; }
         tail -1 $O/tests_part.log ;;
+    mpc:*)  # mpc:N -- one MPC request end to end over N templates (tools/mpc_request.py)
+        timeout -k 10 700 python tools/mpc_request.py ${S#mpc:} 3 > $O/mpc_request_${S#mpc:}.log 2>&1 ||
+            { echo "mpc rc=$?"; tail -5 $O/mpc_request_${S#mpc:}.log; exit 1; }
+        tail -1 $O/mpc_request_${S#mpc:}.log ;;
     diag)
         timeout -k 10 300 python tools/resident_diag.py > $O/resident_diag.log 2>&1 || { echo "diag rc=$?"; tail -5 $O/resident_diag.log; exit 1; }
         cat $O/resident_diag.log ;;
